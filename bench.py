@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark of the exact top-k search engine (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3b1|c2]
+
+A "step" is one pass of the hot path over one batch of queries: scan of the
+whole (row-sharded) corpus, fused per-GPU top-k, RCCL all-gather of the local
+lists (N > 1), on-device merge. Inputs (corpus and queries) are resident in
+HBM before the timed region; nothing is skipped inside it.
+
+Default workload (config c3 = BASELINE.json configs[2], the only config quoted
+on a 10M x 768 corpus with top-10): 10,000,000 x 768 bf16 synthetic unit rows,
+256-query batches, top-10, inner product. Scaling is strong: the corpus is
+fixed and row-sharded over the N GPUs; value = queries/s of the whole job.
+
+Prints ONE JSON line on rank 0 (driver contract), with "roofline" for the
+dominant kernel (HIP-event durations on the engine's stream) and
+"cpu_baseline" (oracle/ CPU scan timed on this host, rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_DENSE_TFLOPS = 2516.6       # 256 CU x 4096 flop/clk x 2.4 GHz (dense, no sparsity)
+
+CONFIGS = {
+    # name: (rows, dim, dtype, metric, batch, k, description)
+    "c3": (10_000_000, 768, "bf16", "dot", 256, 10,
+           "C3: 10M x 768 bf16 corpus, 256-query batches, exact top-10, inner product"),
+    "c3b1": (10_000_000, 768, "bf16", "dot", 1, 10,
+             "10M x 768 bf16 corpus, single query, exact top-10, inner product (GEMV)"),
+    "c2": (1_000_000, 768, "f32", "cosine", 1, 10,
+           "C2: 1M x 768 fp32 corpus, single query, exact top-10, cosine (GEMV)"),
+}
+METRIC_NAME = "exact top-10 QPS on 10M×768 corpus at 1/2/4/8 GPUs; % of HBM/MFMA peak"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample-queries", type=int, default=32)
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def kernel_roofline(cfg_rows_local, dim, elem, batch, k, t_ms, bound):
+    """Algorithmic work of one scan launch / its measured duration."""
+    bytes_ = cfg_rows_local * dim * elem + batch * dim * elem + batch * k * 12
+    flops = 2.0 * batch * cfg_rows_local * dim
+    t = t_ms / 1e3
+    gbs = bytes_ / t / 1e9
+    tfs = flops / t / 1e12
+    if bound == "mfma":
+        return {"bound": "mfma", "achieved": round(tfs, 2), "peak": BF16_DENSE_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(tfs / BF16_DENSE_TFLOPS, 4),
+                "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                "kernel_ms": round(t_ms, 4), "bytes_per_launch": int(bytes_),
+                "flops_per_launch": int(flops)}
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(t_ms, 4),
+            "bytes_per_launch": int(bytes_)}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_fn, row0):
+    """Times `steps` searches of one batch; returns (max elapsed s over ranks, scan/merge ms)."""
+    import torch.distributed as dist
+
+    q = torch.empty((batch, dim), dtype=torch.float32, device="cuda")
+    eng.generate_vectors(0xC0FFEE, row0, batch, dim, q.data_ptr(), stream_fn())
+    for _ in range(warmup):
+        sharded.search(q, k)
+    torch.cuda.synchronize()
+    eng.timing(reset=True)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = sharded.search(q, k)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    tm = eng.timing(reset=True)
+    return el, tm, out
+
+
+def cpu_baseline(cfg, args, n_full):
+    from oracle import oracle
+
+    rows, dim, dtype, metric, batch, k, _ = cfg
+    bf16 = dtype == "bf16"
+    ns = min(args.cpu_sample_rows, n_full)
+    nq = args.cpu_sample_queries
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    X = oracle.generate_raw(oracle.SEED_CORPUS, 0, ns, dim, bf16)
+    Q = oracle.generate(oracle.SEED_QUERY, 0, nq, dim, bf16=bf16)
+    oracle.cpu_scan(X, bf16, Q[:1], k, threads=threads)  # warm
+    t0 = time.perf_counter()
+    _, _, nth = oracle.cpu_scan(X, bf16, Q, k, threads=threads)
+    el = time.perf_counter() - t0
+    qps_full = nq / (el * (n_full / ns))
+    return {"value": round(qps_full, 3), "unit": "queries/s", "cores": int(nth), "kind": "port",
+            "sample": f"{nq} queries one at a time over the first {ns:,} of {n_full:,} rows "
+                      f"({dtype}, dim {dim}, top-{k}); {el:.2f} s measured, QPS scaled by "
+                      f"{n_full / ns:.2f} to the full corpus",
+            "measured_s": round(el, 3)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist_on = world > 1
+    if dist_on:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from importlib import import_module
+    shard = import_module(pkg.__name__ + ".shard")
+
+    cfg = CONFIGS[args.config]
+    n_full, dim, dtype, metric, batch, k, desc = cfg
+    if args.rows:
+        n_full = args.rows
+    lo, hi = shard.shard_range(n_full, world, rank)
+    eng = pkg.VectorEngine(device=local, timing=True)
+    coll = "bench"
+    eng.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else pkg.METRIC_COSINE,
+                          pkg.DTYPE_BF16 if dtype == "bf16" else pkg.DTYPE_F32, hi - lo, lo)
+    t0 = time.perf_counter()
+    eng.generate(coll, hi - lo, 0x5EED)
+    log(f"[bench] rank {rank}/{world}: rows [{lo}, {hi}) generated in "
+        f"{time.perf_counter() - t0:.2f}s on {torch.cuda.get_device_name(local)}")
+
+    stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    ls, mg = shard.engine_callables(eng, coll, dim, stream_fn)
+    sharded = shard.ShardedSearch(ls, mg)
+
+    el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
+                            stream_fn, 0)
+    elem = 2 if dtype == "bf16" else 4
+    bound = "mfma" if batch > 1 and dtype == "bf16" else "hbm"
+    roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound)
+    roof["traffic"] = pmc_traffic(args.config)
+    roof["merge_ms"] = round(tm["merge_ms"], 4)
+    roof["kernel_launches_timed"] = tm["scan_n"]
+
+    result = {
+        "metric": METRIC_NAME,
+        "value": round(batch * args.steps / el, 2),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
+        "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
+                   "metric": metric, "parallelism": f"row-shard x{world}",
+                   "rows_per_gpu": hi - lo},
+        "roofline": roof,
+    }
+
+    # secondary: the single-query GEMV line on the same resident corpus
+    if not args.no_secondary and batch > 1:
+        el1, tm1, _ = run_phase(eng, sharded, coll, dim, 1, k, max(20, args.steps), 3, dist_on,
+                                stream_fn, 1000)
+        steps1 = max(20, args.steps)
+        r1 = kernel_roofline(hi - lo, dim, elem, 1, k, tm1["scan_ms"], "hbm")
+        r1["merge_ms"] = round(tm1["merge_ms"], 4)
+        result["secondary"] = {"workload": "same corpus, single query (GEMV path)",
+                               "value": round(steps1 / el1, 2), "unit": "queries/s",
+                               "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(cfg, args, n_full)
+        except Exception as e:  # the baseline never decides the run
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    elif rank == 0:
+        result["cpu_baseline"] = None
+
+    # sanity: the last step's results are well-formed (full k, sorted)
+    if rank == 0 and out is not None:
+        s, r, c = pkg.keys_decode(out.cpu().numpy().view(np.uint64))
+        assert int(c.min()) == min(k, n_full), "incomplete result lists"
+        assert np.all(np.diff(s, axis=1) <= 0), "unsorted results"
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist_on:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

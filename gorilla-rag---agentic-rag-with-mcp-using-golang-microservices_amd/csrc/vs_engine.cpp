@@ -1,0 +1,668 @@
+// vs_engine.cpp — host side of the engine: the C-ABI of include/vsearch.h.
+//
+// One vs_engine owns one HIP device, one stream and a set of resident
+// collections (row-major fp32/bf16 matrices in HBM). It replaces the Qdrant
+// server and the gRPC client globals of rag/vector-service/main.go:44-65.
+// All device work of an engine is serialised on its stream; collections are
+// guarded by reader/writer locks (search = reader, upsert = writer), which is
+// what net/http's goroutine-per-request handlers (main.go:77) need.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "../../include/vsearch.h"
+#include "vs_common.h"
+#include "vs_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+int fail_hip(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? VS_ERR_OOM : VS_ERR_DEVICE,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+#define VS_HIP(call, what)                       \
+  do {                                           \
+    hipError_t e_ = (call);                      \
+    if (e_ != hipSuccess) return fail_hip(e_, what); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  // Grows the buffer; the caller has drained the stream that used it.
+  hipError_t ensure(size_t want) {
+    if (want <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t b = std::max(want, (size_t)4096);
+    hipError_t e = hipMalloc(&p, b);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+  template <typename T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+struct Collection {
+  std::string name;
+  uint32_t dim = 0;
+  int metric = VS_METRIC_COSINE;
+  int dtype = VS_DTYPE_F32;
+  uint64_t row_base = 0;
+  void* data = nullptr;  // cap x dim elements
+  uint64_t rows = 0, cap = 0;
+  std::shared_mutex mu;
+  size_t elem() const { return dtype == VS_DTYPE_BF16 ? 2 : 4; }
+  size_t row_bytes() const { return elem() * dim; }
+  ~Collection() {
+    if (data) (void)hipFree(data);
+  }
+};
+
+struct EventPair {
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct vs_engine {
+  int device = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  std::string device_name;
+  std::mutex map_mu;
+  std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
+  std::mutex work_mu;  // scratch buffers + stream
+  DevBuf q_in, q_pre, q_bf16, lists, keys, upsert_vecs, upsert_rows;
+  std::vector<uint64_t> h_keys;
+  // timing
+  std::vector<EventPair> scan_ev, merge_ev;
+  double scan_ms = 0, merge_ms = 0;
+  uint64_t scan_n = 0, merge_n = 0;
+};
+
+namespace {
+
+std::shared_ptr<Collection> find_coll(vs_engine* eng, const char* name) {
+  std::lock_guard<std::mutex> g(eng->map_mu);
+  auto it = eng->colls.find(name ? name : "");
+  return it == eng->colls.end() ? nullptr : it->second;
+}
+
+hipError_t set_dev(vs_engine* eng) { return hipSetDevice(eng->device); }
+
+bool timing_on(vs_engine* eng) { return (eng->flags & VS_FLAG_TIMING) != 0; }
+
+hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
+  if (!timing_on(eng)) return hipSuccess;
+  EventPair p{};
+  hipError_t e = hipEventCreate(&p.a);
+  if (e != hipSuccess) return e;
+  e = hipEventCreate(&p.b);
+  if (e != hipSuccess) return e;
+  v.push_back(p);
+  return hipEventRecord(p.a, eng->stream);
+}
+hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
+  if (!timing_on(eng) || v.empty()) return hipSuccess;
+  return hipEventRecord(v.back().b, eng->stream);
+}
+
+// Grows a collection to hold `need` rows (writer lock held by the caller).
+int grow(vs_engine* eng, Collection& c, uint64_t need) {
+  if (need <= c.cap) return VS_OK;
+  uint64_t ncap = std::max<uint64_t>({need, c.cap + c.cap / 2, 1024});
+  void* nd = nullptr;
+  hipError_t e = hipMalloc(&nd, ncap * c.row_bytes());
+  if (e != hipSuccess) {
+    // exact fit as a last resort
+    ncap = need;
+    e = hipMalloc(&nd, ncap * c.row_bytes());
+    if (e != hipSuccess) return fail_hip(e, "collection grow");
+  }
+  if (c.data && c.rows) {
+    VS_HIP(hipMemcpyAsync(nd, c.data, c.rows * c.row_bytes(), hipMemcpyDeviceToDevice,
+                          eng->stream),
+           "collection grow copy");
+    VS_HIP(hipStreamSynchronize(eng->stream), "collection grow sync");
+  }
+  if (c.data) (void)hipFree(c.data);
+  c.data = nd;
+  c.cap = ncap;
+  return VS_OK;
+}
+
+// Core search on device data. d_q: nq x dim fp32 on this device, ordered on
+// eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
+// reader lock are held by the caller.
+int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
+                uint64_t* d_keys) {
+  const uint32_t dim = c.dim;
+  const bool bf16 = c.dtype == VS_DTYPE_BF16;
+  const bool cosine = c.metric == VS_METRIC_COSINE;
+  if (c.rows == 0) {
+    VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
+    return VS_OK;
+  }
+  if (c.rows >= 0xFFFFFFFFull || c.row_base + c.rows >= 0xFFFFFFFFull)
+    return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
+  const uint32_t n_rows = (uint32_t)c.rows;
+  const uint32_t row_base = (uint32_t)c.row_base;
+
+  // 1. query preprocessing (cosine normalise) -> q_pre (fp32)
+  const size_t qbytes = (size_t)nq * dim * 4;
+  if (eng->q_pre.bytes < qbytes) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->q_pre.ensure(qbytes), "alloc query scratch");
+  }
+  float* qp = eng->q_pre.as<float>();
+  VS_HIP(vsk::launch_preprocess(d_q, nq, dim, cosine, false, qp, nullptr, 0, eng->stream),
+         "query preprocess");
+
+  const bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
+  if (use_mfma) {
+    const uint32_t P = vsk::kMfmaQueries;
+    const uint32_t npass = (nq + P - 1) / P;
+    const uint32_t maxl = vsk::mfma_max_lists(n_rows);
+    const size_t lbytes = (size_t)maxl * P * k * 8;
+    const size_t bbytes = (size_t)P * dim * 2;
+    if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
+      VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
+    }
+    for (uint32_t p = 0; p < npass; ++p) {
+      const uint32_t q0 = p * P;
+      const uint32_t nv = std::min(P, nq - q0);
+      uint16_t* qb = eng->q_bf16.as<uint16_t>();
+      if (nv < P)
+        VS_HIP(hipMemsetAsync(qb + (size_t)nv * dim, 0, (size_t)(P - nv) * dim * 2,
+                              eng->stream),
+               "pad queries");
+      VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
+             "queries to bf16");
+      uint32_t L = 0;
+      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k,
+                              eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+             "mfma scan");
+      VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      // lists [L][P][k]; merge reads the first nv queries of every list set
+      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, (uint64_t)P * k, k, nv, k, k,
+                               d_keys + (size_t)q0 * k, eng->stream),
+             "merge");
+      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+    }
+    return VS_OK;
+  }
+
+  // GEMV path, one query per scan
+  if (bf16)
+    VS_HIP(vsk::launch_round_bf16(qp, (uint64_t)nq * dim, qp, eng->stream), "round query");
+  const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
+  const size_t lbytes = (size_t)maxl * k * 8;
+  if (eng->lists.bytes < lbytes) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
+  }
+  for (uint32_t i = 0; i < nq; ++i) {
+    uint32_t L = 0;
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_gemv(c.data, bf16, dim, n_rows, row_base, qp + (size_t)i * dim, k,
+                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+           "gemv scan");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+    VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
+                             d_keys + (size_t)i * k, eng->stream),
+           "merge");
+    VS_HIP(ev_end(eng, eng->merge_ev), "event");
+  }
+  return VS_OK;
+}
+
+void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
+                 uint64_t* rows, uint32_t* count) {
+  for (uint32_t i = 0; i < nq; ++i) {
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint64_t key = keys[(size_t)i * k + j];
+      if (key == 0) {
+        if (scores) scores[(size_t)i * k + j] = 0.f;
+        if (rows) rows[(size_t)i * k + j] = 0;
+        continue;
+      }
+      ++c;
+      if (scores) scores[(size_t)i * k + j] = vs::key_score(key);
+      if (rows) rows[(size_t)i * k + j] = vs::key_row(key);
+    }
+    if (count) count[i] = c;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vs_last_error(void) { return g_last_error.c_str(); }
+
+int vs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int vs_open(const vs_config* cfg, vs_engine** out) {
+  if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0)
+    return fail(VS_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
+  int dev = cfg ? cfg->device : -1;
+  if (dev < 0) VS_HIP(hipGetDevice(&dev), "hipGetDevice");
+  if (dev >= n) return fail(VS_ERR_INVALID_ARG, "device ordinal out of range");
+  VS_HIP(hipSetDevice(dev), "hipSetDevice");
+  auto eng = std::make_unique<vs_engine>();
+  eng->device = dev;
+  eng->flags = cfg ? cfg->flags : 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
+    eng->device_name = std::string(prop.name) + " " + prop.gcnArchName;
+  VS_HIP(hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking), "stream");
+  vsk::device_cu_count();
+  *out = eng.release();
+  return VS_OK;
+}
+
+void vs_close(vs_engine* eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->device);
+  (void)hipStreamSynchronize(eng->stream);
+  for (auto& p : eng->scan_ev) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto& p : eng->merge_ev) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  eng->colls.clear();
+  (void)hipStreamDestroy(eng->stream);
+  delete eng;
+}
+
+int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim, int metric, int dtype,
+                         uint64_t capacity_hint, uint64_t row_base) {
+  if (!eng || !name || !*name) return fail(VS_ERR_INVALID_ARG, "collection name required");
+  if (dim == 0 || dim > 65536) return fail(VS_ERR_INVALID_ARG, "dim must be in [1, 65536]");
+  if (metric != VS_METRIC_COSINE && metric != VS_METRIC_DOT)
+    return fail(VS_ERR_INVALID_ARG, "unknown metric");
+  if (dtype != VS_DTYPE_F32 && dtype != VS_DTYPE_BF16)
+    return fail(VS_ERR_INVALID_ARG, "unknown dtype");
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  auto c = std::make_shared<Collection>();
+  c->name = name;
+  c->dim = dim;
+  c->metric = metric;
+  c->dtype = dtype;
+  c->row_base = row_base;
+  {
+    std::lock_guard<std::mutex> g(eng->map_mu);
+    if (eng->colls.count(name))
+      return fail(VS_ERR_EXISTS, std::string("collection ") + name + " already exists");
+    eng->colls[name] = c;
+  }
+  if (capacity_hint) {
+    std::unique_lock<std::shared_mutex> wl(c->mu);
+    std::lock_guard<std::mutex> g(eng->work_mu);
+    int rc = grow(eng, *c, capacity_hint);
+    if (rc != VS_OK) {
+      std::lock_guard<std::mutex> g2(eng->map_mu);
+      eng->colls.erase(name);
+      return rc;
+    }
+  }
+  return VS_OK;
+}
+
+int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim, uint64_t* rows,
+                       int* metric, int* dtype) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  auto c = find_coll(eng, name);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (name ? name : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  if (dim) *dim = c->dim;
+  if (rows) *rows = c->rows;
+  if (metric) *metric = c->metric;
+  if (dtype) *dtype = c->dtype;
+  return VS_OK;
+}
+
+int vs_collection_drop(vs_engine* eng, const char* name) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  std::shared_ptr<Collection> c;
+  {
+    std::lock_guard<std::mutex> g(eng->map_mu);
+    auto it = eng->colls.find(name ? name : "");
+    if (it == eng->colls.end())
+      return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (name ? name : "") +
+                                        " not found");
+    c = it->second;
+    eng->colls.erase(it);
+  }
+  std::unique_lock<std::shared_mutex> wl(c->mu);
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  (void)set_dev(eng);
+  (void)hipStreamSynchronize(eng->stream);
+  return VS_OK;  // memory released with the last reference
+}
+
+int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim_in,
+              const uint64_t* rows, const float* vecs) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (n == 0) return VS_OK;
+  if (!rows || !vecs) return fail(VS_ERR_INVALID_ARG, "rows and vecs are required");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  if (dim_in != c->dim)
+    return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
+                                         std::to_string(c->dim) + ", got " + std::to_string(dim_in));
+  std::unique_lock<std::shared_mutex> wl(c->mu);
+  // last occurrence of each row wins
+  std::vector<std::pair<uint64_t, uint64_t>> order(n);  // (row, index)
+  for (uint64_t i = 0; i < n; ++i) order[i] = {rows[i], i};
+  std::stable_sort(order.begin(), order.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<uint64_t> keep_idx;
+  keep_idx.reserve(n);
+  for (uint64_t i = 0; i < n; ++i)
+    if (i + 1 == n || order[i + 1].first != order[i].first) keep_idx.push_back(i);
+  // appended rows must be exactly [rows, rows + m)
+  uint64_t expect = c->rows;
+  for (uint64_t t : keep_idx) {
+    const uint64_t r = order[t].first;
+    if (r >= c->rows) {
+      if (r != expect)
+        return fail(VS_ERR_INVALID_ARG, "upsert would leave a hole: appended rows must be "
+                                        "contiguous from the current row count");
+      ++expect;
+    }
+  }
+  if (expect >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  int rc = grow(eng, *c, expect);
+  if (rc != VS_OK) return rc;
+  const uint64_t m = keep_idx.size();
+  const uint32_t dim = c->dim;
+  // stream in chunks of <= 64 MiB of fp32 vectors
+  const uint64_t per = std::max<uint64_t>(1, (64ull << 20) / ((uint64_t)dim * 4));
+  std::vector<float> hv;
+  std::vector<uint64_t> hr;
+  for (uint64_t o = 0; o < m; o += per) {
+    const uint64_t cnt = std::min(per, m - o);
+    hv.resize(cnt * dim);
+    hr.resize(cnt);
+    for (uint64_t t = 0; t < cnt; ++t) {
+      const auto& pr = order[keep_idx[o + t]];
+      hr[t] = pr.first;
+      std::memcpy(&hv[t * dim], vecs + pr.second * dim, (size_t)dim * 4);
+    }
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->upsert_vecs.ensure(cnt * dim * 4), "alloc upsert scratch");
+    VS_HIP(eng->upsert_rows.ensure(cnt * 8), "alloc upsert scratch");
+    VS_HIP(hipMemcpyAsync(eng->upsert_vecs.p, hv.data(), cnt * dim * 4, hipMemcpyHostToDevice,
+                          eng->stream),
+           "upsert H2D");
+    VS_HIP(hipMemcpyAsync(eng->upsert_rows.p, hr.data(), cnt * 8, hipMemcpyHostToDevice,
+                          eng->stream),
+           "upsert H2D");
+    VS_HIP(vsk::launch_preprocess(eng->upsert_vecs.as<float>(), (uint32_t)cnt, dim,
+                                  c->metric == VS_METRIC_COSINE, c->dtype == VS_DTYPE_BF16,
+                                  c->data, eng->upsert_rows.as<uint64_t>(), 0, eng->stream),
+           "upsert preprocess");
+  }
+  VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");
+  c->rows = expect;
+  return VS_OK;
+}
+
+int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  if (n == 0) return VS_OK;
+  std::unique_lock<std::shared_mutex> wl(c->mu);
+  if (c->rows + n >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  int rc = grow(eng, *c, c->rows + n);
+  if (rc != VS_OK) return rc;
+  VS_HIP(vsk::launch_generate(seed, c->row_base + c->rows, n, c->dim,
+                              c->dtype == VS_DTYPE_BF16, c->data, c->rows, eng->stream),
+         "generate");
+  VS_HIP(hipStreamSynchronize(eng->stream), "generate sync");
+  c->rows += n;
+  return VS_OK;
+}
+
+int vs_generate_vectors(vs_engine* eng, uint64_t seed, uint64_t row0, uint64_t n, uint32_t dim,
+                        float* d_out, void* stream) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (n == 0) return VS_OK;
+  if (!d_out || dim == 0) return fail(VS_ERR_INVALID_ARG, "bad output buffer");
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(vsk::launch_generate(seed, row0, n, dim, false, d_out, 0, (hipStream_t)stream),
+         "generate vectors");
+  return VS_OK;
+}
+
+int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, float* out) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  if (first + n > c->rows || first + n < first)
+    return fail(VS_ERR_INVALID_ARG, "row range out of bounds");
+  if (n == 0) return VS_OK;
+  if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  const size_t count = (size_t)n * c->dim;
+  if (c->dtype == VS_DTYPE_F32) {
+    VS_HIP(hipMemcpyAsync(out, (const char*)c->data + first * c->row_bytes(), count * 4,
+                          hipMemcpyDeviceToHost, eng->stream),
+           "read D2H");
+    VS_HIP(hipStreamSynchronize(eng->stream), "read sync");
+  } else {
+    std::vector<uint16_t> tmp(count);
+    VS_HIP(hipMemcpyAsync(tmp.data(), (const char*)c->data + first * c->row_bytes(), count * 2,
+                          hipMemcpyDeviceToHost, eng->stream),
+           "read D2H");
+    VS_HIP(hipStreamSynchronize(eng->stream), "read sync");
+    for (size_t i = 0; i < count; ++i) out[i] = vs::bf16_to_f32(tmp[i]);
+  }
+  return VS_OK;
+}
+
+int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+              uint32_t dim, uint32_t k, float* out_scores, uint64_t* out_rows,
+              uint32_t* out_count) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (nq == 0) return VS_OK;
+  if (!queries) return fail(VS_ERR_INVALID_ARG, "queries is NULL");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  if (dim != c->dim)
+    return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
+                                         std::to_string(c->dim) + ", got " + std::to_string(dim));
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  const size_t qbytes = (size_t)nq * c->dim * 4;
+  const size_t kbytes = (size_t)nq * k * 8;
+  if (eng->q_in.bytes < qbytes || eng->keys.bytes < kbytes) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->q_in.ensure(qbytes), "alloc query input");
+    VS_HIP(eng->keys.ensure(kbytes), "alloc keys");
+  }
+  VS_HIP(hipMemcpyAsync(eng->q_in.p, queries, qbytes, hipMemcpyHostToDevice, eng->stream),
+         "query H2D");
+  int rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>());
+  if (rc != VS_OK) return rc;
+  eng->h_keys.resize((size_t)nq * k);
+  VS_HIP(hipMemcpyAsync(eng->h_keys.data(), eng->keys.p, kbytes, hipMemcpyDeviceToHost,
+                        eng->stream),
+         "keys D2H");
+  VS_HIP(hipStreamSynchronize(eng->stream), "search sync");
+  decode_host(eng->h_keys.data(), nq, k, out_scores, out_rows, out_count);
+  return VS_OK;
+}
+
+int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uint32_t nq,
+                   uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (nq == 0) return VS_OK;
+  if (!d_queries || !d_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  if (dim != c->dim)
+    return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
+                                         std::to_string(c->dim) + ", got " + std::to_string(dim));
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  hipStream_t cs = (hipStream_t)stream;
+  hipEvent_t ev;
+  VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+  VS_HIP(hipEventRecord(ev, cs), "event record");
+  VS_HIP(hipStreamWaitEvent(eng->stream, ev, 0), "stream wait");
+  int rc = search_core(eng, *c, d_queries, nq, k, d_keys);
+  if (rc == VS_OK) {
+    VS_HIP(hipEventRecord(ev, eng->stream), "event record");
+    VS_HIP(hipStreamWaitEvent(cs, ev, 0), "stream wait");
+  }
+  (void)hipEventDestroy(ev);
+  return rc;
+}
+
+int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
+                  uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (k == 0 || k > vsk::kMaxK || k_in == 0 || n_lists == 0)
+    return fail(VS_ERR_INVALID_ARG, "bad merge shape");
+  if (nq == 0) return VS_OK;
+  if (!d_lists || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  hipStream_t cs = (hipStream_t)stream;
+  // the merge has no scratch of its own: it runs directly on the caller's stream
+  hipError_t e = vsk::launch_merge(d_lists, n_lists, (uint64_t)nq * k_in, k_in, nq, k_in, k,
+                                   d_out_keys, cs);
+  if (e != hipSuccess) return fail_hip(e, "merge");
+  return VS_OK;
+}
+
+int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
+                   float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (nq == 0 || k == 0) return VS_OK;
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  std::vector<uint64_t> h((size_t)nq * k);
+  hipStream_t cs = (hipStream_t)stream;
+  VS_HIP(hipMemcpyAsync(h.data(), d_keys, h.size() * 8, hipMemcpyDeviceToHost, cs),
+         "keys D2H");
+  VS_HIP(hipStreamSynchronize(cs), "decode sync");
+  decode_host(h.data(), nq, k, out_scores, out_rows, out_count);
+  return VS_OK;
+}
+
+int vs_health(vs_engine* eng, char* buf, size_t len) {
+  if (!eng || !buf || len == 0) return fail(VS_ERR_INVALID_ARG, "bad health buffer");
+  size_t freeb = 0, totalb = 0;
+  std::string status = "healthy", err;
+  hipError_t e = hipSetDevice(eng->device);
+  if (e == hipSuccess) e = hipMemGetInfo(&freeb, &totalb);
+  if (e != hipSuccess) {
+    status = "degraded";
+    err = hipGetErrorString(e);
+  }
+  size_t ncoll;
+  {
+    std::lock_guard<std::mutex> g(eng->map_mu);
+    ncoll = eng->colls.size();
+  }
+  int n = std::snprintf(buf, len,
+                        "{\"status\":\"%s\",\"engine\":\"vsearch-hip\",\"device\":%d,"
+                        "\"device_name\":\"%s\",\"hbm_free_bytes\":%zu,\"hbm_total_bytes\":%zu,"
+                        "\"collections\":%zu%s%s%s}",
+                        status.c_str(), eng->device, eng->device_name.c_str(), freeb, totalb,
+                        ncoll, err.empty() ? "" : ",\"error\":\"", err.c_str(),
+                        err.empty() ? "" : "\"");
+  if (n < 0 || (size_t)n >= len) return fail(VS_ERR_INVALID_ARG, "health buffer too small");
+  return e == hipSuccess ? VS_OK : fail(VS_ERR_DEVICE, err);
+}
+
+int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double* merge_ms_avg,
+              uint64_t* merge_count, int reset) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(hipDeviceSynchronize(), "timing sync");
+  auto drain = [](std::vector<EventPair>& v, double& acc, uint64_t& n) {
+    for (auto& p : v) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+        acc += ms;
+        ++n;
+      }
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    v.clear();
+  };
+  drain(eng->scan_ev, eng->scan_ms, eng->scan_n);
+  drain(eng->merge_ev, eng->merge_ms, eng->merge_n);
+  if (scan_ms_avg) *scan_ms_avg = eng->scan_n ? eng->scan_ms / eng->scan_n : 0.0;
+  if (scan_count) *scan_count = eng->scan_n;
+  if (merge_ms_avg) *merge_ms_avg = eng->merge_n ? eng->merge_ms / eng->merge_n : 0.0;
+  if (merge_count) *merge_count = eng->merge_n;
+  if (reset) {
+    eng->scan_ms = eng->merge_ms = 0;
+    eng->scan_n = eng->merge_n = 0;
+  }
+  return VS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// vs_kernels.h — host-side launchers for the HIP kernels in vs_kernels.hip.
+// Internal to the library; the public boundary is include/vsearch.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vsk {
+
+// Queries handled by one launch of the MFMA scan (8 waves x 32 queries).
+constexpr uint32_t kMfmaQueries = 256;
+// Largest k the MFMA scan keeps in LDS; larger k uses the GEMV scan.
+constexpr uint32_t kMfmaMaxK = 16;
+// Largest k any scan supports (GEMV register lists: 16 entries per lane).
+constexpr uint32_t kMaxK = 1024;
+
+// Preprocess n fp32 vectors (n x dim, device) and store them as the
+// collection dtype into dst rows: dst_rows[i] if non-null, else dst0 + i.
+hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
+                             bool cosine, bool bf16, void* dst,
+                             const uint64_t* dst_rows, uint64_t dst0,
+                             hipStream_t st);
+
+// Generate n synthetic unit rows with global numbers grow0 .. grow0+n-1 and
+// store them into dst rows dst0 .. (bf16 or fp32), or as fp32 when f32_out.
+hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
+                           uint32_t dim, bool bf16, void* dst, uint64_t dst0,
+                           hipStream_t st);
+
+// Single-query scan (GEMV) with per-wave register top-k. Writes one sorted
+// key list of length k per workgroup to out[nlists][k]; returns nlists.
+// `q` is dim fp32 on the device (already preprocessed / bf16-rounded).
+hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                       uint32_t row_base, const float* q, uint32_t k,
+                       uint64_t* out, uint32_t max_lists, uint32_t* nlists,
+                       hipStream_t st);
+// Upper bound on the lists launch_gemv writes for these sizes.
+uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
+
+// Batched bf16 scan on MFMA with fused top-k. Q is kMfmaQueries x dim bf16
+// (zero-padded), nq_valid <= kMfmaQueries. Writes out[nlists][kMfmaQueries][k].
+bool mfma_supported(uint32_t dim);
+hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows,
+                       uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+                       uint32_t k, uint64_t* out, uint32_t max_lists,
+                       uint32_t* nlists, hipStream_t st);
+uint32_t mfma_max_lists(uint32_t n_rows);
+
+// Merge L sorted key lists per query -> out [nq][k] (global top-k by key).
+// List l of query q starts at lists[l * lstride + q * qstride], kin entries.
+hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
+                        uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k,
+                        uint64_t* out, hipStream_t st);
+
+// Convert fp32 queries (nq x dim) to bf16 (after preprocessing).
+hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out,
+                          hipStream_t st);
+// fp32 -> fp32 with bf16 rounding (values exactly representable in bf16).
+hipError_t launch_round_bf16(const float* in, uint64_t n, float* out,
+                             hipStream_t st);
+
+int device_cu_count();
+
+}  // namespace vsk

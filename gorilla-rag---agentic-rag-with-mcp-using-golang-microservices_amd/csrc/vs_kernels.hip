@@ -1,0 +1,814 @@
+// vs_kernels.hip — CDNA4 (gfx950) kernels of the exact top-k search engine.
+//
+// The reference's hot loop is Qdrant's exact scan behind Points.Search
+// (rag/vector-service/main.go:249-254): score every stored row against the
+// preprocessed query and keep the best `limit`. Here that loop is:
+//   * gemv_topk_kernel  — one query, HBM-bound stream of the resident matrix
+//                         (16-B coalesced loads, wave reduction, per-wave
+//                         register top-k list), fp32 or bf16 rows;
+//   * mfma_topk_kernel  — up to 256 queries per launch, bf16 rows streamed
+//                         once through an LDS ring by LDS-DMA, scores on
+//                         v_mfma_f32_32x32x16_bf16 with the query block
+//                         resident in registers, fused per-query top-k in LDS;
+//   * merge_keys_kernel — global top-k over per-workgroup / per-shard lists.
+// Store side (upsert, Qdrant cosine preprocess) and the synthetic generator
+// are here too. Numerics contract: include/vsearch.h and DESIGN.md.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "vs_common.h"
+#include "vs_kernels.h"
+
+namespace vsk {
+
+using vs::make_key;
+using vs::key_score;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int ln) {
+  uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, ln);
+  uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), ln);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
+  uint32_t lo = __shfl_up((unsigned)(uint32_t)v, 1, 64);
+  uint32_t hi = __shfl_up((unsigned)(uint32_t)(v >> 32), 1, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Sorted (descending) key list of up to 64*KPL entries distributed over the
+// lanes of one wave: entry i*64 + lane lives in e[i] of that lane. All lanes
+// call insert() with the same key (wave-uniform), so the list stays uniform.
+template <int KPL>
+struct WaveList {
+  uint64_t e[KPL];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) e[i] = 0;
+  }
+  __device__ __forceinline__ uint64_t kth(uint32_t k) const {
+    const uint32_t idx = k - 1, blk = idx >> 6;
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i)
+      if ((uint32_t)i == blk) v = e[i];
+    return readlane64(v, (int)(idx & 63));
+  }
+  __device__ __forceinline__ void insert(uint64_t x, uint32_t k, int lane) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const bool gt = ((uint32_t)(i * 64 + lane) < k) && (e[i] > x);
+      pos += (uint32_t)__popcll(__ballot(gt));
+    }
+    uint64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      uint64_t up = shfl_up64(e[i]);
+      const uint64_t last = readlane64(e[i], 63);
+      if (lane == 0) up = carry;
+      carry = last;
+      const uint32_t idx = (uint32_t)(i * 64 + lane);
+      const uint64_t nv = idx < pos ? e[i] : (idx == pos ? x : up);
+      e[i] = idx < k ? nv : 0;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// store side: Qdrant cosine preprocess + dtype conversion
+// ---------------------------------------------------------------------------
+// One wave per vector. The squared norm is accumulated in fp64 in a fixed
+// order (lane l sums elements l, l+64, ... sequentially; then an xor
+// butterfly), so the result is bit-reproducible and the oracle restates it.
+template <bool BF16>
+__global__ __launch_bounds__(256) void preprocess_kernel(
+    const float* __restrict__ in, uint32_t n, uint32_t dim, int cosine,
+    void* __restrict__ dst, const uint64_t* __restrict__ dst_rows, uint64_t dst0) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const float* x = in + (size_t)i * dim;
+  double s = 0.0;
+  for (uint32_t d = lane; d < dim; d += 64) {
+    const double v = (double)x[d];
+    s = s + v * v;
+  }
+  s = wave_sum_f64(s);
+  const bool keep = !cosine || vs::cosine_keep(s);
+  const double nrm = sqrt(s);
+  const uint64_t row = dst_rows ? dst_rows[i] : dst0 + i;
+  for (uint32_t d = lane; d < dim; d += 64) {
+    const float v = x[d];
+    const float y = keep ? v : (float)((double)v / nrm);
+    if (BF16)
+      ((uint16_t*)dst)[row * dim + d] = vs::f32_to_bf16(y);
+    else
+      ((float*)dst)[row * dim + d] = y;
+  }
+}
+
+hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
+                             bool cosine, bool bf16, void* dst,
+                             const uint64_t* dst_rows, uint64_t dst0,
+                             hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((n + 3) / 4), block(256);
+  if (bf16)
+    hipLaunchKernelGGL(preprocess_kernel<true>, grid, block, 0, st, in, n, dim,
+                       (int)cosine, dst, dst_rows, dst0);
+  else
+    hipLaunchKernelGGL(preprocess_kernel<false>, grid, block, 0, st, in, n, dim,
+                       (int)cosine, dst, dst_rows, dst0);
+  return hipGetLastError();
+}
+
+// Synthetic unit rows: x_d = m_d / sqrt(sum m^2) with m_d the Irwin-Hall
+// integers of vs::gen_int; the integer sum is exact and order-free, the
+// division and sqrt are correctly rounded fp64 ops, so host and device agree.
+template <bool BF16>
+__global__ __launch_bounds__(256) void generate_kernel(uint64_t seed, uint64_t grow0,
+                                                       uint64_t n, uint32_t dim,
+                                                       void* __restrict__ dst,
+                                                       uint64_t dst0) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint64_t rk = vs::gen_row_key(seed, grow0 + i);
+  long long s = 0;
+  for (uint32_t d = lane; d < dim; d += 64) {
+    const long long m = vs::gen_int(rk, d);
+    s += m * m;
+  }
+  s = wave_sum_i64(s);
+  const double nrm = sqrt((double)s);
+  const uint64_t row = dst0 + i;
+  for (uint32_t d = lane; d < dim; d += 64) {
+    const int32_t m = vs::gen_int(rk, d);
+    const float y = s > 0 ? (float)((double)m / nrm) : 0.0f;
+    if (BF16)
+      ((uint16_t*)dst)[row * dim + d] = vs::f32_to_bf16(y);
+    else
+      ((float*)dst)[row * dim + d] = y;
+  }
+}
+
+hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
+                           uint32_t dim, bool bf16, void* dst, uint64_t dst0,
+                           hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t kChunk = 1ull << 24;  // keep gridDim.x well below 2^31
+  for (uint64_t o = 0; o < n; o += kChunk) {
+    const uint64_t m = (n - o < kChunk) ? n - o : kChunk;
+    dim3 grid((unsigned)((m + 3) / 4)), block(256);
+    if (bf16)
+      hipLaunchKernelGGL(generate_kernel<true>, grid, block, 0, st, seed, grow0 + o, m,
+                         dim, dst, dst0 + o);
+    else
+      hipLaunchKernelGGL(generate_kernel<false>, grid, block, 0, st, seed, grow0 + o, m,
+                         dim, dst, dst0 + o);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+__global__ void to_bf16_kernel(const float* __restrict__ in, uint64_t n,
+                               uint16_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vs::f32_to_bf16(in[i]);
+}
+__global__ void round_bf16_kernel(const float* __restrict__ in, uint64_t n,
+                                  float* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vs::bf16_to_f32(vs::f32_to_bf16(in[i]));
+}
+hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     in, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_round_bf16(const float* in, uint64_t n, float* out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(round_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     st, in, n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// single-query scan (GEMV) + per-wave top-k
+// ---------------------------------------------------------------------------
+constexpr int kGemvThreads = 512;
+constexpr int kGemvWaves = kGemvThreads / 64;
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+// Rows of D elements are cut into 16-byte chunks; one wave covers RB whole
+// rows per step with J chunks per lane (RB*CPR == 64*J), so every load is a
+// fully coalesced 1 KiB wave-instruction and each lane's query slice is
+// loop-invariant (kept in registers).
+template <int D, bool BF16>
+struct GemvShape {
+  static constexpr int EPC = BF16 ? 8 : 4;  // elements per 16-B chunk
+  static constexpr int CPR = D / EPC;       // chunks per row
+  static constexpr int RB = 64 / cgcd(CPR, 64);
+  static constexpr int J = RB * CPR / 64;
+  static constexpr size_t RBYTES = (size_t)D * (BF16 ? 2 : 4);
+  static_assert(D % EPC == 0, "row must be a whole number of 16-B chunks");
+};
+
+template <bool BF16>
+__device__ __forceinline__ float chunk_dot(const uint4& c, const float* qv) {
+  if constexpr (BF16) {
+    const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc = fmaf(__builtin_bit_cast(float, w[t] << 16), qv[2 * t], acc);
+      acc = fmaf(__builtin_bit_cast(float, w[t] & 0xFFFF0000u), qv[2 * t + 1], acc);
+    }
+    return acc;
+  } else {
+    float acc = __builtin_bit_cast(float, c.x) * qv[0];
+    acc = fmaf(__builtin_bit_cast(float, c.y), qv[1], acc);
+    acc = fmaf(__builtin_bit_cast(float, c.z), qv[2], acc);
+    acc = fmaf(__builtin_bit_cast(float, c.w), qv[3], acc);
+    return acc;
+  }
+}
+
+// After the scan each wave holds its list; KPL == 1 lists are merged across
+// the workgroup in LDS (one list per workgroup), larger ones are written per
+// wave.
+template <int KPL>
+__device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint32_t k,
+                                          int lane, int w, uint64_t* __restrict__ out) {
+  if constexpr (KPL == 1) {
+    __shared__ uint64_t sm[kGemvWaves][64];
+    sm[w][lane] = L.e[0];
+    __syncthreads();
+    if (w == 0) {
+      for (int ow = 1; ow < kGemvWaves; ++ow) {
+        for (uint32_t j = 0; j < k; ++j) {
+          const uint64_t x = sm[ow][j];  // uniform LDS broadcast
+          if (x <= theta) break;         // lists are sorted: the rest cannot enter
+          L.insert(x, k, lane);
+          theta = L.kth(k);
+        }
+      }
+      if ((uint32_t)lane < k) out[(size_t)blockIdx.x * k + lane] = L.e[0];
+    }
+  } else {
+    const size_t li = (size_t)blockIdx.x * kGemvWaves + w;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const uint32_t idx = (uint32_t)(i * 64 + lane);
+      if (idx < k) out[li * k + idx] = L.e[i];
+    }
+  }
+}
+
+template <int D, bool BF16, int KPL>
+__global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
+    const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
+    const float* __restrict__ q, uint32_t k, uint32_t rows_per_wave,
+    uint64_t* __restrict__ out) {
+  using S = GemvShape<D, BF16>;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
+  const uint64_t lo64 = gw * rows_per_wave;
+  const uint32_t lo = lo64 < n_rows ? (uint32_t)lo64 : n_rows;
+  const uint32_t hi = (uint64_t)lo + rows_per_wave < n_rows ? lo + rows_per_wave : n_rows;
+
+  int rowsel[S::J];
+  int coff[S::J];  // chunk index within its row
+  float qv[S::J][S::EPC];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) {
+    const int c = lane + 64 * j;
+    rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
+    coff[j] = c % S::CPR;
+#pragma unroll
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = q[coff[j] * S::EPC + e];
+  }
+
+  WaveList<KPL> L;
+  L.init();
+  uint64_t theta = 0;
+  const char* X = (const char*)Xv;
+
+  if (lo < hi) {
+    uint4 cur[S::J], nxt[S::J];
+    auto load = [&](uint4* dst, uint32_t r0) {
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        uint32_t row = r0 + rowsel[j];
+        row = row < hi ? row : hi - 1;
+        dst[j] = *(const uint4*)(X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16);
+      }
+    };
+    load(cur, lo);
+    for (uint32_t r = lo; r < hi; r += S::RB) {
+      load(nxt, r + S::RB < hi ? r + S::RB : r);
+      float p[S::RB];
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) p[b] = 0.f;
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        const float d = chunk_dot<BF16>(cur[j], qv[j]);
+        if constexpr (S::RB == 1) {
+          p[0] += d;
+        } else {
+#pragma unroll
+          for (int b = 0; b < S::RB; ++b) p[b] += (rowsel[j] == b) ? d : 0.f;
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) {
+        const float s = wave_sum(p[b]);
+        const uint32_t row = r + b;
+        if (row < hi) {
+          const uint64_t key = make_key(s, row_base + row);
+          if (key > theta) {
+            L.insert(key, k, lane);
+            theta = L.kth(k);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) cur[j] = nxt[j];
+    }
+  }
+  gemv_emit<KPL>(L, theta, k, lane, w, out);
+}
+
+// Any dimension: one row per wave step, lane-strided scalar loads.
+template <bool BF16, int KPL>
+__global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
+    const void* __restrict__ Xv, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+    const float* __restrict__ q, uint32_t k, uint32_t rows_per_wave,
+    uint64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
+  const uint64_t lo64 = gw * rows_per_wave;
+  const uint32_t lo = lo64 < n_rows ? (uint32_t)lo64 : n_rows;
+  const uint32_t hi = (uint64_t)lo + rows_per_wave < n_rows ? lo + rows_per_wave : n_rows;
+  WaveList<KPL> L;
+  L.init();
+  uint64_t theta = 0;
+  for (uint32_t r = lo; r < hi; ++r) {
+    float p = 0.f;
+    for (uint32_t d = lane; d < dim; d += 64) {
+      const float x = BF16 ? vs::bf16_to_f32(((const uint16_t*)Xv)[(size_t)r * dim + d])
+                           : ((const float*)Xv)[(size_t)r * dim + d];
+      p = fmaf(x, q[d], p);
+    }
+    const float s = wave_sum(p);
+    const uint64_t key = make_key(s, row_base + r);
+    if (key > theta) {
+      L.insert(key, k, lane);
+      theta = L.kth(k);
+    }
+  }
+  gemv_emit<KPL>(L, theta, k, lane, w, out);
+}
+
+static int g_cu_count = 0;
+int device_cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  g_cu_count = cus;
+  return cus;
+}
+
+static int gemv_kpl(uint32_t k) { return k <= 64 ? 1 : (k <= 128 ? 2 : 16); }
+
+struct GemvGrid {
+  uint32_t nwg, rows_per_wave;
+};
+static GemvGrid gemv_grid(uint32_t n_rows, int rb) {
+  const int cus = g_cu_count ? g_cu_count : device_cu_count();
+  uint64_t want = (uint64_t)cus * 3;  // 3 x 8 waves per CU
+  const uint64_t by_rows = ((uint64_t)n_rows + kGemvWaves * 64 - 1) / (kGemvWaves * 64);
+  if (want > by_rows) want = by_rows;
+  if (want < 1) want = 1;
+  const uint64_t waves = want * kGemvWaves;
+  uint64_t rpw = ((uint64_t)n_rows + waves - 1) / waves;
+  rpw = (rpw + rb - 1) / rb * rb;
+  if (rpw == 0) rpw = rb;
+  const uint64_t nwg = (((uint64_t)n_rows + rpw - 1) / rpw + kGemvWaves - 1) / kGemvWaves;
+  return GemvGrid{(uint32_t)(nwg ? nwg : 1), (uint32_t)rpw};
+}
+
+uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k) {
+  (void)dim;
+  (void)bf16;
+  GemvGrid g = gemv_grid(n_rows, 1);
+  // rb > 1 only lowers the workgroup count; rb == 1 is the upper bound.
+  const uint32_t per = gemv_kpl(k) == 1 ? 1 : kGemvWaves;
+  return g.nwg * per;
+}
+
+template <int D, bool BF16>
+static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row_base,
+                                    const float* q, uint32_t k, uint64_t* out,
+                                    uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+  using S = GemvShape<D, BF16>;
+  GemvGrid g = gemv_grid(n_rows, S::RB);
+  const int kpl = gemv_kpl(k);
+  const uint32_t lists = g.nwg * (kpl == 1 ? 1 : kGemvWaves);
+  if (lists > max_lists) return hipErrorInvalidValue;
+  *nlists = lists;
+  dim3 grid(g.nwg), block(kGemvThreads);
+  if (kpl == 1)
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1>), grid, block, 0, st, X, n_rows,
+                       row_base, q, k, g.rows_per_wave, out);
+  else if (kpl == 2)
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 2>), grid, block, 0, st, X, n_rows,
+                       row_base, q, k, g.rows_per_wave, out);
+  else
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 16>), grid, block, 0, st, X, n_rows,
+                       row_base, q, k, g.rows_per_wave, out);
+  return hipGetLastError();
+}
+
+template <bool BF16>
+static hipError_t gemv_generic(const void* X, uint32_t dim, uint32_t n_rows,
+                               uint32_t row_base, const float* q, uint32_t k,
+                               uint64_t* out, uint32_t max_lists, uint32_t* nlists,
+                               hipStream_t st) {
+  GemvGrid g = gemv_grid(n_rows, 1);
+  const int kpl = gemv_kpl(k);
+  const uint32_t lists = g.nwg * (kpl == 1 ? 1 : kGemvWaves);
+  if (lists > max_lists) return hipErrorInvalidValue;
+  *nlists = lists;
+  dim3 grid(g.nwg), block(kGemvThreads);
+  if (kpl == 1)
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 1>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, k, g.rows_per_wave, out);
+  else if (kpl == 2)
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 2>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, k, g.rows_per_wave, out);
+  else
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 16>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, k, g.rows_per_wave, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                       uint32_t row_base, const float* q, uint32_t k, uint64_t* out,
+                       uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+  if (k == 0 || k > kMaxK || n_rows == 0) return hipErrorInvalidValue;
+#define VS_GEMV_CASE(DD)                                                              \
+  case DD:                                                                            \
+    return bf16 ? gemv_dispatch_kpl<DD, true>(X, n_rows, row_base, q, k, out,         \
+                                              max_lists, nlists, st)                  \
+                : gemv_dispatch_kpl<DD, false>(X, n_rows, row_base, q, k, out,        \
+                                               max_lists, nlists, st);
+  switch (dim) {
+    VS_GEMV_CASE(128)
+    VS_GEMV_CASE(256)
+    VS_GEMV_CASE(384)
+    VS_GEMV_CASE(512)
+    VS_GEMV_CASE(768)
+    VS_GEMV_CASE(1024)
+    VS_GEMV_CASE(1536)
+    VS_GEMV_CASE(2048)
+    VS_GEMV_CASE(3072)
+    VS_GEMV_CASE(4096)
+    default:
+      return bf16 ? gemv_generic<true>(X, dim, n_rows, row_base, q, k, out, max_lists,
+                                       nlists, st)
+                  : gemv_generic<false>(X, dim, n_rows, row_base, q, k, out, max_lists,
+                                        nlists, st);
+  }
+#undef VS_GEMV_CASE
+}
+
+// ---------------------------------------------------------------------------
+// batched bf16 scan on MFMA + fused top-k
+// ---------------------------------------------------------------------------
+// Workgroup = 8 waves; wave w owns queries [32w, 32w+32) and keeps their
+// B-operand fragments for the whole row (D/16 k-steps x 4 VGPRs) resident in
+// registers. Corpus tiles of 32 rows x D stream HBM -> LDS once per
+// workgroup by global_load_lds (1 KiB pieces = 8 rows x 128 B), double
+// buffered; every wave reads the tile's A fragments with ds_read_b128 and
+// runs D/16 v_mfma_f32_32x32x16_bf16 into one 32x32 accumulator
+// (C[row][query], query = lane & 31). The epilogue filters the 16 scores per
+// lane against the query's current k-th key and inserts survivors into a
+// per-query sorted list in LDS. Scores never reach HBM.
+constexpr int kMfThreads = 512;
+constexpr int kMfLists = (int)kMfmaMaxK * (int)kMfmaQueries;  // LDS list entries
+
+// XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
+// ds_read_b128 lane groups over all 64 banks (conflict-free).
+__device__ __forceinline__ int mf_swz(int ri, int rg) {
+  return ((ri >> 1) & 3) | ((rg & 1) << 2);
+}
+
+template <int D>
+struct MfShape {
+  static constexpr int S = D / 16;         // MFMA k-steps per row
+  static constexpr int S4 = D / 64;        // 128-B pieces per row
+  static constexpr int NBLK = S4 * 4;      // 1-KiB LDS-DMA pieces per tile
+  static constexpr int TILE_BYTES = NBLK * 1024;
+  static constexpr int BPW = NBLK / 8;     // pieces issued per wave per tile
+  static constexpr int LDS_BYTES = 2 * TILE_BYTES + kMfLists * 8;
+  static_assert(D % 128 == 0, "MFMA scan needs D % 128 == 0");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int D>
+__global__ __launch_bounds__(kMfThreads) void mfma_topk_kernel(
+    const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t row_base,
+    uint32_t rows_per_wg, const uint16_t* __restrict__ Q, uint32_t nq_valid, uint32_t k,
+    uint64_t* __restrict__ out) {
+  using S = MfShape<D>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
+  uint64_t* lists = (uint64_t*)(smem + 2 * S::TILE_BYTES);
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const uint32_t ql = (uint32_t)(w * 32 + r);
+  const bool qvalid = ql < nq_valid;
+  const uint32_t wr0 = blockIdx.x * rows_per_wg;
+  const uint32_t wr1 = (uint64_t)wr0 + rows_per_wg < n_rows ? wr0 + rows_per_wg : n_rows;
+  const uint32_t ntiles = (wr1 - wr0 + 31) / 32;
+
+  for (int i = threadIdx.x; i < kMfLists; i += kMfThreads) lists[i] = 0;
+
+  // B operand: Q[query ql][16s + 8h + j], j = 0..7  -> one 16-B load per step.
+  bf16x8_t qf[S::S];
+  {
+    const uint4* qrow = (const uint4*)(Q + (size_t)ql * D);
+#pragma unroll
+    for (int s = 0; s < S::S; ++s) qf[s] = __builtin_bit_cast(bf16x8_t, qrow[2 * s + h]);
+  }
+
+  // LDS-DMA source mapping: piece (s4, rg) holds rows rg*8 .. rg*8+7, bytes
+  // [128*s4, 128*s4+128) of each; lane -> (row lane>>3, position lane&7).
+  const int g_ri = lane >> 3;
+  const int g_p = lane & 7;
+  auto issue = [&](uint32_t t, int slot) {
+    const uint32_t trow0 = wr0 + t * 32;
+#pragma unroll
+    for (int i = 0; i < S::BPW; ++i) {
+      const int b = w + 8 * i;
+      const int s4 = b >> 2, rg = b & 3;
+      uint32_t row = trow0 + rg * 8 + g_ri;
+      row = row < n_rows ? row : n_rows - 1;
+      const int c = g_p ^ mf_swz(g_ri, rg);
+      const uint16_t* src = X + (size_t)row * D + s4 * 64 + c * 8;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src, (lds_ptr_t)(smem + slot * S::TILE_BYTES + (s4 * 4 + rg) * 1024),
+          16, 0, 0);
+    }
+  };
+
+  // A operand read offsets: lane (r, h) reads row r, k-chunk 2u+h of piece s4.
+  int offu[4];
+  {
+    const int rg = r >> 3, ri = r & 7, sw = mf_swz(ri, rg);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) offu[u] = rg * 1024 + ri * 128 + (((2 * u + h) ^ sw) << 4);
+  }
+
+  uint64_t th = 0;        // current k-th key of query ql (0 = list not full)
+  float th_s = -INFINITY; // its score
+
+  if (ntiles > 0) issue(0, 0);
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    __syncthreads();  // tile t landed (each wave drained its own DMA), slot (t+1)&1 free
+    if (t + 1 < ntiles) issue(t + 1, (int)((t + 1) & 1));
+    const unsigned char* base = smem + (t & 1) * S::TILE_BYTES;
+    f32x16_t acc = {};
+#pragma unroll
+    for (int s = 0; s < S::S; ++s) {
+      const uint4 a = *(const uint4*)(base + (s >> 2) * 4096 + offu[s & 3]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), qf[s],
+                                                     acc, 0, 0, 0);
+    }
+    // epilogue: acc[i] = score(row trow0 + (i&3) + 8(i>>2) + 4h, query ql)
+    const uint32_t trow0 = wr0 + t * 32;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (row < wr1) mx = fmaxf(mx, acc[i]);
+    }
+    if (__any(qvalid && mx >= th_s)) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const bool p = qvalid && row < wr1 && acc[i] >= th_s;
+        if (__any(p)) {
+          for (int hh = 0; hh < 2; ++hh) {
+            if (p && h == hh) {
+              const uint64_t key = make_key(acc[i], row_base + row);
+              if (key > lists[(k - 1) * kMfmaQueries + ql]) {
+                int j = (int)k - 1;
+                while (j > 0) {
+                  const uint64_t prev = lists[(j - 1) * kMfmaQueries + ql];
+                  if (prev >= key) break;
+                  lists[j * kMfmaQueries + ql] = prev;
+                  --j;
+                }
+                lists[j * kMfmaQueries + ql] = key;
+              }
+            }
+          }
+          th = lists[(k - 1) * kMfmaQueries + ql];
+          th_s = th ? key_score(th) : -INFINITY;
+        }
+      }
+    }
+  }
+  // each wave owns its queries' lists: no barrier needed before the write-out
+  for (uint32_t j = h; j < k; j += 2)
+    out[((size_t)blockIdx.x * kMfmaQueries + ql) * k + j] = lists[j * kMfmaQueries + ql];
+}
+
+bool mfma_supported(uint32_t dim) { return dim == 768 || dim == 512 || dim == 384 || dim == 256; }
+
+static void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg) {
+  const int cus = g_cu_count ? g_cu_count : device_cu_count();
+  uint64_t want = (uint64_t)cus;
+  const uint64_t tiles = ((uint64_t)n_rows + 31) / 32;
+  if (want > tiles) want = tiles;
+  if (want < 1) want = 1;
+  uint64_t rpw = (((uint64_t)n_rows + want - 1) / want + 31) / 32 * 32;
+  if (rpw == 0) rpw = 32;
+  *rows_per_wg = (uint32_t)rpw;
+  *nwg = (uint32_t)(((uint64_t)n_rows + rpw - 1) / rpw);
+  if (*nwg == 0) *nwg = 1;
+}
+
+uint32_t mfma_max_lists(uint32_t n_rows) {
+  uint32_t nwg, rpw;
+  mfma_grid(n_rows, &nwg, &rpw);
+  return nwg;
+}
+
+hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                       const uint16_t* Q, uint32_t nq_valid, uint32_t k, uint64_t* out,
+                       uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+  if (k == 0 || k > kMfmaMaxK || n_rows == 0 || nq_valid == 0 || nq_valid > kMfmaQueries)
+    return hipErrorInvalidValue;
+  uint32_t nwg, rpw;
+  mfma_grid(n_rows, &nwg, &rpw);
+  if (nwg > max_lists) return hipErrorInvalidValue;
+  *nlists = nwg;
+  dim3 grid(nwg), block(kMfThreads);
+  switch (dim) {
+    case 768:
+      hipLaunchKernelGGL(mfma_topk_kernel<768>, grid, block, 0, st, X, n_rows, row_base, rpw,
+                         Q, nq_valid, k, out);
+      break;
+    case 512:
+      hipLaunchKernelGGL(mfma_topk_kernel<512>, grid, block, 0, st, X, n_rows, row_base, rpw,
+                         Q, nq_valid, k, out);
+      break;
+    case 384:
+      hipLaunchKernelGGL(mfma_topk_kernel<384>, grid, block, 0, st, X, n_rows, row_base, rpw,
+                         Q, nq_valid, k, out);
+      break;
+    case 256:
+      hipLaunchKernelGGL(mfma_topk_kernel<256>, grid, block, 0, st, X, n_rows, row_base, rpw,
+                         Q, nq_valid, k, out);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// merge: global top-k over L sorted lists per query
+// ---------------------------------------------------------------------------
+// One workgroup per query. Lower bound: the k-th entry of any full list is
+// <= the global k-th key, so only keys >= max_l list_l[k-1] can enter. The
+// candidates are streamed in chunks; survivors are appended to an LDS buffer
+// that also holds the running top-k, which is re-sorted (bitonic) only when a
+// chunk added something. Correct for any input; fast when the bound is good.
+constexpr int kMergeThreads = 512;
+constexpr int kMergeCap = 4096;
+
+__device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n_pow2 / 2; i += kMergeThreads) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const uint64_t a = buf[lo], b = buf[hi];
+        if ((a < b) == desc) {
+          buf[lo] = b;
+          buf[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
+    const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
+    uint32_t kin, uint32_t k, uint64_t* __restrict__ out) {
+  __shared__ uint64_t buf[kMergeCap];
+  __shared__ uint64_t red[kMergeThreads / 64];
+  __shared__ uint32_t cnt;
+  const uint32_t q = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+
+  // initial bound (strict filter "key > thr")
+  uint64_t b = 0;
+  if (kin >= k)
+    for (uint32_t l = threadIdx.x; l < L; l += kMergeThreads) {
+      const uint64_t x = lists[l * lstride + q * qstride + (k - 1)];
+      b = x > b ? x : b;
+    }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t o = __shfl_xor(b, m, 64);
+    b = o > b ? o : b;
+  }
+  if (lane == 0) red[w] = b;
+  __syncthreads();
+  uint64_t bound = 0;
+  for (int i = 0; i < kMergeThreads / 64; ++i) bound = red[i] > bound ? red[i] : bound;
+  uint64_t thr = bound ? bound - 1 : 0;  // admit the bound itself
+
+  const uint64_t total = (uint64_t)L * kin;
+  const uint32_t chunk = kMergeCap - k;
+  uint32_t nR = 0;  // running top-k size in buf[0, nR)
+  for (uint64_t base = 0; base < total; base += chunk) {
+    if (threadIdx.x == 0) cnt = nR;
+    __syncthreads();
+    const uint64_t end = base + chunk < total ? base + chunk : total;
+    for (uint64_t i = base + threadIdx.x; i < end; i += kMergeThreads) {
+      const uint32_t l = (uint32_t)(i / kin), j = (uint32_t)(i - (uint64_t)l * kin);
+      const uint64_t x = lists[l * lstride + q * qstride + j];
+      if (x > thr) {
+        const uint32_t idx = atomicAdd(&cnt, 1u);
+        buf[idx] = x;
+      }
+    }
+    __syncthreads();
+    const uint32_t c = cnt;
+    if (c > nR) {
+      int p2 = 1;
+      while ((uint32_t)p2 < c) p2 <<= 1;
+      for (int i = (int)c + threadIdx.x; i < p2; i += kMergeThreads) buf[i] = 0;
+      __syncthreads();
+      bitonic_sort_desc(buf, p2);
+      nR = c < k ? c : k;
+      if (nR == k) {
+        const uint64_t kth = buf[k - 1];
+        thr = kth > thr ? kth : thr;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads)
+    out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
+}
+
+hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
+                        uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out,
+                        hipStream_t st) {
+  if (k == 0 || k > kMaxK || nq == 0 || L == 0 || kin == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_keys_kernel, dim3(nq), dim3(kMergeThreads), 0, st, lists, L,
+                     lstride, qstride, kin, k, out);
+  return hipGetLastError();
+}
+
+}  // namespace vsk

@@ -1,0 +1,242 @@
+"""ctypes binding of the engine's C-ABI (include/vsearch.h).
+
+This is the Python counterpart of the cgo package shown in INTEGRATION.md:
+the same entry points, the same ownership rules (caller-owned buffers, no
+retained pointers), and errors surfaced as exceptions carrying the
+``vs_status`` code and ``vs_last_error()`` text.
+
+There is no CPU fallback anywhere in this module: when the HIP library is
+missing or no GPU is visible, the calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libvsearch.so")
+
+VS_OK = 0
+VS_ERR_INVALID_ARG = -1
+VS_ERR_NOT_FOUND = -2
+VS_ERR_DIM_MISMATCH = -3
+VS_ERR_OOM = -4
+VS_ERR_DEVICE = -5
+VS_ERR_EXISTS = -6
+VS_ERR_INTERNAL = -7
+
+METRIC_COSINE = 0
+METRIC_DOT = 1
+DTYPE_F32 = 0
+DTYPE_BF16 = 1
+FLAG_TIMING = 1
+
+# Every function include/vsearch.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "vs_open", "vs_close", "vs_device_count", "vs_collection_create",
+    "vs_collection_info", "vs_collection_drop", "vs_upsert", "vs_generate",
+    "vs_generate_vectors",
+    "vs_read_rows", "vs_search", "vs_search_keys", "vs_merge_keys",
+    "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
+)
+
+
+class VSError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vsearch error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads libvsearch.so (built by __graft_entry__.build()). Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build the HIP library first "
+                          "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(path)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    cp = ctypes.c_char_p
+    sig = {
+        "vs_open": ([ctypes.POINTER(_Config), ctypes.POINTER(vp)], i32),
+        "vs_close": ([vp], None),
+        "vs_device_count": ([], i32),
+        "vs_collection_create": ([vp, cp, u32, i32, i32, u64, u64], i32),
+        "vs_collection_info": ([vp, cp, vp, vp, vp, vp], i32),
+        "vs_collection_drop": ([vp, cp], i32),
+        "vs_upsert": ([vp, cp, u64, u32, vp, vp], i32),
+        "vs_generate": ([vp, cp, u64, u64], i32),
+        "vs_generate_vectors": ([vp, u64, u64, u64, u32, vp, vp], i32),
+        "vs_read_rows": ([vp, cp, u64, u64, vp], i32),
+        "vs_search": ([vp, cp, vp, u32, u32, u32, vp, vp, vp], i32),
+        "vs_search_keys": ([vp, cp, vp, u32, u32, u32, vp, vp], i32),
+        "vs_merge_keys": ([vp, vp, u32, u32, u32, u32, vp, vp], i32),
+        "vs_decode_keys": ([vp, vp, u32, u32, vp, vp, vp, vp], i32),
+        "vs_health": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
+        "vs_last_error": ([], ctypes.c_char_p),
+        "vs_timing": ([vp, vp, vp, vp, vp, i32], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(rc: int):
+    if rc != VS_OK:
+        msg = _lib.vs_last_error().decode("utf-8", "replace")
+        raise VSError(rc, msg)
+
+
+def device_count() -> int:
+    return int(load_library().vs_device_count())
+
+
+# key helpers (include/vsearch.h "Result key layout")
+def keys_decode(keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    keys = np.asarray(keys, np.uint64)
+    o = (keys >> np.uint64(32)).astype(np.uint32)
+    u = np.where(o & 0x80000000, o & 0x7FFFFFFF, ~o).astype(np.uint32)
+    scores = u.view(np.float32).copy()
+    rows = (np.uint32(0xFFFFFFFF) - (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)).astype(np.uint64)
+    valid = keys != 0
+    scores[~valid] = 0
+    rows[~valid] = 0
+    return scores, rows, valid.sum(axis=-1).astype(np.uint32)
+
+
+class VectorEngine:
+    """One engine = one HIP device (vs_open). Mirrors the C-ABI 1:1."""
+
+    def __init__(self, device: int = -1, timing: bool = False):
+        L = load_library()
+        cfg = _Config(device, FLAG_TIMING if timing else 0)
+        h = ctypes.c_void_p()
+        _check(L.vs_open(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.vs_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # collections ---------------------------------------------------------
+    def create_collection(self, name: str, dim: int, metric: int = METRIC_COSINE,
+                          dtype: int = DTYPE_F32, capacity: int = 0, row_base: int = 0):
+        _check(self._L.vs_collection_create(self._h, name.encode(), dim, metric, dtype,
+                                            capacity, row_base))
+
+    def collection_info(self, name: str) -> dict:
+        dim, rows = ctypes.c_uint32(), ctypes.c_uint64()
+        metric, dtype = ctypes.c_int(), ctypes.c_int()
+        _check(self._L.vs_collection_info(self._h, name.encode(), ctypes.byref(dim),
+                                          ctypes.byref(rows), ctypes.byref(metric),
+                                          ctypes.byref(dtype)))
+        return {"dim": dim.value, "rows": rows.value, "metric": metric.value,
+                "dtype": dtype.value}
+
+    def drop_collection(self, name: str):
+        _check(self._L.vs_collection_drop(self._h, name.encode()))
+
+    # store side ----------------------------------------------------------
+    def upsert(self, name: str, rows: Sequence[int], vectors: np.ndarray):
+        v = np.ascontiguousarray(vectors, np.float32)
+        r = np.ascontiguousarray(rows, np.uint64)
+        if v.ndim != 2 or v.shape[0] != r.shape[0]:
+            raise ValueError("vectors must be (n, dim) with one row number per vector")
+        _check(self._L.vs_upsert(self._h, name.encode(), r.shape[0], v.shape[1], _p(r), _p(v)))
+
+    def generate(self, name: str, n: int, seed: int):
+        _check(self._L.vs_generate(self._h, name.encode(), n, seed))
+
+    def generate_vectors(self, seed: int, row0: int, n: int, dim: int, d_out: int,
+                         stream: int = 0):
+        _check(self._L.vs_generate_vectors(self._h, seed, row0, n, dim, ctypes.c_void_p(d_out),
+                                           ctypes.c_void_p(stream)))
+
+    def read_rows(self, name: str, first: int, n: int) -> np.ndarray:
+        dim = self.collection_info(name)["dim"]
+        out = np.empty((n, dim), np.float32)
+        _check(self._L.vs_read_rows(self._h, name.encode(), first, n, _p(out)))
+        return out
+
+    # search side ---------------------------------------------------------
+    def search(self, name: str, queries: np.ndarray, k: int):
+        q = np.ascontiguousarray(queries, np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        scores = np.zeros((nq, k), np.float32)
+        rows = np.zeros((nq, k), np.uint64)
+        count = np.zeros(nq, np.uint32)
+        _check(self._L.vs_search(self._h, name.encode(), _p(q), nq, q.shape[1], k, _p(scores),
+                                 _p(rows), _p(count)))
+        return scores, rows, count
+
+    def search_keys(self, name: str, d_queries: int, nq: int, dim: int, k: int, d_keys: int,
+                    stream: int = 0):
+        _check(self._L.vs_search_keys(self._h, name.encode(), ctypes.c_void_p(d_queries), nq,
+                                      dim, k, ctypes.c_void_p(d_keys), ctypes.c_void_p(stream)))
+
+    def merge_keys(self, d_lists: int, n_lists: int, nq: int, k_in: int, k: int,
+                   d_out: int, stream: int = 0):
+        _check(self._L.vs_merge_keys(self._h, ctypes.c_void_p(d_lists), n_lists, nq, k_in, k,
+                                     ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
+
+    def decode_keys(self, d_keys: int, nq: int, k: int, stream: int = 0):
+        scores = np.zeros((nq, k), np.float32)
+        rows = np.zeros((nq, k), np.uint64)
+        count = np.zeros(nq, np.uint32)
+        _check(self._L.vs_decode_keys(self._h, ctypes.c_void_p(d_keys), nq, k, _p(scores),
+                                      _p(rows), _p(count), ctypes.c_void_p(stream)))
+        return scores, rows, count
+
+    def health(self) -> str:
+        buf = ctypes.create_string_buffer(1024)
+        rc = self._L.vs_health(self._h, buf, len(buf))
+        if rc not in (VS_OK, VS_ERR_DEVICE):
+            _check(rc)
+        return buf.value.decode()
+
+    def timing(self, reset: bool = False) -> dict:
+        sm, mm = ctypes.c_double(), ctypes.c_double()
+        sn, mn = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.vs_timing(self._h, ctypes.byref(sm), ctypes.byref(sn),
+                                 ctypes.byref(mm), ctypes.byref(mn), int(reset)))
+        return {"scan_ms": sm.value, "scan_n": sn.value, "merge_ms": mm.value,
+                "merge_n": mn.value}

@@ -1,0 +1,75 @@
+"""Row-sharded search across GPUs: one process per GPU, one all-gather per batch.
+
+A collection of N rows is cut into contiguous shards: rank p of P owns global
+rows [p*ceil(N/P), min(N, (p+1)*ceil(N/P))). Every rank scans its shard for the
+whole query batch and produces a local top-k key list per query (64-bit keys
+that carry the global row, include/vsearch.h "Result key layout"). The only
+exchange is an all-gather of those lists (RCCL over xGMI via
+``torch.distributed``'s nccl backend); each rank then merges the P lists on its
+own device (vs_merge_keys). Messages are tiny (P x B x k x 8 bytes), so the
+step is latency-bound, not link-bandwidth-bound.
+
+The orchestration below is written against two callables so the CPU tests can
+drive it with gloo and the oracle; the product passes the HIP engine.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+
+def shard_range(n_rows: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous row shard [lo, hi) of `rank`."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    per = -(-n_rows // world)
+    lo = min(n_rows, rank * per)
+    hi = min(n_rows, lo + per)
+    return lo, hi
+
+
+@dataclass
+class ShardedSearch:
+    """Distributed top-k over a row-sharded collection.
+
+    local_search(queries, k) -> keys tensor [nq, k] (int64 bit patterns)
+    merge(gathered [P, nq, k], k) -> keys tensor [nq, k]
+    """
+
+    local_search: Callable
+    merge: Callable
+    group: Optional[object] = None
+
+    def search(self, queries, k: int):
+        import torch
+        import torch.distributed as dist
+
+        local = self.local_search(queries, k)
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return local
+        P = dist.get_world_size(self.group)
+        local = local.contiguous()
+        # concatenated along dim 0 (the form every backend accepts), viewed as [P, nq, k]
+        flat = torch.empty((P * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                           device=local.device)
+        dist.all_gather_into_tensor(flat, local, group=self.group)
+        return self.merge(flat.view((P,) + tuple(local.shape)), k)
+
+
+def engine_callables(engine, collection: str, dim: int, stream_fn: Callable[[], int]):
+    """Binds ShardedSearch to the HIP engine (device tensors, caller's stream)."""
+    import torch
+
+    def local_search(queries, k):
+        nq = queries.shape[0]
+        out = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+        engine.search_keys(collection, queries.data_ptr(), nq, dim, k, out.data_ptr(), stream_fn())
+        return out
+
+    def merge(gathered, k):
+        P, nq, kin = gathered.shape
+        out = torch.empty((nq, k), dtype=torch.int64, device=gathered.device)
+        engine.merge_keys(gathered.data_ptr(), P, nq, kin, k, out.data_ptr(), stream_fn())
+        return out
+
+    return local_search, merge

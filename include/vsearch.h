@@ -1,0 +1,210 @@
+/*
+ * vsearch.h — C-ABI of the MI355X exact top-k vector search engine.
+ *
+ * This is the drop-in boundary for GoRilla-RAG's rag/vector-service. In the
+ * reference, vector-service is a Go HTTP shim over a Qdrant server reached by
+ * gRPC. Its engine calls are exactly five:
+ *
+ *   Collections.Get      rag/vector-service/main.go:91   -> vs_collection_info
+ *   Collections.Create   rag/vector-service/main.go:102  -> vs_collection_create
+ *   Qdrant.HealthCheck   rag/vector-service/main.go:126  -> vs_health
+ *   Points.Upsert        rag/vector-service/main.go:209  -> vs_upsert
+ *   Points.Search        rag/vector-service/main.go:249  -> vs_search
+ *
+ * The gRPC client globals they go through (main.go:44-51, created at
+ * main.go:56-65) are replaced by one engine handle from vs_open.
+ *
+ * Conventions
+ *  - Plain C types only: no HIP, torch or Go types in any signature.
+ *  - Every function returns VS_OK (0) or a negative vs_status. The message of
+ *    the last failure on the calling thread is available from vs_last_error().
+ *  - The caller owns every buffer it passes. The library copies inputs before
+ *    returning and never keeps a caller pointer (this satisfies cgo's pointer
+ *    passing rules for Go slices).
+ *  - The engine deals in dense row numbers only. Point UUIDs and payloads stay
+ *    on the caller's side, exactly as the Go service keeps
+ *    them outside the engine.
+ *  - Thread safety: every entry point may be called concurrently. Collections
+ *    are guarded by reader/writer locks (upsert = writer, search = reader).
+ *
+ * Search semantics (what Qdrant's exact search returns for SearchPoints with
+ * no filter/offset/threshold, rag/vector-service/main.go:249-254):
+ *  - COSINE: both the stored rows and the query are L2-normalised
+ *    ("cosine preprocess"); the score is the dot product of the normalised
+ *    vectors. A vector whose squared norm is < FLT_EPSILON, or within 1e-6 of
+ *    1, is left unchanged.
+ *  - DOT: plain inner product, no preprocessing.
+ *  - Results are ordered by score descending; equal scores are ordered by row
+ *    ascending (the reference leaves tie order unspecified; this fixes it).
+ *  - min(k, rows) results are returned per query.
+ *  - BF16 collections store the preprocessed row rounded to bfloat16
+ *    (round-to-nearest-even); queries are preprocessed in fp32 then rounded
+ *    to bf16; products are accumulated in fp32.
+ */
+#ifndef VSEARCH_H_
+#define VSEARCH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSEARCH_ABI_VERSION 1
+
+typedef struct vs_engine vs_engine;
+
+typedef enum vs_status {
+  VS_OK = 0,
+  VS_ERR_INVALID_ARG = -1,  /* bad argument (maps to HTTP 400 in the service) */
+  VS_ERR_NOT_FOUND = -2,    /* unknown collection (mirrors codes.NotFound, main.go:96) */
+  VS_ERR_DIM_MISMATCH = -3, /* vector length != collection dim */
+  VS_ERR_OOM = -4,          /* device or host allocation failed */
+  VS_ERR_DEVICE = -5,       /* HIP runtime error, or no usable GPU */
+  VS_ERR_EXISTS = -6,       /* collection already exists */
+  VS_ERR_INTERNAL = -7
+} vs_status;
+
+/* Mirrors qdrant.Distance (main.go:108 uses Distance_Cosine). */
+typedef enum vs_metric { VS_METRIC_COSINE = 0, VS_METRIC_DOT = 1 } vs_metric;
+
+/* Storage element type of a collection. */
+typedef enum vs_dtype { VS_DTYPE_F32 = 0, VS_DTYPE_BF16 = 1 } vs_dtype;
+
+typedef struct vs_config {
+  int32_t device; /* HIP device ordinal this engine owns; -1 = current device */
+  uint32_t flags; /* VS_FLAG_* */
+} vs_config;
+
+/* Record HIP events around every scan/merge launch (read with vs_timing). */
+#define VS_FLAG_TIMING 1u
+
+/* ---- engine lifetime ---------------------------------------------------- */
+
+/* Replaces grpc.DialContext + New{Collections,Points,Qdrant}Client
+ * (rag/vector-service/main.go:56-65). Fails with VS_ERR_DEVICE when no HIP
+ * device is usable: there is no CPU fallback. */
+int vs_open(const vs_config* cfg, vs_engine** out);
+void vs_close(vs_engine* eng);
+
+/* Number of visible HIP devices (0 when none). Never fails. */
+int vs_device_count(void);
+
+/* ---- collections ---------------------------------------------------------- */
+
+/* Replaces Collections.Create (main.go:102-112). `capacity_hint` pre-reserves
+ * rows in HBM (0 = grow on demand). `row_base` is the global number of this
+ * collection's row 0: a shard of a row-sharded collection stores global rows
+ * [row_base, row_base + rows). Single-GPU callers pass 0. */
+int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim,
+                         int metric, int dtype, uint64_t capacity_hint,
+                         uint64_t row_base);
+
+/* Replaces Collections.Get (main.go:91). Any out pointer may be NULL. */
+int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim,
+                       uint64_t* rows, int* metric, int* dtype);
+
+/* Frees the collection's device memory. */
+int vs_collection_drop(vs_engine* eng, const char* name);
+
+/* ---- store side ----------------------------------------------------------- */
+
+/* Replaces Points.Upsert(wait=true) (main.go:208-213): writes `n` vectors
+ * (n x dim fp32, row-major; `dim` must equal the collection's, else
+ * VS_ERR_DIM_MISMATCH) into local rows `rows[i]`. A row below the
+ * collection's current row count is overwritten; rows at or above it are
+ * appended and must form exactly the range [rows, rows + m) (no holes).
+ * Duplicate rows in one call: the last occurrence wins. The vectors are
+ * preprocessed on the device (COSINE) and stored as the collection dtype.
+ * Returns after the data is resident. */
+int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim,
+              const uint64_t* rows, const float* vecs);
+
+/* Appends `n` synthetic unit-norm rows generated on the device by the
+ * counter-based generator of DESIGN.md §4 (seed, global row numbers
+ * row_base + rows ... ). Used for benchmarks: no host data is moved. */
+int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed);
+
+/* Writes n synthetic unit vectors (generator rows row0 .. row0+n-1 of `seed`)
+ * as fp32 into the device buffer d_out (n x dim), ordered on `stream`. Used to
+ * build benchmark queries on the device. */
+int vs_generate_vectors(vs_engine* eng, uint64_t seed, uint64_t row0, uint64_t n,
+                        uint32_t dim, float* d_out, void* stream);
+
+/* Copies stored (preprocessed) rows [first, first + n) back to the host as
+ * fp32 (bf16 rows are widened exactly). For verification. */
+int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n,
+                 float* out);
+
+/* ---- search side ---------------------------------------------------------- */
+
+/* Replaces Points.Search (main.go:249-254), batched: `nq` queries of `dim`
+ * fp32 each (`dim` must equal the collection's, else VS_ERR_DIM_MISMATCH).
+ * For query i, out_scores[i*k + j] / out_rows[i*k + j] hold the j-th best (score desc, row asc) for j < out_count[i] = min(k, rows).
+ * Rows are global (row_base added). Blocking. k must be in [1, 1024]. */
+int vs_search(vs_engine* eng, const char* coll, const float* queries,
+              uint32_t nq, uint32_t dim, uint32_t k, float* out_scores,
+              uint64_t* out_rows, uint32_t* out_count);
+
+/* Device-pointer form for sharded callers. `d_queries` (nq x dim fp32) and
+ * `d_keys` (nq x k uint64) are device pointers on this engine's device;
+ * `stream` is a hipStream_t (NULL = the null stream). The work is ordered
+ * after prior work on `stream`, and later work on `stream` sees the result.
+ * Each result is a 64-bit key (see below); unused slots hold 0. */
+int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries,
+                   uint32_t nq, uint32_t dim, uint32_t k, uint64_t* d_keys,
+                   void* stream);
+
+/* Merges `n_lists` per-shard key lists into the global top-k on the device:
+ * d_lists is [n_lists][nq][k_in] (e.g. the result of an all-gather of
+ * vs_search_keys outputs); d_out_keys is [nq][k]. */
+int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists,
+                  uint32_t nq, uint32_t k_in, uint32_t k, uint64_t* d_out_keys,
+                  void* stream);
+
+/* Decodes device keys into host scores/rows/counts (blocking D2H). */
+int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq,
+                   uint32_t k, float* out_scores, uint64_t* out_rows,
+                   uint32_t* out_count, void* stream);
+
+/* Result key layout (host helpers below are the reference definition):
+ *   key = ord(score) << 32 | (0xFFFFFFFF - row)
+ * where ord() maps fp32 bits to an order-preserving uint32 (-0.0 is encoded
+ * as +0.0). Larger key =
+ * better result (higher score; lower row on equal score). 0 = empty slot. */
+static inline uint64_t vs_key_encode(float score, uint32_t row) {
+  union { float f; uint32_t u; } c; c.f = score == 0.0f ? 0.0f : score;
+  uint32_t o = (c.u & 0x80000000u) ? ~c.u : (c.u | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)(0xFFFFFFFFu - row);
+}
+static inline float vs_key_score(uint64_t key) {
+  uint32_t o = (uint32_t)(key >> 32);
+  union { float f; uint32_t u; } c;
+  c.u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+  return c.f;
+}
+static inline uint32_t vs_key_row(uint64_t key) {
+  return 0xFFFFFFFFu - (uint32_t)key;
+}
+
+/* ---- health / errors / timing -------------------------------------------- */
+
+/* Replaces Qdrant.HealthCheck (main.go:126). Writes a NUL-terminated JSON
+ * object {"status":"healthy"|"degraded","engine":"vsearch-hip",...}. */
+int vs_health(vs_engine* eng, char* buf, size_t len);
+
+/* Thread-local message of the last failure ("" if none). */
+const char* vs_last_error(void);
+
+/* With VS_FLAG_TIMING: average device duration (ms) of scan and merge kernel
+ * launches recorded since the last reset, and their counts. Blocks until the
+ * recorded work is done. reset != 0 clears the accumulators afterwards. */
+int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count,
+              double* merge_ms_avg, uint64_t* merge_count, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSEARCH_H_ */

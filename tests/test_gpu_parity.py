@@ -1,0 +1,248 @@
+"""Device parity against the oracle, through the C-ABI (run on an MI355X).
+
+Bar (BASELINE.json north_star): returned rows equal the oracle's except for
+near-ties (< 1e-5 relative), scores within 1e-5 relative of the exact score
+(the spec allows 2e-3 for bf16; the tests hold bf16 to 1e-5 as well, because
+the oracle scores the same bf16 values). Stored rows and generated corpora
+are compared bit for bit.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SCORE_RTOL = 1e-5
+
+
+def _parity(orc, X, Qp, s, r, c, k, row_base=0):
+    s32, s64, rows, cnt = orc.search(X, Qp, k, row_base)
+    resc = orc.rescore(X, Qp, r, c, row_base)
+    bad = orc.check_topk(s, r, c, s64, rows, cnt, resc, SCORE_RTOL)
+    assert not bad, bad[:10]
+    return rows
+
+
+# ------------------------------------------------------------- store side
+@pytest.mark.parametrize("dtype", [0, 1])
+@pytest.mark.parametrize("dim", [768, 1024, 100])
+def test_generate_bit_exact(engine, orc, dtype, dim):
+    name = f"gen_{dtype}_{dim}"
+    engine.create_collection(name, dim, 0, dtype)
+    engine.generate(name, 3000, orc.SEED_CORPUS)
+    engine.generate(name, 1000, orc.SEED_CORPUS)  # appended rows continue the row numbers
+    got = engine.read_rows(name, 0, 4000)
+    ref = orc.generate(orc.SEED_CORPUS, 0, 4000, dim, bf16=bool(dtype))
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    engine.drop_collection(name)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_upsert_preprocess_bit_exact(engine, orc, metric, dtype):
+    rng = np.random.default_rng(11)
+    dim = 768
+    raw = (rng.standard_normal((300, dim)) * rng.uniform(1e-3, 1e3, (300, 1))).astype(np.float32)
+    raw[0] = 0
+    raw[1] = orc.generate(orc.SEED_QUERY, 0, 1, dim)[0]
+    name = f"ups_{metric}_{dtype}"
+    engine.create_collection(name, dim, metric, dtype)
+    engine.upsert(name, np.arange(300), raw)
+    got = engine.read_rows(name, 0, 300)
+    ref = orc.preprocess(raw, metric == 0, bool(dtype))
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    engine.drop_collection(name)
+
+
+def test_upsert_overwrite_and_duplicates(engine, orc):
+    dim = 64
+    engine.create_collection("ow", dim, 0, 0)
+    a = orc.generate(1, 0, 10, dim)
+    engine.upsert("ow", np.arange(10), a)
+    b = orc.generate(2, 0, 3, dim)
+    # overwrite rows 2 and 7; append 10; duplicate row 7: last occurrence wins
+    engine.upsert("ow", [2, 7, 10, 7], np.stack([b[0], b[1], b[2], a[0]]))
+    got = engine.read_rows("ow", 0, 11)
+    exp = np.concatenate([a, b[2:3]])
+    exp[2] = b[0]
+    exp[7] = a[0]
+    assert np.array_equal(got, orc.preprocess(exp, True))
+    assert engine.collection_info("ow")["rows"] == 11
+    with pytest.raises(Exception):
+        engine.upsert("ow", [13], a[:1])  # hole
+    with pytest.raises(Exception):
+        engine.upsert("ow", [0], np.zeros((1, dim + 1), np.float32))  # dim mismatch
+    engine.drop_collection("ow")
+
+
+# ------------------------------------------------------------- search side
+@pytest.fixture(scope="module")
+def corpora(engine, orc):
+    """1 x fp32 and 1 x bf16 collection of 20k x 768 synthetic rows."""
+    out = {}
+    n, dim = 20000, 768
+    for dtype in (0, 1):
+        name = f"c768_{dtype}"
+        engine.create_collection(name, dim, 0, dtype)
+        engine.generate(name, n, orc.SEED_CORPUS)
+        out[dtype] = (name, orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=bool(dtype)))
+    return out
+
+
+@pytest.mark.parametrize("k", [1, 5, 10, 64, 100, 1024])
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_gemv_single_query(engine, orc, corpora, dtype, k):
+    name, X = corpora[dtype]
+    Q = orc.generate(orc.SEED_QUERY, 0, 3, 768)
+    for i in range(3):
+        s, r, c = engine.search(name, Q[i], k)
+        _parity(orc, X, orc.preprocess(Q[i:i + 1], True, bool(dtype)), s, r, c, k)
+
+
+@pytest.mark.parametrize("nq,k", [(2, 10), (33, 1), (256, 10), (300, 16), (64, 5)])
+def test_mfma_batched(engine, orc, corpora, nq, k):
+    name, X = corpora[1]
+    Q = orc.generate(orc.SEED_QUERY, 100, nq, 768)
+    s, r, c = engine.search(name, Q, k)
+    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+
+
+def test_fp32_batched(engine, orc, corpora):
+    name, X = corpora[0]
+    Q = orc.generate(orc.SEED_QUERY, 500, 5, 768)
+    s, r, c = engine.search(name, Q, 10)
+    _parity(orc, X, orc.preprocess(Q, True, False), s, r, c, 10)
+
+
+def test_golden_fixture_on_device(engine, orc):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "search_4096x768.npz"))
+    Q = orc.generate(orc.SEED_QUERY, 0, 32, 768)
+    for tag, dtype in (("f32", 0), ("bf16", 1)):
+        name = f"gold_{tag}"
+        engine.create_collection(name, 768, 0, dtype)
+        engine.generate(name, 4096, orc.SEED_CORPUS)
+        X = orc.generate(orc.SEED_CORPUS, 0, 4096, 768, bf16=bool(dtype))
+        for k in (1, 5, 10, 100):
+            s, r, c = engine.search(name, Q, k)
+            resc = orc.rescore(X, g[f"qpre_{tag}"], r, c)
+            bad = orc.check_topk(s, r, c, g[f"scores64_{tag}_k{k}"], g[f"rows_{tag}_k{k}"],
+                                 np.full(32, k, np.uint32), resc, SCORE_RTOL)
+            assert not bad, (tag, k, bad[:5])
+        engine.drop_collection(name)
+
+
+@pytest.mark.parametrize("dim", [100, 384, 1024, 1536, 256])
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_other_dims(engine, orc, dim, dtype):
+    n = 3001
+    name = f"d{dim}_{dtype}"
+    engine.create_collection(name, dim, 0, dtype)
+    engine.generate(name, n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=bool(dtype))
+    Q = orc.generate(orc.SEED_QUERY, 0, 6, dim)
+    for nq in (1, 6):
+        s, r, c = engine.search(name, Q[:nq], 7)
+        _parity(orc, X, orc.preprocess(Q[:nq], True, bool(dtype)), s, r, c, 7)
+    engine.drop_collection(name)
+
+
+# ------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_edges(engine, orc, dtype):
+    dim = 768
+    name = f"edge_{dtype}"
+    engine.create_collection(name, dim, 0, dtype)
+    q = orc.generate(orc.SEED_QUERY, 0, 2, dim)
+    # empty collection -> no results
+    s, r, c = engine.search(name, q, 5)
+    assert c.tolist() == [0, 0]
+    base = orc.generate(orc.SEED_CORPUS, 0, 7, dim)
+    vecs = np.concatenate([base, base[[3, 3]], np.zeros((1, dim), np.float32)])  # dups + zero row
+    engine.upsert(name, np.arange(10), vecs)
+    X = orc.preprocess(vecs, True, bool(dtype))
+    # k > rows
+    s, r, c = engine.search(name, q, 50)
+    assert c.tolist() == [10, 10]
+    _parity(orc, X, orc.preprocess(q, True, bool(dtype)), s, r, c, 50)
+    # exact duplicates tie -> row ascending; self match first
+    s, r, c = engine.search(name, base[[3, 3]], 3)
+    assert r[0].tolist() == [3, 7, 8] and r[1].tolist() == [3, 7, 8]
+    # zero query: every score 0, rows ascending
+    s, r, c = engine.search(name, np.zeros((1, dim), np.float32), 4)
+    assert r[0].tolist() == [0, 1, 2, 3] and np.all(s == 0)
+    with pytest.raises(Exception):
+        engine.search(name, np.zeros((1, dim - 1), np.float32), 4)
+    with pytest.raises(Exception):
+        engine.search(name, q, 0)
+    with pytest.raises(Exception):
+        engine.search("nope", q, 3)
+    engine.drop_collection(name)
+
+
+def test_dot_metric(engine, orc):
+    dim = 768
+    rng = np.random.default_rng(5)
+    X = (rng.standard_normal((5000, dim)) * rng.uniform(0.1, 3, (5000, 1))).astype(np.float32)
+    q = rng.standard_normal((3, dim)).astype(np.float32)
+    for dtype in (0, 1):
+        name = f"dot_{dtype}"
+        engine.create_collection(name, dim, 1, dtype)
+        engine.upsert(name, np.arange(5000), X)
+        Xs = orc.preprocess(X, False, bool(dtype))
+        for nq in (1, 3):
+            s, r, c = engine.search(name, q[:nq], 10)
+            _parity(orc, Xs, orc.preprocess(q[:nq], False, bool(dtype)), s, r, c, 10)
+        engine.drop_collection(name)
+
+
+# ----------------------------------------------- sharded merge on one device
+def test_sharded_merge_equals_unsharded(engine, orc):
+    torch = pytest.importorskip("torch")
+    dim, n, P, nq, k = 768, 30000, 4, 40, 10
+    per = (n + P - 1) // P
+    names = []
+    for p in range(P):
+        lo, hi = p * per, min(n, (p + 1) * per)
+        nm = f"shard{p}"
+        engine.create_collection(nm, dim, 0, 1, 0, lo)
+        engine.generate(nm, hi - lo, orc.SEED_CORPUS)
+        names.append(nm)
+    dq = torch.empty((nq, dim), dtype=torch.float32, device="cuda")
+    engine.generate_vectors(orc.SEED_QUERY, 0, nq, dim, dq.data_ptr())
+    torch.cuda.synchronize()
+    lists = torch.zeros((P, nq, k), dtype=torch.int64, device="cuda")
+    for p, nm in enumerate(names):
+        engine.search_keys(nm, dq.data_ptr(), nq, dim, k, lists[p].data_ptr())
+    out = torch.zeros((nq, k), dtype=torch.int64, device="cuda")
+    engine.merge_keys(lists.data_ptr(), P, nq, k, k, out.data_ptr())
+    s, r, c = engine.decode_keys(out.data_ptr(), nq, k)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 0, nq, dim)
+    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    for nm in names:
+        engine.drop_collection(nm)
+
+
+def test_large_properties(engine, orc):
+    """Size-independent checks at 2M rows: self-match and monotone k-prefixes."""
+    dim, n = 768, 2_000_000
+    engine.create_collection("big", dim, 0, 1, n)
+    engine.generate("big", n, orc.SEED_CORPUS)
+    probe = [0, 123457, 1999999]
+    Xp = orc.generate(orc.SEED_CORPUS, 0, 1, dim, True)  # noqa: F841 (warm)
+    Q = np.concatenate([orc.generate(orc.SEED_CORPUS, i, 1, dim, True) for i in probe])
+    s, r, c = engine.search("big", Q, 10)            # MFMA path
+    assert r[:, 0].tolist() == probe and np.all(np.abs(s[:, 0] - 1) < 1e-2)
+    for i, p in enumerate(probe):
+        s1, r1, c1 = engine.search("big", Q[i], 10)  # GEMV path
+        assert r1[0, 0] == p
+        s2, r2, c2 = engine.search("big", Q[i], 100)
+        assert r2[0, :10].tolist() == r1[0].tolist()
+        assert np.all(np.diff(s2[0]) <= 0)
+    engine.drop_collection("big")
+
+
+def test_health(engine):
+    import json
+    h = json.loads(engine.health())
+    assert h["status"] == "healthy" and h["hbm_total_bytes"] > 0
