@@ -196,31 +196,74 @@ def test_dot_metric(engine, orc):
 
 
 # ----------------------------------------------- sharded merge on one device
-def test_sharded_merge_equals_unsharded(engine, orc):
-    torch = pytest.importorskip("torch")
-    dim, n, P, nq, k = 768, 30000, 4, 40, 10
-    per = (n + P - 1) // P
-    names = []
-    for p in range(P):
-        lo, hi = p * per, min(n, (p + 1) * per)
-        nm = f"shard{p}"
-        engine.create_collection(nm, dim, 0, 1, 0, lo)
-        engine.generate(nm, hi - lo, orc.SEED_CORPUS)
-        names.append(nm)
-    dq = torch.empty((nq, dim), dtype=torch.float32, device="cuda")
-    engine.generate_vectors(orc.SEED_QUERY, 0, nq, dim, dq.data_ptr())
-    torch.cuda.synchronize()
-    lists = torch.zeros((P, nq, k), dtype=torch.int64, device="cuda")
-    for p, nm in enumerate(names):
-        engine.search_keys(nm, dq.data_ptr(), nq, dim, k, lists[p].data_ptr())
-    out = torch.zeros((nq, k), dtype=torch.int64, device="cuda")
-    engine.merge_keys(lists.data_ptr(), P, nq, k, k, out.data_ptr())
-    s, r, c = engine.decode_keys(out.data_ptr(), nq, k)
-    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
-    Q = orc.generate(orc.SEED_QUERY, 0, nq, dim)
-    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
-    for nm in names:
-        engine.drop_collection(nm)
+_SHARDED = r"""
+import sys, json
+import torch                      # first: the library then binds torch's HIP runtime
+import numpy as np
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+eng = pkg.VectorEngine(device=0)
+dim, n, P, nq, k = 768, 30000, 4, 40, 10
+per = (n + P - 1) // P
+for p in range(P):
+    lo, hi = p * per, min(n, (p + 1) * per)
+    eng.create_collection(f"shard{p}", dim, 0, 1, 0, lo)
+    eng.generate(f"shard{p}", hi - lo, orc.SEED_CORPUS)
+dq = torch.empty((nq, dim), dtype=torch.float32, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+eng.generate_vectors(orc.SEED_QUERY, 0, nq, dim, dq.data_ptr(), st)
+lists = torch.zeros((P, nq, k), dtype=torch.int64, device="cuda")
+for p in range(P):
+    eng.search_keys(f"shard{p}", dq.data_ptr(), nq, dim, k, lists[p].data_ptr(), st)
+out = torch.zeros((nq, k), dtype=torch.int64, device="cuda")
+eng.merge_keys(lists.data_ptr(), P, nq, k, k, out.data_ptr(), st)
+s, r, c = eng.decode_keys(out.data_ptr(), nq, k, st)
+# the device-generated queries equal the oracle's generator rows
+assert np.array_equal(dq.cpu().numpy(), orc.generate(orc.SEED_QUERY, 0, nq, dim))
+X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+Qp = orc.preprocess(orc.generate(orc.SEED_QUERY, 0, nq, dim), True, True)
+s32, s64, rows, cnt = orc.search(X, Qp, k)
+resc = orc.rescore(X, Qp, r, c)
+bad = orc.check_topk(s, r, c, s64, rows, cnt, resc, 1e-5)
+print(json.dumps({"bad": bad[:10]}))
+"""
+
+
+def _run_py(code, timeout=300):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", f"ROOT={root!r}\n" + code], capture_output=True,
+                         text=True, timeout=timeout)
+    assert res.returncode == 0, res.stderr[-3000:]
+    return json.loads(res.stdout.strip().splitlines()[-1])
+
+
+def test_sharded_merge_equals_unsharded():
+    """4 row shards (row_base offsets) searched by device pointer, keys merged on device."""
+    assert _run_py(_SHARDED)["bad"] == []
+
+
+def test_bench_small_runs():
+    """bench.py end to end (torch first, device queries, JSON line) on a small corpus."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for cfg in ("c3", "c2"):
+        res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", cfg,
+                              "--rows", "300000", "--steps", "3", "--warmup", "1",
+                              "--cpu-sample-rows", "20000", "--cpu-sample-queries", "2"],
+                             capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stderr[-3000:]
+        line = json.loads(res.stdout.strip().splitlines()[-1])
+        assert line["value"] > 0 and line["roofline"]["frac"] > 0
+        assert line["cpu_baseline"]["value"] > 0
 
 
 def test_large_properties(engine, orc):
