@@ -1,0 +1,549 @@
+// vector_service.cpp — rag/vector-service's handlers restated over the
+// engine C-ABI (see include/vsearch_service.h for the route map).
+//
+// Each handler follows the Go function line by line in behaviour: the same
+// decode step (json.NewDecoder(r.Body).Decode into the request struct), the
+// same validation order and messages, the same response structs. Where the
+// reference forwards to Qdrant, the engine is called instead and Qdrant's
+// gRPC error shape ("rpc error: code = ... desc = ...") is kept in the
+// messages, as the Go service surfaces err.Error() verbatim.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/vsearch_service.h"
+#include "json.h"
+
+using vsjson::Json;
+
+namespace {
+
+struct CollState {
+  std::string name;
+  uint32_t dim = 0;
+  std::shared_mutex mu;                              // upsert = writer, search = reader
+  std::unordered_map<std::string, uint64_t> row_of;  // canonical UUID -> row
+  std::vector<std::string> uuid_of;                  // row -> UUID
+  std::vector<Json> payload_of;                      // row -> payload (a decoded map)
+};
+
+struct Response {
+  int status = 200;
+  std::string body;
+  const char* type = "application/json";
+};
+
+const char* kJsonType = "application/json";
+const char* kTextType = "text/plain; charset=utf-8";
+
+// respondError (main.go:388-392)
+Response error_json(const std::string& msg, int status) {
+  Json o = Json::object();
+  o.obj.emplace_back("error", Json::string(msg));
+  Response r;
+  r.status = status;
+  vsjson::encode(o, &r.body);
+  r.body.push_back('\n');
+  return r;
+}
+
+// http.Error(w, msg, code)
+Response error_text(const std::string& msg, int status) {
+  Response r;
+  r.status = status;
+  r.type = kTextType;
+  r.body = msg + "\n";
+  return r;
+}
+
+std::string last_error() { return vs_last_error(); }
+
+std::string grpc_error(int rc, const std::string& msg) {
+  const char* code = rc == VS_ERR_NOT_FOUND ? "NotFound"
+                     : (rc == VS_ERR_INVALID_ARG || rc == VS_ERR_DIM_MISMATCH) ? "InvalidArgument"
+                     : rc == VS_ERR_OOM ? "ResourceExhausted"
+                                        : "Internal";
+  return std::string("rpc error: code = ") + code + " desc = " + msg;
+}
+
+std::string not_found(const std::string& coll) {
+  return grpc_error(VS_ERR_NOT_FOUND, "Not found: Collection `" + coll + "` doesn't exist!");
+}
+
+std::string dim_error(uint32_t want, size_t got) {
+  return grpc_error(VS_ERR_DIM_MISMATCH, "Wrong input: Vector dimension error: expected dim: " +
+                                             std::to_string(want) + ", got " + std::to_string(got));
+}
+
+// Uuid::parse_str (upstream Qdrant, rust `uuid` crate): simple, hyphenated,
+// braced or urn forms, any hex case; canonical form is lowercase hyphenated.
+bool canonical_uuid(const std::string& in, std::string* out) {
+  std::string s = in;
+  if (s.size() == 45 && s.compare(0, 9, "urn:uuid:") == 0) s = s.substr(9);
+  if (s.size() == 38 && s.front() == '{' && s.back() == '}') s = s.substr(1, 36);
+  std::string hex;
+  if (s.size() == 36) {
+    for (size_t i = 0; i < 36; ++i) {
+      bool dash = (i == 8 || i == 13 || i == 18 || i == 23);
+      if (dash) {
+        if (s[i] != '-') return false;
+      } else {
+        hex.push_back(s[i]);
+      }
+    }
+  } else if (s.size() == 32) {
+    hex = s;
+  } else {
+    return false;
+  }
+  for (char& c : hex) {
+    if (c >= 'A' && c <= 'F') c = (char)(c - 'A' + 'a');
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+  }
+  *out = hex.substr(0, 8) + "-" + hex.substr(8, 4) + "-" + hex.substr(12, 4) + "-" +
+         hex.substr(16, 4) + "-" + hex.substr(20, 12);
+  return true;
+}
+
+// Go decodes numbers inside interface{} values with ParseFloat(s, 64): a
+// literal beyond float64's range is an UnmarshalTypeError.
+bool interface_numbers_ok(const Json& v) {
+  switch (v.kind) {
+    case Json::Number: return std::abs(v.num) <= 1.7976931348623157e308;
+    case Json::Array:
+      for (const auto& e : v.arr)
+        if (!interface_numbers_ok(e)) return false;
+      return true;
+    case Json::Object:
+      for (const auto& e : v.obj)
+        if (!interface_numbers_ok(e.second)) return false;
+      return true;
+    default: return true;
+  }
+}
+
+// ---- request decoding (json.Decoder.Decode into the Go structs) -------------
+struct SearchRequest {  // main.go:26-31
+  std::string collection;
+  std::vector<float> query;
+  int64_t top_k = 0;
+};
+
+// Returns "" on success, else the decode error.
+std::string decode_search(const char* body, size_t len, SearchRequest* req) {
+  Json root;
+  std::string err;
+  if (!vsjson::parse(body, len, &root, &err)) return err;
+  if (root.kind == Json::Null) return "";
+  if (root.kind != Json::Object) return "cannot unmarshal into SearchRequest";
+  std::string first;
+  if (const Json* c = root.field("collection")) {
+    if (c->kind == Json::String) req->collection = c->str;
+    else if (c->kind != Json::Null && first.empty()) first = "collection: not a string";
+  }
+  if (const Json* q = root.field("query")) {
+    if (q->kind == Json::Array) {
+      req->query.assign(q->arr.size(), 0.0f);
+      for (size_t i = 0; i < q->arr.size(); ++i) {
+        const Json& e = q->arr[i];
+        if (e.kind == Json::Number) {
+          float f;
+          if (!vsjson::parse_float32(e.str, &f)) {
+            if (first.empty()) first = "cannot unmarshal number " + e.str + " into float32";
+          } else {
+            req->query[i] = f;
+          }
+        } else if (e.kind != Json::Null && first.empty()) {
+          first = "query: non-numeric element";
+        }
+      }
+    } else if (q->kind == Json::Null) {
+      req->query.clear();
+    } else if (first.empty()) {
+      first = "query: not an array";
+    }
+  }
+  if (const Json* k = root.field("top_k")) {
+    if (k->kind == Json::Number) {
+      int64_t v;
+      if (!vsjson::parse_int64(k->str, &v)) {
+        if (first.empty()) first = "cannot unmarshal number " + k->str + " into int";
+      } else {
+        req->top_k = v;
+      }
+    } else if (k->kind != Json::Null && first.empty()) {
+      first = "top_k: not a number";
+    }
+  }
+  if (const Json* f = root.field("filter")) {
+    if (f->kind == Json::Object) {
+      if (!interface_numbers_ok(*f) && first.empty()) first = "filter: number out of range";
+    } else if (f->kind != Json::Null && first.empty()) {
+      first = "filter: not an object";
+    }
+  }
+  return first;
+}
+
+struct UpsertRequest {  // main.go:21-24
+  std::string collection;
+  std::vector<const Json*> points;  // nullptr = a JSON null point (nil map)
+  Json root;
+};
+
+std::string decode_upsert(const char* body, size_t len, UpsertRequest* req) {
+  std::string err;
+  if (!vsjson::parse(body, len, &req->root, &err)) return err;
+  const Json& root = req->root;
+  if (root.kind == Json::Null) return "";
+  if (root.kind != Json::Object) return "cannot unmarshal into UpsertRequest";
+  std::string first;
+  if (const Json* c = root.field("collection")) {
+    if (c->kind == Json::String) req->collection = c->str;
+    else if (c->kind != Json::Null && first.empty()) first = "collection: not a string";
+  }
+  if (const Json* p = root.field("points")) {
+    if (p->kind == Json::Array) {
+      for (const auto& e : p->arr) {
+        if (e.kind == Json::Object) {
+          if (!interface_numbers_ok(e) && first.empty()) first = "point: number out of range";
+          req->points.push_back(&e);
+        } else if (e.kind == Json::Null) {
+          req->points.push_back(nullptr);
+        } else if (first.empty()) {
+          first = "points: element is not an object";
+        }
+      }
+    } else if (p->kind != Json::Null && first.empty()) {
+      first = "points: not an array";
+    }
+  }
+  return first;
+}
+
+// convertVector (main.go:343-375) for a decoded interface{}
+bool convert_vector(const Json& v, std::vector<float>* out, std::string* err) {
+  if (v.kind != Json::Array) {
+    *err = "point vector must be an array";
+    return false;
+  }
+  out->resize(v.arr.size());
+  for (size_t i = 0; i < v.arr.size(); ++i) {
+    if (v.arr[i].kind != Json::Number) {
+      *err = "vector contains non-numeric value";
+      return false;
+    }
+    (*out)[i] = (float)v.arr[i].num;  // float32(num): float64 -> float32, round to nearest even
+  }
+  return true;
+}
+
+}  // namespace
+
+struct vsvc {
+  vs_engine* eng = nullptr;
+  std::vector<std::string> listed;  // the /collections reply (hard-coded in the reference)
+  std::mutex mu;
+  std::unordered_map<std::string, std::shared_ptr<CollState>> colls;
+
+  std::shared_ptr<CollState> find(const std::string& name) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = colls.find(name);
+    return it == colls.end() ? nullptr : it->second;
+  }
+};
+
+namespace {
+
+// healthHandler (main.go:121-136)
+Response handle_health(vsvc* svc) {
+  char buf[1024];
+  int rc = vs_health(svc->eng, buf, sizeof(buf));
+  Json o = Json::object();
+  Json eng_info;
+  std::string perr;
+  bool parsed = vsjson::parse(buf, std::strlen(buf), &eng_info, &perr);
+  std::string status = "healthy";
+  if (rc != VS_OK) {
+    status = "degraded";
+    o.obj.emplace_back("error", Json::string(last_error()));
+  } else if (parsed) {
+    const Json* dn = eng_info.get("device_name");
+    o.obj.emplace_back("engine", Json::string(std::string("vsearch-hip") +
+                                              (dn ? " " + dn->str : std::string())));
+  }
+  o.obj.emplace_back("service", Json::string("vector-service"));
+  o.obj.emplace_back("status", Json::string(status));
+  Response r;
+  vsjson::encode(o, &r.body);  // map[string]string: keys sorted
+  r.body.push_back('\n');
+  return r;
+}
+
+// collectionsHandler (main.go:138-147)
+Response handle_collections(vsvc* svc, const std::string& method) {
+  if (method != "GET") return error_text("Method not allowed", 405);
+  Json arr = Json::array();
+  for (const auto& n : svc->listed) arr.arr.push_back(Json::string(n));
+  Json o = Json::object();
+  o.obj.emplace_back("collections", std::move(arr));
+  Response r;
+  vsjson::encode(o, &r.body);
+  r.body.push_back('\n');
+  return r;
+}
+
+// upsertHandler (main.go:149-225)
+Response handle_upsert(vsvc* svc, const std::string& method, const char* body, size_t len) {
+  if (method != "POST") return error_text("Method not allowed", 405);
+  UpsertRequest req;
+  if (!decode_upsert(body, len, &req).empty()) return error_json("Invalid request body", 400);
+  if (req.collection.empty()) return error_json("Collection name required", 400);
+
+  const size_t n = req.points.size();
+  std::vector<std::string> ids(n);
+  std::vector<std::vector<float>> vecs(n);
+  std::vector<Json> payloads(n, Json::object());
+  for (size_t i = 0; i < n; ++i) {
+    const Json* p = req.points[i];
+    const Json* id = p ? p->get("id") : nullptr;
+    if (!id || id->kind != Json::String) return error_json("Point ID must be a string", 400);
+    ids[i] = id->str;
+    const Json* v = p->get("vector");
+    if (!v) return error_json("Point vector must be provided", 400);
+    std::string err;
+    if (!convert_vector(*v, &vecs[i], &err)) return error_json(err, 400);
+    if (const Json* pl = p->get("payload"))
+      if (pl->kind == Json::Object) payloads[i] = *pl;
+  }
+
+  // --- Points.Upsert(wait=true) ---
+  auto cs = svc->find(req.collection);
+  if (!cs) return error_json("Failed to upsert: " + not_found(req.collection), 500);
+  std::vector<std::string> canon(n);
+  for (size_t i = 0; i < n; ++i)
+    if (!canonical_uuid(ids[i], &canon[i]))
+      return error_json("Failed to upsert: " +
+                            grpc_error(VS_ERR_INVALID_ARG, "Unable to parse UUID: " + ids[i]),
+                        500);
+  for (size_t i = 0; i < n; ++i)
+    if (vecs[i].size() != cs->dim)
+      return error_json("Failed to upsert: " + dim_error(cs->dim, vecs[i].size()), 500);
+
+  std::unique_lock<std::shared_mutex> wl(cs->mu);
+  const uint64_t base = cs->uuid_of.size();
+  std::unordered_map<std::string, uint64_t> fresh;  // new UUIDs of this batch
+  std::vector<uint64_t> rows(n);
+  for (size_t i = 0; i < n; ++i) {
+    auto it = cs->row_of.find(canon[i]);
+    if (it != cs->row_of.end()) {
+      rows[i] = it->second;
+    } else {
+      auto f = fresh.find(canon[i]);
+      if (f != fresh.end()) {
+        rows[i] = f->second;
+      } else {
+        rows[i] = base + fresh.size();
+        fresh.emplace(canon[i], rows[i]);
+      }
+    }
+  }
+  if (n) {
+    std::vector<float> flat(n * (size_t)cs->dim);
+    for (size_t i = 0; i < n; ++i)
+      std::memcpy(&flat[i * cs->dim], vecs[i].data(), (size_t)cs->dim * 4);
+    int rc = vs_upsert(svc->eng, req.collection.c_str(), n, cs->dim, rows.data(), flat.data());
+    if (rc != VS_OK) return error_json("Failed to upsert: " + grpc_error(rc, last_error()), 500);
+  }
+  cs->uuid_of.resize(base + fresh.size());
+  cs->payload_of.resize(base + fresh.size());
+  for (size_t i = 0; i < n; ++i) {  // in request order: the last duplicate wins
+    cs->row_of[canon[i]] = rows[i];
+    cs->uuid_of[rows[i]] = canon[i];
+    cs->payload_of[rows[i]] = payloads[i];
+  }
+  wl.unlock();
+
+  Json o = Json::object();
+  o.obj.emplace_back("status", Json::string("success"));
+  o.obj.emplace_back("collection", Json::string(req.collection));
+  o.obj.emplace_back("points", Json::number((double)n));
+  Response r;
+  vsjson::encode(o, &r.body);  // map[string]interface{}: keys sorted
+  r.body.push_back('\n');
+  return r;
+}
+
+// searchHandler (main.go:227-278)
+Response handle_search(vsvc* svc, const std::string& method, const char* body, size_t len) {
+  if (method != "POST") return error_text("Method not allowed", 405);
+  SearchRequest req;
+  if (!decode_search(body, len, &req).empty()) return error_json("Invalid request body", 400);
+  if (req.top_k == 0) req.top_k = 5;
+  const uint64_t limit = (uint64_t)req.top_k;  // Limit: uint64(req.TopK)
+
+  auto cs = svc->find(req.collection);
+  if (!cs) return error_json("Search failed: " + not_found(req.collection), 500);
+  std::shared_lock<std::shared_mutex> rl(cs->mu);
+  if (req.query.size() != cs->dim)
+    return error_json("Search failed: " + dim_error(cs->dim, req.query.size()), 500);
+  const uint64_t rows = cs->uuid_of.size();
+  uint64_t k = std::min<uint64_t>(limit, std::max<uint64_t>(rows, 1));
+  if (k > 1024)
+    return error_json("Search failed: " + grpc_error(VS_ERR_INVALID_ARG,
+                                                     "limit " + std::to_string(limit) +
+                                                         " exceeds the engine maximum 1024"),
+                      500);
+  std::vector<float> scores(k);
+  std::vector<uint64_t> hit_rows(k);
+  uint32_t count = 0;
+  int rc = vs_search(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
+                     (uint32_t)k, scores.data(), hit_rows.data(), &count);
+  if (rc != VS_OK) return error_json("Search failed: " + grpc_error(rc, last_error()), 500);
+
+  // SearchResponse{Results, Count}: struct fields in declaration order
+  std::string out;
+  out.append("{\"results\":[");
+  for (uint32_t j = 0; j < count; ++j) {
+    if (j) out.push_back(',');
+    const uint64_t row = hit_rows[j];
+    out.append("{\"id\":");
+    vsjson::encode_string(row < rows ? cs->uuid_of[row] : std::string(), &out);
+    out.append(",\"score\":");
+    vsjson::encode_float64((double)scores[j], &out);  // float64(hit.GetScore())
+    out.append(",\"payload\":");
+    vsjson::encode(row < rows ? cs->payload_of[row] : Json::object(), &out);
+    out.push_back('}');
+  }
+  out.append("],\"count\":");
+  out.append(std::to_string(count));
+  out.append("}\n");
+  Response r;
+  r.body = std::move(out);
+  return r;
+}
+
+char* dup_bytes(const std::string& s) {
+  char* p = (char*)std::malloc(s.size() + 1);
+  if (p) {
+    std::memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+  }
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
+  if (!eng || !out) return VS_ERR_INVALID_ARG;
+  *out = nullptr;
+  struct Spec {
+    std::string name;
+    uint32_t dim;
+    int metric, dtype;
+  };
+  std::vector<Spec> specs;
+  if (!config_json) {
+    for (const char* n : {"regulatory_docs", "merchant_docs", "kyc_docs"})
+      specs.push_back({n, 768, VS_METRIC_COSINE, VS_DTYPE_F32});
+  } else {
+    Json cfg;
+    std::string err;
+    if (!vsjson::parse(config_json, std::strlen(config_json), &cfg, &err)) return VS_ERR_INVALID_ARG;
+    const Json* cl = cfg.get("collections");
+    if (!cl || cl->kind != Json::Array) return VS_ERR_INVALID_ARG;
+    for (const auto& c : cl->arr) {
+      const Json* nm = c.get("name");
+      const Json* dm = c.get("dim");
+      const Json* mt = c.get("metric");
+      const Json* dt = c.get("dtype");
+      if (!nm || nm->kind != Json::String || !dm || dm->kind != Json::Number)
+        return VS_ERR_INVALID_ARG;
+      Spec s{nm->str, (uint32_t)dm->num, VS_METRIC_COSINE, VS_DTYPE_F32};
+      if (mt && mt->kind == Json::String && (mt->str == "Dot" || mt->str == "dot"))
+        s.metric = VS_METRIC_DOT;
+      if (dt && dt->kind == Json::String && dt->str == "bf16") s.dtype = VS_DTYPE_BF16;
+      specs.push_back(s);
+    }
+  }
+  auto svc = std::make_unique<vsvc>();
+  svc->eng = eng;
+  for (const auto& s : specs) {
+    // initializeCollections: Get, and Create when NotFound (main.go:91-112)
+    uint32_t dim = 0;
+    uint64_t rows = 0;
+    int rc = vs_collection_info(eng, s.name.c_str(), &dim, &rows, nullptr, nullptr);
+    if (rc == VS_ERR_NOT_FOUND)
+      rc = vs_collection_create(eng, s.name.c_str(), s.dim, s.metric, s.dtype, 0, 0);
+    else if (rc == VS_OK && rows != 0)
+      rc = VS_ERR_EXISTS;  // rows without UUIDs cannot be served through this layer
+    if (rc != VS_OK) return rc;
+    auto cs = std::make_shared<CollState>();
+    cs->name = s.name;
+    cs->dim = dim ? dim : s.dim;
+    svc->colls[s.name] = cs;
+    svc->listed.push_back(s.name);
+  }
+  *out = svc.release();
+  return VS_OK;
+}
+
+void vsvc_close(vsvc* svc) { delete svc; }
+
+int vsvc_handle(vsvc* svc, const char* method, const char* path, const char* body,
+                size_t body_len, int* status, char** resp, size_t* resp_len,
+                const char** content_type) {
+  if (!svc || !method || !path || !status || !resp) return VS_ERR_INVALID_ARG;
+  if (!body) body = "";
+  const std::string m = method, p = path;
+  Response r;
+  if (p == "/health") r = handle_health(svc);
+  else if (p == "/collections") r = handle_collections(svc, m);
+  else if (p == "/upsert") r = handle_upsert(svc, m, body, body_len);
+  else if (p == "/search") r = handle_search(svc, m, body, body_len);
+  else r = error_text("404 page not found", 404);
+  *status = r.status;
+  *resp = dup_bytes(r.body);
+  if (resp_len) *resp_len = r.body.size();
+  if (content_type) *content_type = r.type == kTextType ? kTextType : kJsonType;
+  return *resp ? VS_OK : VS_ERR_OOM;
+}
+
+void vsvc_free(char* p) { std::free(p); }
+
+int vsvc_reencode(const char* json, size_t len, char** out) {
+  Json v;
+  std::string err;
+  if (!vsjson::parse(json, len, &v, &err)) {
+    *out = dup_bytes(err);
+    return -1;
+  }
+  std::string s;
+  vsjson::encode(v, &s);
+  s.push_back('\n');
+  *out = dup_bytes(s);
+  return 0;
+}
+
+int vsvc_validate(const char* path, const char* body, size_t len, char** msg) {
+  std::string p = path ? path : "", err;
+  if (p == "/search") {
+    SearchRequest r;
+    err = decode_search(body ? body : "", len, &r);
+  } else if (p == "/upsert") {
+    UpsertRequest r;
+    err = decode_upsert(body ? body : "", len, &r);
+  }
+  if (msg) *msg = dup_bytes(err);
+  return err.empty() ? 0 : 400;
+}
+
+}  // extern "C"

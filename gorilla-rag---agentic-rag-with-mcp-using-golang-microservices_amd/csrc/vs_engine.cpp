@@ -94,7 +94,7 @@ struct vs_engine {
   std::mutex map_mu;
   std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
   std::mutex work_mu;  // scratch buffers + stream
-  DevBuf q_in, q_pre, q_bf16, lists, keys, upsert_vecs, upsert_rows;
+  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
   std::vector<uint64_t> h_keys;
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
@@ -187,10 +187,13 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     const uint32_t maxl = vsk::mfma_max_lists(n_rows);
     const size_t lbytes = (size_t)maxl * P * k * 8;
     const size_t bbytes = (size_t)P * dim * 2;
-    if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes) {
+    const size_t sbytes = (size_t)P * k * 8;
+    if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes ||
+        eng->sample_keys.bytes < sbytes) {
       VS_HIP(hipStreamSynchronize(eng->stream), "sync");
       VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
       VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
+      VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
     }
     for (uint32_t p = 0; p < npass; ++p) {
       const uint32_t q0 = p * P;
@@ -203,9 +206,24 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
       VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
              "queries to bf16");
       uint32_t L = 0;
+      // sample pass: exact top-k over the first 1/64 of every workgroup's
+      // tiles; its k-th key per query lower-bounds the global k-th key
+      const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
+      const uint64_t* init = nullptr;
+      if (tpw >= 64) {
+        uint64_t* skeys = eng->sample_keys.as<uint64_t>();
+        VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k,
+                                tpw / 64, nullptr, 0, eng->lists.as<uint64_t>(), maxl, &L,
+                                eng->stream),
+               "mfma sample scan");
+        VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, (uint64_t)P * k, k, nv, k, k,
+                                 skeys, eng->stream),
+               "sample merge");
+        init = skeys + (k - 1);
+      }
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k,
-                              eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+      VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k, 0, init,
+                              k, eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
              "mfma scan");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");

@@ -38,12 +38,18 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 
 // Batched bf16 scan on MFMA with fused top-k. Q is kMfmaQueries x dim bf16
 // (zero-padded), nq_valid <= kMfmaQueries. Writes out[nlists][kMfmaQueries][k].
+// max_tiles > 0 limits every workgroup to its first max_tiles 32-row tiles
+// (the sample pass); init_th (nullable) gives per-query lower-bound keys at
+// init_th[q * init_stride].
 bool mfma_supported(uint32_t dim);
 hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                        uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
-                       uint32_t k, uint64_t* out, uint32_t max_lists,
+                       uint32_t k, uint32_t max_tiles, const uint64_t* init_th,
+                       uint32_t init_stride, uint64_t* out, uint32_t max_lists,
                        uint32_t* nlists, hipStream_t st);
 uint32_t mfma_max_lists(uint32_t n_rows);
+uint32_t mfma_tiles_per_wg(uint32_t n_rows);
+void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);
 
 // Merge L sorted key lists per query -> out [nq][k] (global top-k by key).
 // List l of query q starts at lists[l * lstride + q * qstride], kin entries.

@@ -516,17 +516,29 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // ---------------------------------------------------------------------------
 // batched bf16 scan on MFMA + fused top-k
 // ---------------------------------------------------------------------------
-// Workgroup = 8 waves; wave w owns queries [32w, 32w+32) and keeps their
-// B-operand fragments for the whole row (D/16 k-steps x 4 VGPRs) resident in
-// registers. Corpus tiles of 32 rows x D stream HBM -> LDS once per
-// workgroup by global_load_lds (1 KiB pieces = 8 rows x 128 B), double
-// buffered; every wave reads the tile's A fragments with ds_read_b128 and
-// runs D/16 v_mfma_f32_32x32x16_bf16 into one 32x32 accumulator
-// (C[row][query], query = lane & 31). The epilogue filters the 16 scores per
-// lane against the query's current k-th key and inserts survivors into a
-// per-query sorted list in LDS. Scores never reach HBM.
-constexpr int kMfThreads = 512;
+// Workgroup = 4 waves, one per SIMD (512-VGPR budget each); wave w owns
+// queries [64w, 64w+64) as two MFMA column groups of 32 and keeps their
+// B-operand fragments for the whole row (2 x D/16 k-steps x 4 VGPRs) resident
+// in registers. The workgroup streams its contiguous row range HBM -> LDS once,
+// by global_load_lds (1 KiB pieces = 8 rows x 128 B), through a ring of
+// K-chunks (32 rows x 256 k = 16 KiB); AHEAD chunks stay in flight across the
+// raw s_barrier that publishes each chunk (counted vmcnt, never a drain inside
+// the loop). Each A fragment read from LDS (ds_read_b128) feeds two
+// v_mfma_f32_32x32x16_bf16, one per query group, into two 32x32 accumulators
+// per 32-row tile (C[row][query], query = lane & 31). The tile epilogue
+// filters the 16 scores per lane and group against the query's current
+// threshold key and inserts survivors into a per-query sorted list in LDS.
+// Scores never reach HBM.
+//
+// Threshold: max(the list's own k-th key, init_th[q] - 1). init_th is the
+// k-th key of an exact top-k over a sample of the same rows (the "sample
+// pass"): every row outside the final top-k of the sample
+// ranks below it, so it is a lower bound on the global k-th key and rows
+// under it can never enter the result. It cuts the insert traffic ~25x.
+constexpr int kMfThreads = 256;
+constexpr int kMfWaves = kMfThreads / 64;
 constexpr int kMfLists = (int)kMfmaMaxK * (int)kMfmaQueries;  // LDS list entries
+constexpr int kMfRingBytes = 112 * 1024;
 
 // XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
 // ds_read_b128 lane groups over all 64 banks (conflict-free).
@@ -534,67 +546,115 @@ __device__ __forceinline__ int mf_swz(int ri, int rg) {
   return ((ri >> 1) & 3) | ((rg & 1) << 2);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 16-B-per-lane LDS-DMA (global_load_lds_dwordx4) to the wave-uniform LDS
+// byte address `lds` (+ lane*16). Issued from inline asm so hipcc's waitcnt
+// pass does not see an LDS store and cannot drain vmcnt before every
+// ds_read of the ring; completion is counted by wait_vmcnt<N>() by hand.
+// M0 is written and restored inside the statement (§5.7: M0 is reserved).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
 template <int D>
 struct MfShape {
-  static constexpr int S = D / 16;         // MFMA k-steps per row
-  static constexpr int S4 = D / 64;        // 128-B pieces per row
-  static constexpr int NBLK = S4 * 4;      // 1-KiB LDS-DMA pieces per tile
-  static constexpr int TILE_BYTES = NBLK * 1024;
-  static constexpr int BPW = NBLK / 8;     // pieces issued per wave per tile
-  static constexpr int LDS_BYTES = 2 * TILE_BYTES + kMfLists * 8;
+  static constexpr int S = D / 16;                        // MFMA k-steps per row
+  static constexpr int CS4 = (D % 256 == 0) ? 4 : 2;      // 128-B pieces per row per chunk
+  static constexpr int CK = CS4 * 4;                      // MFMA k-steps per chunk
+  static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
+  static constexpr int CHUNK_BYTES = CS4 * 4 * 1024;      // 32 rows x CS4*128 B
+  static constexpr int NSLOT = kMfRingBytes / CHUNK_BYTES;
+  static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
+  static constexpr int PPW = CS4 * 4 / kMfWaves;          // LDS-DMA pieces per wave per chunk
+  static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + kMfLists * 8;
   static_assert(D % 128 == 0, "MFMA scan needs D % 128 == 0");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int D>
-__global__ __launch_bounds__(kMfThreads) void mfma_topk_kernel(
+// MODE: 0 = main pass; 3 = sample pass (same code, separate symbol so the
+// two launches are told apart in rocprof); 1/2 = ablation builds only
+// (tools/ablate_mfma.hip): 1 = no top-k epilogue, 2 = LDS-DMA stream only.
+template <int D, int MODE = 0>
+__global__ __launch_bounds__(kMfThreads, 1) void mfma_topk_kernel(
     const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t row_base,
-    uint32_t rows_per_wg, const uint16_t* __restrict__ Q, uint32_t nq_valid, uint32_t k,
+    uint32_t rows_per_wg, uint32_t max_tiles, const uint16_t* __restrict__ Q,
+    uint32_t nq_valid, uint32_t k, const uint64_t* __restrict__ init_th, uint32_t init_stride,
     uint64_t* __restrict__ out) {
   using S = MfShape<D>;
+  // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
+  // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
-  uint64_t* lists = (uint64_t*)(smem + 2 * S::TILE_BYTES);
+  // The two lanes of a query (h = 0, 1) hand list entries to each other
+  // through LDS inside one wave with no barrier: volatile keeps every access
+  // in program order (a wave's DS instructions execute in order), so the
+  // compiler cannot forward a stale entry across the two insert passes.
+  volatile uint64_t* lists = (volatile uint64_t*)(smem + S::NSLOT * S::CHUNK_BYTES);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const uint32_t ql = (uint32_t)(w * 32 + r);
-  const bool qvalid = ql < nq_valid;
   const uint32_t wr0 = blockIdx.x * rows_per_wg;
   const uint32_t wr1 = (uint64_t)wr0 + rows_per_wg < n_rows ? wr0 + rows_per_wg : n_rows;
-  const uint32_t ntiles = (wr1 - wr0 + 31) / 32;
+  uint32_t ntiles = (wr1 - wr0 + 31) / 32;
+  if (max_tiles && ntiles > max_tiles) ntiles = max_tiles;
+  const uint32_t nchunks = ntiles * S::CPT;
 
   for (int i = threadIdx.x; i < kMfLists; i += kMfThreads) lists[i] = 0;
 
-  // B operand: Q[query ql][16s + 8h + j], j = 0..7  -> one 16-B load per step.
-  bf16x8_t qf[S::S];
-  {
-    const uint4* qrow = (const uint4*)(Q + (size_t)ql * D);
+  // B operand of group g: Q[query 64w+32g+r][16s + 8h + j], j = 0..7.
+  bf16x8_t qf[2][S::S];
+  uint32_t ql[2];
+  bool qvalid[2];
+  uint64_t thi[2], th[2];
+  float th_s[2];
 #pragma unroll
-    for (int s = 0; s < S::S; ++s) qf[s] = __builtin_bit_cast(bf16x8_t, qrow[2 * s + h]);
+  for (int g = 0; g < 2; ++g) {
+    ql[g] = (uint32_t)(w * 64 + g * 32 + r);
+    qvalid[g] = ql[g] < nq_valid;
+    const uint4* qrow = (const uint4*)(Q + (size_t)ql[g] * D);
+#pragma unroll
+    for (int s = 0; s < S::S; ++s) qf[g][s] = __builtin_bit_cast(bf16x8_t, qrow[2 * s + h]);
+    const uint64_t it = (init_th && qvalid[g]) ? init_th[(size_t)ql[g] * init_stride] : 0;
+    thi[g] = it ? it - 1 : 0;  // admit the bound itself ("key > th")
+    th[g] = thi[g];
+    th_s[g] = it ? key_score(it) : -INFINITY;
   }
 
-  // LDS-DMA source mapping: piece (s4, rg) holds rows rg*8 .. rg*8+7, bytes
-  // [128*s4, 128*s4+128) of each; lane -> (row lane>>3, position lane&7).
+  // LDS-DMA source mapping: piece (s4l, rg) of a chunk holds rows rg*8 ..
+  // rg*8+7, bytes [128*s4, 128*s4+128) of each; lane -> (row lane>>3,
+  // 16-B position lane&7 holding chunk (lane&7) ^ swz). Wave w loads row
+  // group w of every piece column.
   const int g_ri = lane >> 3;
   const int g_p = lane & 7;
-  auto issue = [&](uint32_t t, int slot) {
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  auto issue = [&](uint32_t c) {
+    const uint32_t t = c / S::CPT;
+    const int u = (int)(c - t * S::CPT);
     const uint32_t trow0 = wr0 + t * 32;
+    const uint32_t sb = lds_base + (c % S::NSLOT) * S::CHUNK_BYTES;
 #pragma unroll
-    for (int i = 0; i < S::BPW; ++i) {
-      const int b = w + 8 * i;
-      const int s4 = b >> 2, rg = b & 3;
+    for (int i = 0; i < S::PPW; ++i) {
+      const int b = w + kMfWaves * i;
+      const int s4l = b >> 2, rg = b & 3;
       uint32_t row = trow0 + rg * 8 + g_ri;
       row = row < n_rows ? row : n_rows - 1;
-      const int c = g_p ^ mf_swz(g_ri, rg);
-      const uint16_t* src = X + (size_t)row * D + s4 * 64 + c * 8;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src, (lds_ptr_t)(smem + slot * S::TILE_BYTES + (s4 * 4 + rg) * 1024),
-          16, 0, 0);
+      const int c16 = g_p ^ mf_swz(g_ri, rg);
+      const uint16_t* src = X + (size_t)row * D + (u * S::CS4 + s4l) * 64 + c16 * 8;
+      glds16(src, __builtin_amdgcn_readfirstlane(sb + (s4l * 4 + rg) * 1024));
     }
   };
 
-  // A operand read offsets: lane (r, h) reads row r, k-chunk 2u+h of piece s4.
+  // A operand read offsets: lane (r, h) reads row r, k-chunk 2u+h of a piece.
   int offu[4];
   {
     const int rg = r >> 3, ri = r & 7, sw = mf_swz(ri, rg);
@@ -602,64 +662,94 @@ __global__ __launch_bounds__(kMfThreads) void mfma_topk_kernel(
     for (int u = 0; u < 4; ++u) offu[u] = rg * 1024 + ri * 128 + (((2 * u + h) ^ sw) << 4);
   }
 
-  uint64_t th = 0;        // current k-th key of query ql (0 = list not full)
-  float th_s = -INFINITY; // its score
+  __syncthreads();  // lists initialised
+  for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
+    if (c < nchunks) issue(c);
 
-  if (ntiles > 0) issue(0, 0);
   for (uint32_t t = 0; t < ntiles; ++t) {
-    __syncthreads();  // tile t landed (each wave drained its own DMA), slot (t+1)&1 free
-    if (t + 1 < ntiles) issue(t + 1, (int)((t + 1) & 1));
-    const unsigned char* base = smem + (t & 1) * S::TILE_BYTES;
-    f32x16_t acc = {};
+    f32x16_t acc[2] = {{}, {}};
 #pragma unroll
-    for (int s = 0; s < S::S; ++s) {
-      const uint4 a = *(const uint4*)(base + (s >> 2) * 4096 + offu[s & 3]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), qf[s],
-                                                     acc, 0, 0, 0);
+    for (int u = 0; u < S::CPT; ++u) {
+      const uint32_t c = t * S::CPT + u;
+      // chunk c landed for this wave: at most AHEAD-1 younger chunks pending
+      if (c + S::AHEAD <= nchunks)
+        wait_vmcnt<S::PPW * (S::AHEAD - 1)>();
+      else
+        wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // chunk c visible to all; slot of chunk c-1 free
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + S::AHEAD < nchunks) issue(c + S::AHEAD);
+      const unsigned char* sb = smem + (c % S::NSLOT) * S::CHUNK_BYTES;
+      if constexpr (MODE != 2) {
+#pragma unroll
+        for (int s = 0; s < S::CK; ++s) {
+          const bf16x8_t a =
+              __builtin_bit_cast(bf16x8_t, *(const uint4*)(sb + (s >> 2) * 4096 + offu[s & 3]));
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][u * S::CK + s], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][u * S::CK + s], acc[1], 0, 0, 0);
+        }
+      }
     }
-    // epilogue: acc[i] = score(row trow0 + (i&3) + 8(i>>2) + 4h, query ql)
+    if constexpr (MODE == 1 || MODE == 2) {
+      asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][5]), "v"(acc[0][15]));
+      continue;
+    }
+    // epilogue: acc[g][i] = score(row trow0 + (i&3) + 8(i>>2) + 4h, query ql[g])
     const uint32_t trow0 = wr0 + t * 32;
-    float mx = -INFINITY;
+    const bool full = trow0 + 32 <= wr1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (row < wr1) mx = fmaxf(mx, acc[i]);
-    }
-    if (__any(qvalid && mx >= th_s)) {
+    for (int g = 0; g < 2; ++g) {
+      float mx = -INFINITY;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const bool p = qvalid && row < wr1 && acc[i] >= th_s;
-        if (__any(p)) {
-          for (int hh = 0; hh < 2; ++hh) {
-            if (p && h == hh) {
-              const uint64_t key = make_key(acc[i], row_base + row);
-              if (key > lists[(k - 1) * kMfmaQueries + ql]) {
-                int j = (int)k - 1;
-                while (j > 0) {
-                  const uint64_t prev = lists[(j - 1) * kMfmaQueries + ql];
-                  if (prev >= key) break;
-                  lists[j * kMfmaQueries + ql] = prev;
-                  --j;
+        if (full || row < wr1) mx = fmaxf(mx, acc[g][i]);
+      }
+      if (__any(qvalid[g] && mx >= th_s[g])) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const bool p = qvalid[g] && (full || row < wr1) && acc[g][i] >= th_s[g];
+          if (__any(p)) {
+            for (int hh = 0; hh < 2; ++hh) {
+              if (p && h == hh) {
+                const uint64_t key = make_key(acc[g][i], row_base + row);
+                const uint32_t q = ql[g];
+                if (key > th[g] && key > lists[(k - 1) * kMfmaQueries + q]) {
+                  int j = (int)k - 1;
+                  while (j > 0) {
+                    const uint64_t prev = lists[(j - 1) * kMfmaQueries + q];
+                    if (prev >= key) break;
+                    lists[j * kMfmaQueries + q] = prev;
+                    --j;
+                  }
+                  lists[j * kMfmaQueries + q] = key;
                 }
-                lists[j * kMfmaQueries + ql] = key;
               }
             }
+            const uint64_t kth = lists[(k - 1) * kMfmaQueries + ql[g]];
+            if (kth > th[g]) {
+              th[g] = kth;
+              th_s[g] = key_score(kth);
+            }
           }
-          th = lists[(k - 1) * kMfmaQueries + ql];
-          th_s = th ? key_score(th) : -INFINITY;
         }
       }
     }
   }
   // each wave owns its queries' lists: no barrier needed before the write-out
-  for (uint32_t j = h; j < k; j += 2)
-    out[((size_t)blockIdx.x * kMfmaQueries + ql) * k + j] = lists[j * kMfmaQueries + ql];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    for (uint32_t j = h; j < k; j += 2)
+      out[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * k + j] =
+          lists[j * kMfmaQueries + ql[g]];
 }
 
 bool mfma_supported(uint32_t dim) { return dim == 768 || dim == 512 || dim == 384 || dim == 256; }
 
-static void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg) {
+void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg) {
   const int cus = g_cu_count ? g_cu_count : device_cu_count();
   uint64_t want = (uint64_t)cus;
   const uint64_t tiles = ((uint64_t)n_rows + 31) / 32;
@@ -679,7 +769,8 @@ uint32_t mfma_max_lists(uint32_t n_rows) {
 }
 
 hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
-                       const uint16_t* Q, uint32_t nq_valid, uint32_t k, uint64_t* out,
+                       const uint16_t* Q, uint32_t nq_valid, uint32_t k, uint32_t max_tiles,
+                       const uint64_t* init_th, uint32_t init_stride, uint64_t* out,
                        uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
   if (k == 0 || k > kMfmaMaxK || n_rows == 0 || nq_valid == 0 || nq_valid > kMfmaQueries)
     return hipErrorInvalidValue;
@@ -688,27 +779,31 @@ hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_
   if (nwg > max_lists) return hipErrorInvalidValue;
   *nlists = nwg;
   dim3 grid(nwg), block(kMfThreads);
+#define VS_MFMA_CASE(DD)                                                                     \
+  case DD:                                                                                   \
+    if (max_tiles)                                                                           \
+      hipLaunchKernelGGL((mfma_topk_kernel<DD, 3>), grid, block, 0, st, X, n_rows, row_base, \
+                         rpw, max_tiles, Q, nq_valid, k, init_th, init_stride, out);         \
+    else                                                                                     \
+      hipLaunchKernelGGL((mfma_topk_kernel<DD, 0>), grid, block, 0, st, X, n_rows, row_base, \
+                         rpw, 0u, Q, nq_valid, k, init_th, init_stride, out);                \
+    break;
   switch (dim) {
-    case 768:
-      hipLaunchKernelGGL(mfma_topk_kernel<768>, grid, block, 0, st, X, n_rows, row_base, rpw,
-                         Q, nq_valid, k, out);
-      break;
-    case 512:
-      hipLaunchKernelGGL(mfma_topk_kernel<512>, grid, block, 0, st, X, n_rows, row_base, rpw,
-                         Q, nq_valid, k, out);
-      break;
-    case 384:
-      hipLaunchKernelGGL(mfma_topk_kernel<384>, grid, block, 0, st, X, n_rows, row_base, rpw,
-                         Q, nq_valid, k, out);
-      break;
-    case 256:
-      hipLaunchKernelGGL(mfma_topk_kernel<256>, grid, block, 0, st, X, n_rows, row_base, rpw,
-                         Q, nq_valid, k, out);
-      break;
+    VS_MFMA_CASE(768)
+    VS_MFMA_CASE(512)
+    VS_MFMA_CASE(384)
+    VS_MFMA_CASE(256)
     default:
       return hipErrorInvalidValue;
   }
+#undef VS_MFMA_CASE
   return hipGetLastError();
+}
+
+uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
+  uint32_t nwg, rpw;
+  mfma_grid(n_rows, &nwg, &rpw);
+  return (rpw + 31) / 32;
 }
 
 // ---------------------------------------------------------------------------

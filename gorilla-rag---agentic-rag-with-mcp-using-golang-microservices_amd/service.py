@@ -1,0 +1,104 @@
+"""ctypes binding of the vector-service handler mirror (include/vsearch_service.h).
+
+``VectorService.handle(method, path, body)`` answers exactly what
+rag/vector-service's Go handlers answer (main.go:121-278): same routes, JSON
+shapes, status codes and messages, with the HIP engine in place of Qdrant.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from typing import Optional, Tuple
+
+from .engine import HERE, VSError, _check, load_library
+
+SVC_LIB_PATH = os.path.join(HERE, "lib", "libvsearch_service.so")
+
+_svc = None
+
+
+def load_service_library(path: str = SVC_LIB_PATH):
+    global _svc
+    if _svc is not None:
+        return _svc
+    load_library()  # resolves libvsearch.so first (same directory)
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    vp, cp, sz = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t
+    L.vsvc_open.argtypes = [vp, cp, ctypes.POINTER(vp)]
+    L.vsvc_open.restype = ctypes.c_int
+    L.vsvc_close.argtypes = [vp]
+    L.vsvc_close.restype = None
+    L.vsvc_handle.argtypes = [vp, cp, cp, cp, sz, ctypes.POINTER(ctypes.c_int),
+                              ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(cp)]
+    L.vsvc_handle.restype = ctypes.c_int
+    L.vsvc_free.argtypes = [vp]
+    L.vsvc_free.restype = None
+    L.vsvc_reencode.argtypes = [cp, sz, ctypes.POINTER(vp)]
+    L.vsvc_reencode.restype = ctypes.c_int
+    L.vsvc_validate.argtypes = [cp, cp, sz, ctypes.POINTER(vp)]
+    L.vsvc_validate.restype = ctypes.c_int
+    _svc = L
+    return L
+
+
+def _take(L, p: ctypes.c_void_p, n: Optional[int] = None) -> bytes:
+    if not p.value:
+        return b""
+    data = ctypes.string_at(p.value, n) if n is not None else ctypes.string_at(p.value)
+    L.vsvc_free(p)
+    return data
+
+
+def reencode(doc: bytes) -> Tuple[int, bytes]:
+    """(0, Go json.Encoder output) or (-1, syntax error text)."""
+    L = load_service_library()
+    out = ctypes.c_void_p()
+    rc = L.vsvc_reencode(doc, len(doc), ctypes.byref(out))
+    return rc, _take(L, out)
+
+
+def validate(path: str, body: bytes) -> Tuple[int, str]:
+    """(400, decode error) or (0, '') for a /search or /upsert body."""
+    L = load_service_library()
+    out = ctypes.c_void_p()
+    rc = L.vsvc_validate(path.encode(), body, len(body), ctypes.byref(out))
+    return rc, _take(L, out).decode()
+
+
+class VectorService:
+    """rag/vector-service's four handlers over an engine (not owned)."""
+
+    def __init__(self, engine, config: Optional[dict] = None):
+        L = load_service_library()
+        h = ctypes.c_void_p()
+        cfg = json.dumps(config).encode() if config is not None else None
+        rc = L.vsvc_open(engine.handle, cfg, ctypes.byref(h))
+        if rc != 0:
+            _check(rc)
+        self._h, self._L, self.engine = h, L, engine
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.vsvc_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def handle(self, method: str, path: str, body: bytes = b"") -> Tuple[int, bytes, str]:
+        st = ctypes.c_int()
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        ct = ctypes.c_char_p()
+        rc = self._L.vsvc_handle(self._h, method.encode(), path.encode(), body, len(body),
+                                 ctypes.byref(st), ctypes.byref(out), ctypes.byref(n),
+                                 ctypes.byref(ct))
+        if rc != 0:
+            raise VSError(rc, "vsvc_handle failed")
+        return st.value, _take(self._L, out, n.value), ct.value.decode()

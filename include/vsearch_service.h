@@ -1,0 +1,66 @@
+/*
+ * vsearch_service.h — host-side mirror of rag/vector-service's HTTP handlers
+ * over the engine C-ABI (include/vsearch.h).
+ *
+ * The reference service is Go (rag/vector-service/main.go); no Go toolchain
+ * exists in this build image, so the handler logic is restated in C++ with
+ * the same routes, JSON shapes, status codes and error texts:
+ *
+ *   GET  /health       healthHandler       main.go:121-136
+ *   GET  /collections  collectionsHandler  main.go:138-147
+ *   POST /upsert       upsertHandler       main.go:149-225
+ *   POST /search       searchHandler       main.go:227-278
+ *
+ * Point UUIDs and payloads live here (a UUID -> row map and a row-indexed
+ * payload store per collection); the engine sees dense rows only. A Go
+ * deployment binds the same engine C-ABI through cgo and
+ * keeps this logic in Go; this library is the drop-in for hosts without Go
+ * and the executable specification the parity tests run against.
+ */
+#ifndef VSEARCH_SERVICE_H_
+#define VSEARCH_SERVICE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vsearch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vsvc vsvc;
+
+/* Creates the service over `eng` (not owned). `config_json` may be NULL for
+ * the reference defaults (initializeCollections, main.go:80-119: collections
+ * regulatory_docs, merchant_docs, kyc_docs, dim 768, Cosine, fp32) or
+ * {"collections":[{"name":"..","dim":768,"metric":"Cosine"|"Dot",
+ *  "dtype":"f32"|"bf16"}...]}. Existing collections are reused. */
+int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out);
+void vsvc_close(vsvc* svc);
+
+/* Serves one HTTP request. Sets *status, *body (malloc'd, NUL-terminated;
+ * free with vsvc_free) and *content_type (static string). Safe to call from
+ * many threads at once. Returns VS_OK, or a negative vs_status if the
+ * arguments are unusable. */
+int vsvc_handle(vsvc* svc, const char* method, const char* path, const char* body,
+                size_t body_len, int* status, char** resp, size_t* resp_len,
+                const char** content_type);
+void vsvc_free(char* p);
+
+/* Pure helpers exposed for tests (no engine needed). */
+/* Re-encodes a JSON document the way Go's json.Encoder writes a decoded
+ * interface{} (sorted keys, shortest floats, HTML escaping, trailing '\n').
+ * Returns 0, or -1 with *out = the syntax error text. */
+int vsvc_reencode(const char* json, size_t len, char** out);
+/* Validates a /search or /upsert body exactly as the handler's decode step
+ * does, without touching the engine. Returns the HTTP status the handler
+ * would answer for a malformed body (400) or 0 when the body decodes;
+ * *msg (malloc'd) gets the error text or "". */
+int vsvc_validate(const char* path, const char* body, size_t len, char** msg);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSEARCH_SERVICE_H_ */

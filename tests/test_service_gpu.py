@@ -1,0 +1,186 @@
+"""vector-service handler mirror end to end on the device: /upsert then /search
+through the same JSON the reference exchanges (ingest-service storeVectors,
+rag/ingest-service/main.go:359-393; retrieval-service searchVectorDB,
+rag/retrieval-service/main.go:219-276), checked against the oracle.
+
+Config 1 of BASELINE.json (regulatory_docs, ~220 chunk embeddings, top_k 5)
+is exercised with synthetic 768-d vectors in place of the Gemini embeddings
+(not reproducible offline)."""
+import json
+import threading
+import uuid
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def svcmod(pkg):
+    from importlib import import_module
+    return import_module(pkg.__name__ + ".service")
+
+
+@pytest.fixture()
+def service(pkg, svcmod):
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng)  # reference defaults: 3 x 768 Cosine collections
+    yield s
+    s.close()
+    eng.close()
+
+
+def _post(s, path, obj):
+    st, body, ct = s.handle("POST", path, json.dumps(obj).encode())
+    return st, body, ct
+
+
+def _ids(n, seed=0):
+    rng = np.random.default_rng(seed)
+    return [str(uuid.UUID(bytes=rng.bytes(16), version=4)) for _ in range(n)]
+
+
+def test_routes_and_methods(service):
+    st, body, ct = service.handle("GET", "/health")
+    h = json.loads(body)
+    assert st == 200 and h["status"] == "healthy" and h["service"] == "vector-service"
+    assert list(h) == sorted(h) and body.endswith(b"\n")
+    st, body, ct = service.handle("GET", "/collections")
+    assert st == 200 and body == b'{"collections":["regulatory_docs","merchant_docs","kyc_docs"]}\n'
+    for path in ("/collections",):
+        st, body, ct = service.handle("POST", path)
+        assert (st, body, ct) == (405, b"Method not allowed\n", "text/plain; charset=utf-8")
+    for path in ("/upsert", "/search"):
+        st, body, ct = service.handle("GET", path)
+        assert (st, body) == (405, b"Method not allowed\n")
+    st, body, ct = service.handle("GET", "/nope")
+    assert (st, body) == (404, b"404 page not found\n")
+
+
+def test_config1_regulatory_docs(service, orc):
+    """~220 chunk vectors upserted as ingest-service does, searched top_k 5."""
+    n, dim = 220, 768
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim) * 3.0  # not unit: exercises the cosine preprocess
+    ids = _ids(n)
+    for lo in range(0, n, 100):  # ingest batches
+        pts = [{"id": ids[i], "vector": X[i].tolist(),
+                "payload": {"text": f"chunk <{i}> & more", "document_id": "doc-1", "position": i}}
+               for i in range(lo, min(n, lo + 100))]
+        st, body, _ = _post(service, "/upsert", {"collection": "regulatory_docs", "points": pts})
+        assert st == 200, body
+        assert json.loads(body) == {"collection": "regulatory_docs", "points": len(pts),
+                                    "status": "success"}
+    Q = orc.generate(orc.SEED_QUERY, 0, 8, dim)
+    Xp = orc.preprocess(X, True)
+    for qi in range(8):
+        # the query goes over the wire as JSON numbers decoded straight to float32
+        st, body, _ = _post(service, "/search", {"collection": "regulatory_docs",
+                                                 "query": Q[qi].tolist(), "top_k": 5,
+                                                 "filter": {}})
+        assert st == 200, body
+        assert body.endswith(b"\n")
+        res = json.loads(body)
+        assert res["count"] == 5 and len(res["results"]) == 5
+        assert list(res["results"][0]) == ["id", "score", "payload"]
+        rows = np.array([[ids.index(r["id"]) for r in res["results"]]], np.uint64)
+        scores = np.array([[r["score"] for r in res["results"]]])
+        qp = orc.preprocess(Q[qi:qi + 1], True)
+        s32, s64, rr, cc = orc.search(Xp, qp, 5)
+        resc = orc.rescore(Xp, qp, rows, np.array([5], np.uint32))
+        assert not orc.check_topk(scores, rows, np.array([5]), s64, rr, cc, resc, 1e-5)
+        # score is float64(float32): exactly representable as f32
+        assert all(np.float64(np.float32(x)) == x for x in scores[0])
+        top = res["results"][0]
+        i = ids.index(top["id"])
+        assert top["payload"] == {"document_id": "doc-1", "position": i,
+                                  "text": f"chunk <{i}> & more"}
+    # raw bytes: payload keys sorted, HTML escaped
+    assert b'"payload":{"document_id":"doc-1","position":' in body
+    assert b"\\u003c" in body and b"\\u0026" in body
+
+
+def test_default_topk_and_overwrite(service, orc):
+    dim = 768
+    X = orc.generate(7, 0, 12, dim)
+    ids = _ids(12, seed=3)
+    _post(service, "/upsert", {"collection": "kyc_docs",
+                               "points": [{"id": ids[i], "vector": X[i].tolist()} for i in range(12)]})
+    st, body, _ = _post(service, "/search", {"collection": "kyc_docs", "query": X[4].tolist()})
+    res = json.loads(body)
+    assert res["count"] == 5 and res["results"][0]["id"] == ids[4]   # TopK 0 -> 5
+    assert res["results"][0]["payload"] == {}
+    # overwrite point 4 by id (upper-case UUID input, canonical lower-case output)
+    st, body, _ = _post(service, "/upsert", {"collection": "kyc_docs", "points": [
+        {"id": ids[4].upper(), "vector": (-X[4]).tolist(), "payload": {"v": 2}}]})
+    assert st == 200
+    st, body, _ = _post(service, "/search", {"collection": "kyc_docs", "query": X[4].tolist(),
+                                             "top_k": 12})
+    res = json.loads(body)
+    assert res["count"] == 12
+    assert res["results"][-1]["id"] == ids[4] and res["results"][-1]["payload"] == {"v": 2}
+    assert abs(res["results"][-1]["score"] + 1.0) < 1e-5
+
+
+def test_errors(service):
+    up = lambda pts, coll="merchant_docs": _post(service, "/upsert", {"collection": coll, "points": pts})
+    assert up([{"id": 5, "vector": [0.0] * 768}]) == (400, b'{"error":"Point ID must be a string"}\n',
+                                                       "application/json")
+    assert up([{"id": "x"}])[:2] == (400, b'{"error":"Point vector must be provided"}\n')
+    assert up([{"id": "x", "vector": "no"}])[:2] == (400, b'{"error":"point vector must be an array"}\n')
+    assert up([{"id": "x", "vector": [1, "a"]}])[:2] == (400, b'{"error":"vector contains non-numeric value"}\n')
+    assert _post(service, "/upsert", {"points": []})[:2] == (400, b'{"error":"Collection name required"}\n')
+    st, body, _ = service.handle("POST", "/upsert", b"{bad")
+    assert (st, body) == (400, b'{"error":"Invalid request body"}\n')
+    st, body, _ = up([{"id": "not-a-uuid", "vector": [0.0] * 768}])
+    assert st == 500 and body.startswith(b'{"error":"Failed to upsert: ')
+    st, body, _ = up([{"id": _ids(1)[0], "vector": [0.1, 0.2, 0.3]}])
+    assert st == 500 and b"expected dim: 768, got 3" in body
+    st, body, _ = up([{"id": _ids(1)[0], "vector": [0.0] * 768}], coll="nope")
+    assert st == 500 and b"Not found: Collection `nope` doesn't exist!" in body
+    # README.md:725-738's 3-d probe against a 768-d collection: an engine error, not results
+    st, body, _ = _post(service, "/search", {"collection": "regulatory_docs", "query": [0.1, 0.2, 0.3],
+                                             "top_k": 1})
+    assert st == 500 and body.startswith(b'{"error":"Search failed: ')
+    st, body, _ = _post(service, "/search", {"collection": "nope", "query": [0.0] * 768})
+    assert st == 500 and b"Not found" in body
+    st, body, _ = service.handle("POST", "/search", b'{"query":"x"}')
+    assert (st, body) == (400, b'{"error":"Invalid request body"}\n')
+    # empty collection: results is [] (make([]SearchResult, 0)), not null
+    st, body, _ = _post(service, "/search", {"collection": "merchant_docs", "query": [0.5] * 768})
+    assert (st, body) == (200, b'{"results":[],"count":0}\n')
+
+
+def test_concurrent_search_and_upsert(service, orc):
+    dim = 768
+    X = orc.generate(11, 0, 400, dim)
+    ids = _ids(400, seed=9)
+    _post(service, "/upsert", {"collection": "merchant_docs",
+                               "points": [{"id": ids[i], "vector": X[i].tolist()} for i in range(200)]})
+    errors = []
+
+    def searcher(t):
+        for j in range(10):
+            q = X[(t * 10 + j) % 200]
+            st, body, _ = _post(service, "/search", {"collection": "merchant_docs",
+                                                     "query": q.tolist(), "top_k": 3})
+            r = json.loads(body)
+            if st != 200 or r["results"][0]["id"] != ids[(t * 10 + j) % 200]:
+                errors.append((t, j, st, body[:200]))
+
+    def upserter():
+        for lo in range(200, 400, 50):
+            st, body, _ = _post(service, "/upsert", {"collection": "merchant_docs", "points": [
+                {"id": ids[i], "vector": X[i].tolist()} for i in range(lo, lo + 50)]})
+            if st != 200:
+                errors.append(("up", st, body))
+
+    th = [threading.Thread(target=searcher, args=(t,)) for t in range(6)] + [threading.Thread(target=upserter)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]
+    st, body, _ = _post(service, "/search", {"collection": "merchant_docs", "query": X[399].tolist(),
+                                             "top_k": 1})
+    assert json.loads(body)["results"][0]["id"] == ids[399]
