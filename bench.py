@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
-    ap.add_argument("--cpu-sample-queries", type=int, default=32)
+    ap.add_argument("--cpu-sample-queries", type=int, default=320)
     return ap.parse_args()
 
 

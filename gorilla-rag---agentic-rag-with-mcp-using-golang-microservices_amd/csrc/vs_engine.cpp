@@ -129,18 +129,26 @@ hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
   return hipEventRecord(v.back().b, eng->stream);
 }
 
+// Rows allocated past the capacity: the MFMA scan streams whole 32-row tiles
+// and reads (then masks) up to 31 rows beyond the last one.
+constexpr uint64_t kPadRows = 32;
+
 // Grows a collection to hold `need` rows (writer lock held by the caller).
 int grow(vs_engine* eng, Collection& c, uint64_t need) {
   if (need <= c.cap) return VS_OK;
   uint64_t ncap = std::max<uint64_t>({need, c.cap + c.cap / 2, 1024});
   void* nd = nullptr;
-  hipError_t e = hipMalloc(&nd, ncap * c.row_bytes());
+  hipError_t e = hipMalloc(&nd, (ncap + kPadRows) * c.row_bytes());
   if (e != hipSuccess) {
     // exact fit as a last resort
     ncap = need;
-    e = hipMalloc(&nd, ncap * c.row_bytes());
+    e = hipMalloc(&nd, (ncap + kPadRows) * c.row_bytes());
     if (e != hipSuccess) return fail_hip(e, "collection grow");
   }
+  // zero the padding so masked tail rows are finite
+  VS_HIP(hipMemsetAsync((char*)nd + ncap * c.row_bytes(), 0, kPadRows * c.row_bytes(),
+                        eng->stream),
+         "pad rows");
   if (c.data && c.rows) {
     VS_HIP(hipMemcpyAsync(nd, c.data, c.rows * c.row_bytes(), hipMemcpyDeviceToDevice,
                           eng->stream),

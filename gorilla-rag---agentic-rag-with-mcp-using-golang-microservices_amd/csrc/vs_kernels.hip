@@ -27,6 +27,7 @@ using vs::key_score;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) volatile uint64_t lds_vu64_t;
 
 // ---------------------------------------------------------------------------
 // wave helpers (wave64)
@@ -516,34 +517,46 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // ---------------------------------------------------------------------------
 // batched bf16 scan on MFMA + fused top-k
 // ---------------------------------------------------------------------------
-// Workgroup = 4 waves, one per SIMD (512-VGPR budget each); wave w owns
-// queries [64w, 64w+64) as two MFMA column groups of 32 and keeps their
-// B-operand fragments for the whole row (2 x D/16 k-steps x 4 VGPRs) resident
-// in registers. The workgroup streams its contiguous row range HBM -> LDS once,
-// by global_load_lds (1 KiB pieces = 8 rows x 128 B), through a ring of
-// K-chunks (32 rows x 256 k = 16 KiB); AHEAD chunks stay in flight across the
-// raw s_barrier that publishes each chunk (counted vmcnt, never a drain inside
-// the loop). Each A fragment read from LDS (ds_read_b128) feeds two
-// v_mfma_f32_32x32x16_bf16, one per query group, into two 32x32 accumulators
-// per 32-row tile (C[row][query], query = lane & 31). The tile epilogue
-// filters the 16 scores per lane and group against the query's current
-// threshold key and inserts survivors into a per-query sorted list in LDS.
-// Scores never reach HBM.
+// Workgroup = 8 waves, two per SIMD; wave w owns queries [32w, 32w+32) as
+// two 16-query column groups of v_mfma_f32_16x16x32_bf16 and keeps their
+// B-operand fragments for the whole row (2 x D/32 k-steps x 4 VGPRs = 192 at
+// D = 768) resident in registers. The workgroup streams its contiguous row
+// range HBM -> LDS once, by global_load_lds (1 KiB pieces = 8 rows x 128 B),
+// through a ring of K-chunks (32 rows x 256 k = 16 KiB); AHEAD chunks stay in
+// flight across the raw s_barrier that publishes each chunk (counted vmcnt,
+// never a drain inside the loop). Per 32-k step a wave reads two A fragments
+// (rows 0-15 and 16-31 of the tile, ds_read_b128) and each feeds both query
+// groups: 4 MFMAs per 2 LDS reads. Two waves per SIMD let one wave's LDS-DMA
+// issue, LDS latency and top-k epilogue hide under the partner's MFMAs.
+// The tile epilogue filters each lane's 8 scores per group against the
+// query's threshold key and inserts survivors into a per-query sorted list in
+// LDS. Scores never reach HBM.
 //
 // Threshold: max(the list's own k-th key, init_th[q] - 1). init_th is the
 // k-th key of an exact top-k over a sample of the same rows (the "sample
 // pass"): every row outside the final top-k of the sample
 // ranks below it, so it is a lower bound on the global k-th key and rows
 // under it can never enter the result. It cuts the insert traffic ~25x.
-constexpr int kMfThreads = 256;
+constexpr int kMfThreads = 512;
 constexpr int kMfWaves = kMfThreads / 64;
 constexpr int kMfLists = (int)kMfmaMaxK * (int)kMfmaQueries;  // LDS list entries
 constexpr int kMfRingBytes = 112 * 1024;
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 // XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
-// ds_read_b128 lane groups over all 64 banks (conflict-free).
+// ds_read_b128 lane groups of the 16x16x32 A fragment over all 64 banks
+// (conflict-free, measured SQ_LDS_BANK_CONFLICT = 0).
 __device__ __forceinline__ int mf_swz(int ri, int rg) {
   return ((ri >> 1) & 3) | ((rg & 1) << 2);
+}
+
+// v_max3_f32 without the canonicalising v_max hipcc adds around fmaxf on
+// MFMA results (scores are finite).
+__device__ __forceinline__ float fmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
 template <int N>
@@ -556,36 +569,39 @@ __device__ __forceinline__ void wait_vmcnt() {
 // pass does not see an LDS store and cannot drain vmcnt before every
 // ds_read of the ring; completion is counted by wait_vmcnt<N>() by hand.
 // M0 is written and restored inside the statement (§5.7: M0 is reserved).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+// Address = wave-uniform 64-bit base (SGPRs) + per-lane 32-bit byte offset.
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds) {
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gsrc), "s"(lds)
+      : "v"(voff), "s"(sbase), "s"(lds)
       : "memory");
 }
 
 template <int D>
 struct MfShape {
-  static constexpr int S = D / 16;                        // MFMA k-steps per row
+  static constexpr int T = D / 32;                        // 32-k MFMA steps per row
   static constexpr int CS4 = (D % 256 == 0) ? 4 : 2;      // 128-B pieces per row per chunk
-  static constexpr int CK = CS4 * 4;                      // MFMA k-steps per chunk
+  static constexpr int CT = CS4 * 2;                      // 32-k steps per chunk
   static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
   static constexpr int CHUNK_BYTES = CS4 * 4 * 1024;      // 32 rows x CS4*128 B
   static constexpr int NSLOT = kMfRingBytes / CHUNK_BYTES;
   static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
   static constexpr int PPW = CS4 * 4 / kMfWaves;          // LDS-DMA pieces per wave per chunk
   static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + kMfLists * 8;
-  static_assert(D % 128 == 0, "MFMA scan needs D % 128 == 0");
+  static_assert(D % 256 == 0 || D % 128 == 0, "MFMA scan needs D % 128 == 0");
+  static_assert(PPW >= 1, "one LDS-DMA piece per wave at least");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
 // MODE: 0 = main pass; 3 = sample pass (same code, separate symbol so the
-// two launches are told apart in rocprof); 1/2 = ablation builds only
-// (tools/ablate_mfma.hip): 1 = no top-k epilogue, 2 = LDS-DMA stream only.
+// two launches are told apart in rocprof); ablation builds only
+// (tools/ablate_mfma.hip): 1 = no top-k epilogue, 2 = LDS-DMA stream only,
+// 4 = MFMA + LDS reads + barriers with no DMA, 5 = 4 without barriers.
 template <int D, int MODE = 0>
-__global__ __launch_bounds__(kMfThreads, 1) void mfma_topk_kernel(
+__global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(
     const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t row_base,
     uint32_t rows_per_wg, uint32_t max_tiles, const uint16_t* __restrict__ Q,
     uint32_t nq_valid, uint32_t k, const uint64_t* __restrict__ init_th, uint32_t init_stride,
@@ -594,15 +610,18 @@ __global__ __launch_bounds__(kMfThreads, 1) void mfma_topk_kernel(
   // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
-  // The two lanes of a query (h = 0, 1) hand list entries to each other
-  // through LDS inside one wave with no barrier: volatile keeps every access
-  // in program order (a wave's DS instructions execute in order), so the
-  // compiler cannot forward a stale entry across the two insert passes.
-  volatile uint64_t* lists = (volatile uint64_t*)(smem + S::NSLOT * S::CHUNK_BYTES);
+  // The four lanes of a query hand list entries to each other through LDS
+  // inside one wave with no barrier: volatile keeps every access in program
+  // order (a wave's DS instructions execute in order), so the compiler cannot
+  // forward a stale entry across the insert passes.
+  // The pointer must stay in the LDS address space: a generic volatile pointer
+  // becomes flat_load/flat_store + vmcnt(0), which drains the DMA ring.
+  lds_vu64_t* lists = (lds_vu64_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, h = lane >> 5;
+  const int col = lane & 15;  // MFMA column (query in group) / A-fragment row
+  const int kq = lane >> 4;   // 8-element k slice; C rows 4kq .. 4kq+3
   const uint32_t wr0 = blockIdx.x * rows_per_wg;
   const uint32_t wr1 = (uint64_t)wr0 + rows_per_wg < n_rows ? wr0 + rows_per_wg : n_rows;
   uint32_t ntiles = (wr1 - wr0 + 31) / 32;
@@ -611,140 +630,182 @@ __global__ __launch_bounds__(kMfThreads, 1) void mfma_topk_kernel(
 
   for (int i = threadIdx.x; i < kMfLists; i += kMfThreads) lists[i] = 0;
 
-  // B operand of group g: Q[query 64w+32g+r][16s + 8h + j], j = 0..7.
-  bf16x8_t qf[2][S::S];
+  // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
+  bf16x8_t qf[2][S::T];
   uint32_t ql[2];
   bool qvalid[2];
-  uint64_t thi[2], th[2];
+  uint64_t th[2];
   float th_s[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    ql[g] = (uint32_t)(w * 64 + g * 32 + r);
+    ql[g] = (uint32_t)(w * 32 + g * 16 + col);
     qvalid[g] = ql[g] < nq_valid;
     const uint4* qrow = (const uint4*)(Q + (size_t)ql[g] * D);
 #pragma unroll
-    for (int s = 0; s < S::S; ++s) qf[g][s] = __builtin_bit_cast(bf16x8_t, qrow[2 * s + h]);
+    for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
     const uint64_t it = (init_th && qvalid[g]) ? init_th[(size_t)ql[g] * init_stride] : 0;
-    thi[g] = it ? it - 1 : 0;  // admit the bound itself ("key > th")
-    th[g] = thi[g];
+    th[g] = it ? it - 1 : 0;  // admit the bound itself ("key > th")
     th_s[g] = it ? key_score(it) : -INFINITY;
   }
 
   // LDS-DMA source mapping: piece (s4l, rg) of a chunk holds rows rg*8 ..
   // rg*8+7, bytes [128*s4, 128*s4+128) of each; lane -> (row lane>>3,
-  // 16-B position lane&7 holding chunk (lane&7) ^ swz). Wave w loads row
-  // group w of every piece column.
-  const int g_ri = lane >> 3;
-  const int g_p = lane & 7;
+  // 16-B position lane&7 holding chunk (lane&7) ^ swz). The per-lane part of
+  // each piece's address is a loop-invariant 32-bit offset; the per-chunk part
+  // is a scalar base. Tiles past the last row read the collection's 32 rows
+  // of allocation padding (vs_engine.cpp grow()) and are masked in the
+  // epilogue.
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  uint32_t loff[S::PPW];
+#pragma unroll
+  for (int i = 0; i < S::PPW; ++i) {
+    const int b = w + kMfWaves * i;
+    const int s4l = b >> 2, rg = b & 3;
+    const int g_ri = lane >> 3, c16 = (lane & 7) ^ mf_swz(g_ri, rg);
+    loff[i] = (uint32_t)(((rg * 8 + g_ri) * D + s4l * 64 + c16 * 8) * 2);
+  }
+  const unsigned char* xw = (const unsigned char*)(X + (size_t)wr0 * D);
   auto issue = [&](uint32_t c) {
     const uint32_t t = c / S::CPT;
-    const int u = (int)(c - t * S::CPT);
-    const uint32_t trow0 = wr0 + t * 32;
+    const uint32_t u = c - t * S::CPT;
+    const unsigned char* base = xw + ((size_t)t * 32 * D + u * S::CS4 * 64) * 2;
     const uint32_t sb = lds_base + (c % S::NSLOT) * S::CHUNK_BYTES;
 #pragma unroll
     for (int i = 0; i < S::PPW; ++i) {
       const int b = w + kMfWaves * i;
       const int s4l = b >> 2, rg = b & 3;
-      uint32_t row = trow0 + rg * 8 + g_ri;
-      row = row < n_rows ? row : n_rows - 1;
-      const int c16 = g_p ^ mf_swz(g_ri, rg);
-      const uint16_t* src = X + (size_t)row * D + (u * S::CS4 + s4l) * 64 + c16 * 8;
-      glds16(src, __builtin_amdgcn_readfirstlane(sb + (s4l * 4 + rg) * 1024));
+      glds16(base, loff[i], __builtin_amdgcn_readfirstlane(sb + (s4l * 4 + rg) * 1024));
     }
   };
 
-  // A operand read offsets: lane (r, h) reads row r, k-chunk 2u+h of a piece.
-  int offu[4];
-  {
-    const int rg = r >> 3, ri = r & 7, sw = mf_swz(ri, rg);
+  // A operand read offsets: half hr (tile rows 16hr..16hr+15), lane reads row
+  // 16hr + col, 16-B chunk 4*(t&1) + kq of piece t>>1.
+  int off[2][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) offu[u] = rg * 1024 + ri * 128 + (((2 * u + h) ^ sw) << 4);
+  for (int hr = 0; hr < 2; ++hr) {
+    const int rr = 16 * hr + col, rg = rr >> 3, ri = rr & 7, sw = mf_swz(ri, rg);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) off[hr][tt] = rg * 1024 + ri * 128 + (((4 * tt + kq) ^ sw) << 4);
   }
+
+  auto lds_a = [&](const unsigned char* sb, int s, int hr) -> bf16x8_t {
+    return __builtin_bit_cast(bf16x8_t, *(const uint4*)(sb + (s >> 1) * 4096 + off[hr][s & 1]));
+  };
 
   __syncthreads();  // lists initialised
   for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
-    if (c < nchunks) issue(c);
+    if (c < nchunks && MODE < 4) issue(c);
+  // publish chunk 0
+  if ((uint32_t)S::AHEAD <= nchunks)
+    wait_vmcnt<S::PPW * (S::AHEAD - 1)>();
+  else
+    wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
 
+  // Chunk c is published one barrier early (at c-1), so its first A fragments
+  // are read before the barrier that publishes chunk c+1: the LDS latency at
+  // the head of every chunk hides under that barrier instead of stalling the
+  // first MFMAs of all eight lock-stepped waves.
   for (uint32_t t = 0; t < ntiles; ++t) {
-    f32x16_t acc[2] = {{}, {}};
+    f32x4_t acc[2][2] = {{{}, {}}, {{}, {}}};  // [row half][query group]
 #pragma unroll
     for (int u = 0; u < S::CPT; ++u) {
       const uint32_t c = t * S::CPT + u;
-      // chunk c landed for this wave: at most AHEAD-1 younger chunks pending
-      if (c + S::AHEAD <= nchunks)
-        wait_vmcnt<S::PPW * (S::AHEAD - 1)>();
-      else
-        wait_vmcnt<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // chunk c visible to all; slot of chunk c-1 free
-      __builtin_amdgcn_sched_barrier(0);
-      if (c + S::AHEAD < nchunks) issue(c + S::AHEAD);
       const unsigned char* sb = smem + (c % S::NSLOT) * S::CHUNK_BYTES;
+      bf16x8_t a0, a1;
+      if constexpr (MODE != 2) {
+        a0 = lds_a(sb, 0, 0);
+        a1 = lds_a(sb, 0, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
+      if constexpr (MODE < 4) {
+        if (c + S::AHEAD <= nchunks)
+          wait_vmcnt<S::PPW * (S::AHEAD - 2)>();
+        else
+          wait_vmcnt<0>();
+      }
+      if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
+      __builtin_amdgcn_sched_barrier(0);
+      if (MODE < 4 && c + S::AHEAD < nchunks) issue(c + S::AHEAD);
       if constexpr (MODE != 2) {
 #pragma unroll
-        for (int s = 0; s < S::CK; ++s) {
-          const bf16x8_t a =
-              __builtin_bit_cast(bf16x8_t, *(const uint4*)(sb + (s >> 2) * 4096 + offu[s & 3]));
-          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][u * S::CK + s], acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][u * S::CK + s], acc[1], 0, 0, 0);
+        for (int s = 0; s < S::CT; ++s) {
+#pragma unroll
+          for (int hr = 0; hr < 2; ++hr) {
+            const bf16x8_t a = s == 0 ? (hr == 0 ? a0 : a1) : lds_a(sb, s, hr);
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+              acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[g][u * S::CT + s],
+                                                                   acc[hr][g], 0, 0, 0);
+          }
         }
       }
     }
-    if constexpr (MODE == 1 || MODE == 2) {
-      asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][5]), "v"(acc[0][15]));
+    if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) {
+      asm volatile("" ::"v"(acc[0][0][0]), "v"(acc[1][1][3]), "v"(acc[0][1][2]),
+                   "v"(acc[1][0][1]));
       continue;
     }
-    // epilogue: acc[g][i] = score(row trow0 + (i&3) + 8(i>>2) + 4h, query ql[g])
+    // epilogue: acc[hr][g][i] = score(row trow0 + 16hr + 4kq + i, query ql[g])
     const uint32_t trow0 = wr0 + t * 32;
     const bool full = trow0 + 32 <= wr1;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       float mx = -INFINITY;
+      if (full) {
+        mx = fmax3(fmax3(acc[0][g][0], acc[0][g][1], acc[0][g][2]),
+                   fmax3(acc[0][g][3], acc[1][g][0], acc[1][g][1]),
+                   fmax3(acc[1][g][2], acc[1][g][3], -INFINITY));
+      } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (full || row < wr1) mx = fmaxf(mx, acc[g][i]);
+        for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t row = trow0 + 16 * hr + 4 * kq + i;
+            if (row < wr1 && acc[hr][g][i] > mx) mx = acc[hr][g][i];
+          }
       }
       if (__any(qvalid[g] && mx >= th_s[g])) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t row = trow0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          const bool p = qvalid[g] && (full || row < wr1) && acc[g][i] >= th_s[g];
-          if (__any(p)) {
-            for (int hh = 0; hh < 2; ++hh) {
-              if (p && h == hh) {
-                const uint64_t key = make_key(acc[g][i], row_base + row);
-                const uint32_t q = ql[g];
-                if (key > th[g] && key > lists[(k - 1) * kMfmaQueries + q]) {
-                  int j = (int)k - 1;
-                  while (j > 0) {
-                    const uint64_t prev = lists[(j - 1) * kMfmaQueries + q];
-                    if (prev >= key) break;
-                    lists[j * kMfmaQueries + q] = prev;
-                    --j;
+        for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t row = trow0 + 16 * hr + 4 * kq + i;
+            const bool p = qvalid[g] && (full || row < wr1) && acc[hr][g][i] >= th_s[g];
+            if (__any(p)) {
+              for (int pp = 0; pp < 4; ++pp) {
+                if (p && kq == pp) {
+                  const uint64_t key = make_key(acc[hr][g][i], row_base + row);
+                  const uint32_t q = ql[g];
+                  if (key > th[g] && key > lists[(k - 1) * kMfmaQueries + q]) {
+                    int j = (int)k - 1;
+                    while (j > 0) {
+                      const uint64_t prev = lists[(j - 1) * kMfmaQueries + q];
+                      if (prev >= key) break;
+                      lists[j * kMfmaQueries + q] = prev;
+                      --j;
+                    }
+                    lists[j * kMfmaQueries + q] = key;
                   }
-                  lists[j * kMfmaQueries + q] = key;
                 }
               }
-            }
-            const uint64_t kth = lists[(k - 1) * kMfmaQueries + ql[g]];
-            if (kth > th[g]) {
-              th[g] = kth;
-              th_s[g] = key_score(kth);
+              const uint64_t kth = lists[(k - 1) * kMfmaQueries + ql[g]];
+              if (kth > th[g]) {
+                th[g] = kth;
+                th_s[g] = key_score(kth);
+              }
             }
           }
-        }
       }
     }
   }
   // each wave owns its queries' lists: no barrier needed before the write-out
 #pragma unroll
   for (int g = 0; g < 2; ++g)
-    for (uint32_t j = h; j < k; j += 2)
-      out[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * k + j] =
-          lists[j * kMfmaQueries + ql[g]];
+    for (uint32_t j = kq; j < k; j += 4)
+      out[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * k + j] = lists[j * kMfmaQueries + ql[g]];
 }
 
 bool mfma_supported(uint32_t dim) { return dim == 768 || dim == 512 || dim == 384 || dim == 256; }
