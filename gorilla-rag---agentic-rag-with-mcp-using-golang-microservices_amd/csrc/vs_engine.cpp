@@ -95,6 +95,8 @@ struct vs_engine {
   std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
+  DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
+  DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
   std::vector<uint64_t> h_keys;
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
@@ -193,20 +195,40 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     const uint32_t P = vsk::kMfmaQueries;
     const uint32_t npass = (nq + P - 1) / P;
     const uint32_t maxl = vsk::mfma_max_lists(n_rows);
+    const uint32_t cap = vsk::kMfmaCandCap;
     const size_t lbytes = (size_t)maxl * P * k * 8;
     const size_t bbytes = (size_t)P * dim * 2;
     const size_t sbytes = (size_t)P * k * 8;
+    const size_t cbytes = (size_t)maxl * P * cap * 8;
+    const size_t nbytes = (size_t)maxl * P * 4;
     if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes ||
-        eng->sample_keys.bytes < sbytes) {
+        eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
+        eng->cand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
       VS_HIP(hipStreamSynchronize(eng->stream), "sync");
       VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
       VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
       VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
+      VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
+      VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
+      VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
+      if (eng->fallbacks.bytes < 4) {
+        VS_HIP(eng->fallbacks.ensure(4), "alloc fallback counter");
+        VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
+      }
     }
+    const uint16_t* X = (const uint16_t*)c.data;
+    uint64_t* lists = eng->lists.as<uint64_t>();
+    uint32_t* ovf = eng->overflow.as<uint32_t>();
+    // The candidate pass needs a lower bound from the sample pass: a few
+    // tiles per workgroup at least. Small collections (< 8 tiles per
+    // workgroup) take the sorted-list pass directly.
+    const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
+    const bool fast = tpw >= 8;
     for (uint32_t p = 0; p < npass; ++p) {
       const uint32_t q0 = p * P;
       const uint32_t nv = std::min(P, nq - q0);
       uint16_t* qb = eng->q_bf16.as<uint16_t>();
+      uint64_t* out = d_keys + (size_t)q0 * k;
       if (nv < P)
         VS_HIP(hipMemsetAsync(qb + (size_t)nv * dim, 0, (size_t)(P - nv) * dim * 2,
                               eng->stream),
@@ -214,32 +236,49 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
       VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
              "queries to bf16");
       uint32_t L = 0;
-      // sample pass: exact top-k over the first 1/64 of every workgroup's
-      // tiles; its k-th key per query lower-bounds the global k-th key
-      const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
-      const uint64_t* init = nullptr;
-      if (tpw >= 64) {
-        uint64_t* skeys = eng->sample_keys.as<uint64_t>();
-        VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k,
-                                tpw / 64, nullptr, 0, eng->lists.as<uint64_t>(), maxl, &L,
-                                eng->stream),
-               "mfma sample scan");
-        VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, (uint64_t)P * k, k, nv, k, k,
-                                 skeys, eng->stream),
-               "sample merge");
-        init = skeys + (k - 1);
+      if (!fast) {
+        VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+        VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
+                                      lists, maxl, &L, eng->stream),
+               "mfma scan (lists)");
+        VS_HIP(ev_end(eng, eng->scan_ev), "event");
+        VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+        VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream),
+               "merge");
+        VS_HIP(ev_end(eng, eng->merge_ev), "event");
+        continue;
       }
+      // 1. sample pass: top-k of tile maxima over the first 1/64 of every
+      //    workgroup's tiles; its merged k-th key lower-bounds the global one
+      uint64_t* skeys = eng->sample_keys.as<uint64_t>();
+      VS_HIP(vsk::launch_mfma_sample(X, dim, n_rows, row_base, qb, nv, k,
+                                     std::max<uint32_t>(1, tpw / 64), lists, maxl, &L,
+                                     eng->stream),
+             "mfma sample scan");
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, skeys, eng->stream),
+             "sample merge");
+      const uint64_t* init = skeys + (k - 1);
+      // 2. main pass: survivors of the bound -> candidate buffers -> select
+      VS_HIP(hipMemsetAsync(ovf, 0, 4, eng->stream), "clear overflow flag");
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma((const uint16_t*)c.data, dim, n_rows, row_base, qb, nv, k, 0, init,
-                              k, eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+      VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
+                                   eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(),
+                                   ovf, maxl, &L, eng->stream),
              "mfma scan");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-      // lists [L][P][k]; merge reads the first nv queries of every list set
-      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, (uint64_t)P * k, k, nv, k, k,
-                               d_keys + (size_t)q0 * k, eng->stream),
-             "merge");
+      VS_HIP(vsk::launch_select(eng->cand.as<uint64_t>(), eng->cand_cnt.as<uint32_t>(), L, cap,
+                                nv, k, out, eng->stream),
+             "select");
       VS_HIP(ev_end(eng, eng->merge_ev), "event");
+      // 3. overflow fallback (adversarial inputs: many rows at or above the
+      //    bound): the sorted-list pass + merge, both no-ops unless *ovf != 0
+      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
+                                    maxl, &L, eng->stream),
+             "mfma scan (fallback)");
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream, ovf,
+                               eng->fallbacks.as<uint32_t>()),
+             "merge (fallback)");
     }
     return VS_OK;
   }
@@ -649,12 +688,24 @@ int vs_health(vs_engine* eng, char* buf, size_t len) {
     std::lock_guard<std::mutex> g(eng->map_mu);
     ncoll = eng->colls.size();
   }
+  uint32_t fallbacks = 0;
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(eng->work_mu);
+    if (eng->fallbacks.bytes >= 4) {
+      e = hipMemcpyAsync(&fallbacks, eng->fallbacks.p, 4, hipMemcpyDeviceToHost, eng->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(eng->stream);
+    }
+    if (e != hipSuccess) {
+      status = "degraded";
+      err = hipGetErrorString(e);
+    }
+  }
   int n = std::snprintf(buf, len,
                         "{\"status\":\"%s\",\"engine\":\"vsearch-hip\",\"device\":%d,"
                         "\"device_name\":\"%s\",\"hbm_free_bytes\":%zu,\"hbm_total_bytes\":%zu,"
-                        "\"collections\":%zu%s%s%s}",
+                        "\"collections\":%zu,\"mfma_fallbacks\":%u%s%s%s}",
                         status.c_str(), eng->device, eng->device_name.c_str(), freeb, totalb,
-                        ncoll, err.empty() ? "" : ",\"error\":\"", err.c_str(),
+                        ncoll, fallbacks, err.empty() ? "" : ",\"error\":\"", err.c_str(),
                         err.empty() ? "" : "\"");
   if (n < 0 || (size_t)n >= len) return fail(VS_ERR_INVALID_ARG, "health buffer too small");
   return e == hipSuccess ? VS_OK : fail(VS_ERR_DEVICE, err);

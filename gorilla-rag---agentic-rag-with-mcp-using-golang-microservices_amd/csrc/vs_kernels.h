@@ -12,6 +12,11 @@ constexpr uint32_t kMfmaQueries = 256;
 constexpr uint32_t kMfmaMaxK = 16;
 // Largest k any scan supports (GEMV register lists: 16 entries per lane).
 constexpr uint32_t kMaxK = 1024;
+// MFMA main pass: workgroups per launch (<= CUs), candidate slots per
+// (workgroup, query), and the select kernel's LDS capacity (all slots full).
+constexpr uint32_t kMfmaMaxLists = 256;
+constexpr uint32_t kMfmaCandCap = 64;
+constexpr uint32_t kMfmaSelCap = kMfmaMaxLists * kMfmaCandCap;
 
 // Preprocess n fp32 vectors (n x dim, device) and store them as the
 // collection dtype into dst rows: dst_rows[i] if non-null, else dst0 + i.
@@ -36,26 +41,48 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 
-// Batched bf16 scan on MFMA with fused top-k. Q is kMfmaQueries x dim bf16
-// (zero-padded), nq_valid <= kMfmaQueries. Writes out[nlists][kMfmaQueries][k].
-// max_tiles > 0 limits every workgroup to its first max_tiles 32-row tiles
-// (the sample pass); init_th (nullable) gives per-query lower-bound keys at
-// init_th[q * init_stride].
+// Batched bf16 scan on MFMA with fused top-k. Q is
+// kMfmaQueries x dim bf16 (zero-padded), nq_valid <= kMfmaQueries; one
+// workgroup per CU streams a contiguous row range (nlists workgroups).
+//  * sample pass: first max_tiles 32-row tiles of every workgroup, top-k of
+//    the tile maxima per query -> lists[nlists][kMfmaQueries][k] (sorted);
+//  * main pass: every row, survivors of the per-query lower bound
+//    init_th[q * init_stride] appended to cand[nlists][kMfmaQueries][cap]
+//    with counts cand_cnt[nlists][kMfmaQueries]; sets *overflow = 1 when a
+//    buffer would overflow (the caller then runs the lists pass);
+//  * lists pass: the main pass with per-query sorted lists in LDS (any
+//    input), written like the sample pass; a no-op unless run_if is null or
+//    *run_if != 0.
 bool mfma_supported(uint32_t dim);
-hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows,
-                       uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
-                       uint32_t k, uint32_t max_tiles, const uint64_t* init_th,
-                       uint32_t init_stride, uint64_t* out, uint32_t max_lists,
-                       uint32_t* nlists, hipStream_t st);
+hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
+                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+                              uint32_t k, uint32_t max_tiles, uint64_t* lists,
+                              uint32_t max_lists, uint32_t* nlists, hipStream_t st);
+hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                            const uint16_t* Q, uint32_t nq_valid, uint32_t k,
+                            const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
+                            uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
+                            uint32_t max_lists, uint32_t* nlists, hipStream_t st);
+hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+                             uint32_t k, const uint64_t* init_th, uint32_t init_stride,
+                             const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
+                             uint32_t* nlists, hipStream_t st);
+// Top-k of the main pass's candidates for queries 0 .. nq-1 -> out[nq][k].
+hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st);
 uint32_t mfma_max_lists(uint32_t n_rows);
 uint32_t mfma_tiles_per_wg(uint32_t n_rows);
 void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);
 
 // Merge L sorted key lists per query -> out [nq][k] (global top-k by key).
 // List l of query q starts at lists[l * lstride + q * qstride], kin entries.
+// A no-op unless run_if is null or *run_if != 0; when it runs, *ran (if
+// non-null) is incremented once.
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k,
-                        uint64_t* out, hipStream_t st);
+                        uint64_t* out, hipStream_t st, const uint32_t* run_if = nullptr,
+                        uint32_t* ran = nullptr);
 
 // Convert fp32 queries (nq x dim) to bf16 (after preprocessing).
 hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out,

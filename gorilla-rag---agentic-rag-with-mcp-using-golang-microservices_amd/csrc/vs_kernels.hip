@@ -517,32 +517,56 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // ---------------------------------------------------------------------------
 // batched bf16 scan on MFMA + fused top-k
 // ---------------------------------------------------------------------------
-// Workgroup = 8 waves, two per SIMD; wave w owns queries [32w, 32w+32) as
-// two 16-query column groups of v_mfma_f32_16x16x32_bf16 and keeps their
-// B-operand fragments for the whole row (2 x D/32 k-steps x 4 VGPRs = 192 at
-// D = 768) resident in registers. The workgroup streams its contiguous row
-// range HBM -> LDS once, by global_load_lds (1 KiB pieces = 8 rows x 128 B),
-// through a ring of K-chunks (32 rows x 256 k = 16 KiB); AHEAD chunks stay in
-// flight across the raw s_barrier that publishes each chunk (counted vmcnt,
-// never a drain inside the loop). Per 32-k step a wave reads two A fragments
-// (rows 0-15 and 16-31 of the tile, ds_read_b128) and each feeds both query
-// groups: 4 MFMAs per 2 LDS reads. Two waves per SIMD let one wave's LDS-DMA
-// issue, LDS latency and top-k epilogue hide under the partner's MFMAs.
-// The tile epilogue filters each lane's 8 scores per group against the
-// query's threshold key and inserts survivors into a per-query sorted list in
-// LDS. Scores never reach HBM.
+// Workgroup = 8 waves, two per SIMD (waves w and w+4 share one); wave w owns
+// queries [32w, 32w+32) as two 16-query column groups of
+// v_mfma_f32_16x16x32_bf16 and keeps their B-operand fragments for the whole
+// row (2 x D/32 k-steps x 4 VGPRs = 192 at D = 768) resident in registers, so
+// the query block is read once per CU and only the corpus streams. The
+// workgroup streams its contiguous row range HBM -> LDS once, by LDS-DMA
+// (global_load_lds_dwordx4; 1 KiB pieces = 8 rows x 128 B), through a ring of
+// K-chunks (32 rows x 256 k = 16 KiB); AHEAD chunks stay in flight across the
+// raw s_barrier that publishes each chunk (counted vmcnt, never a drain
+// inside the loop). Per 32-k step a wave reads two A fragments (rows 0-15 and
+// 16-31 of the tile, ds_read_b128) and each feeds both query groups: 4 MFMAs
+// per 2 LDS reads. Scores never reach HBM.
 //
-// Threshold: max(the list's own k-th key, init_th[q] - 1). init_th is the
-// k-th key of an exact top-k over a sample of the same rows (the "sample
-// pass"): every row outside the final top-k of the sample
-// ranks below it, so it is a lower bound on the global k-th key and rows
-// under it can never enter the result. It cuts the insert traffic ~25x.
+// Top-k, main pass (MODE 0). Every query starts from a lower bound on its
+// global k-th score (init_th, the sample pass below). The tile epilogue tests
+// each lane's 8 scores per group against it (one v_max3 chain + one ballot);
+// the rare survivors are appended, unsorted, to the query's candidate buffer
+// in global memory (slot from an LDS counter, fire-and-forget stores), and
+// select_cand_kernel picks the top k of all workgroups' candidates. No wave
+// ever waits on a list in the loop, so no stall reaches the other seven
+// waves through the per-chunk barrier. A buffer that would overflow sets
+// *overflow instead; the engine then re-runs the batch with MODE 8 (same
+// scan, per-query sorted lists in LDS maintained by mf_insert), whose launch
+// and merge are no-ops unless that flag is set.
+//
+// Sample pass (MODE 3): the same scan over the first 1/64 of every
+// workgroup's tiles, keeping per query the top k of the TILE MAXIMA (mf_insert
+// lists). Those are k distinct rows with scores >= the merged k-th key, so it
+// lower-bounds the global k-th key: rows under it can never enter the result.
 constexpr int kMfThreads = 512;
 constexpr int kMfWaves = kMfThreads / 64;
-constexpr int kMfLists = (int)kMfmaMaxK * (int)kMfmaQueries;  // LDS list entries
+constexpr int kMfListLen = (int)kMfmaMaxK;                      // entries per query list
+constexpr int kMfListBytes = (int)kMfmaQueries * kMfListLen * 8;  // 32 KiB
 constexpr int kMfRingBytes = 112 * 1024;
+static_assert(kMfmaMaxK == 16, "list insert assumes 4 lanes x 4 entries per query");
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// Kernel arguments (one struct, passed by value in the kernarg segment).
+struct MfArgs {
+  const uint16_t* X;        // corpus rows, bf16, row-major, 32 rows of padding
+  const uint16_t* Q;        // kMfmaQueries x D bf16 (zero-padded)
+  const uint64_t* init_th;  // nullable: per-query lower-bound keys at [q * init_stride]
+  uint64_t* lists;          // MODE 3 / 8: [nwg][kMfmaQueries][k] sorted keys
+  uint64_t* cand;           // MODE 0: [nwg][kMfmaQueries][cand_cap] unsorted keys
+  uint32_t* cand_cnt;       // MODE 0: [nwg][kMfmaQueries] keys in each buffer
+  uint32_t* overflow;       // MODE 0: set to 1 when a buffer would overflow
+  const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
+  uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
+};
 
 // XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
 // ds_read_b128 lane groups of the 16x16x32 A fragment over all 64 banks
@@ -580,71 +604,133 @@ __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_
       : "memory");
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((unsigned)(uint32_t)v, src, 64);
+  const uint32_t hi = __shfl((unsigned)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Inserts survivors into the per-query LDS lists of one 16-query group.
+// Lane (col, kq) holds candidate bits `m` (bit b -> key_of(b)) for query
+// column col; all 64 lanes must be active (wave-uniform call site). Each
+// round takes one candidate per query (lowest kq lane, lowest bit); the
+// query's four lanes then insert it together: lane kq holds entries
+// 4kq .. 4kq+3 of the list `lst` (this query's 16 entries, q-major).
+// Entries at positions >= k stay 0; a candidate ranking at position >= k
+// changes nothing, so the list is always the top-min(k, n) of what was
+// offered. Once the list is full, th_s rises to the score of its k-th key.
+// `volatile` keeps every LDS access in program order across rounds (a wave's
+// DS instructions execute in order); the pointer stays in LDS address space.
+template <typename KeyOf>
+__device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* lst,
+                                          uint32_t k, int lane, int col, int kq, float& th_s) {
+  while (__any(m != 0)) {
+    const uint64_t bal = __ballot(m != 0);
+    const uint32_t qb = (uint32_t)((bal >> col) & 1) | (uint32_t)((bal >> (col + 15)) & 2) |
+                        (uint32_t)((bal >> (col + 30)) & 4) | (uint32_t)((bal >> (col + 45)) & 8);
+    const int sel = __builtin_ctz(qb | 16u);  // 4: no candidate for this query
+    const uint64_t x = shfl64(key_of(__builtin_ctz(m | 256u)), col + 16 * (sel & 3));
+    if (kq == sel) m &= m - 1;
+    if (sel != 4) {  // uniform over the query's four lanes
+      const uint32_t j0 = (uint32_t)(4 * kq);
+      const uint64_t e0 = lst[j0], e1 = lst[j0 + 1], e2 = lst[j0 + 2], e3 = lst[j0 + 3];
+      uint32_t gt = (uint32_t)(e0 > x) + (uint32_t)(e1 > x) + (uint32_t)(e2 > x) +
+                    (uint32_t)(e3 > x);
+      gt += __shfl_xor(gt, 16, 64);
+      gt += __shfl_xor(gt, 32, 64);
+      const uint64_t prev = shfl64(e3, lane >= 16 ? lane - 16 : lane);
+      auto nv = [&](uint32_t j, uint64_t cur, uint64_t below) -> uint64_t {
+        const uint64_t v = j < gt ? cur : (j == gt ? x : below);
+        return j < k ? v : 0;
+      };
+      const uint64_t n0 = nv(j0, e0, prev), n1 = nv(j0 + 1, e1, e0), n2 = nv(j0 + 2, e2, e1),
+                     n3 = nv(j0 + 3, e3, e2);
+      if (gt < k) {
+        lst[j0] = n0;
+        lst[j0 + 1] = n1;
+        lst[j0 + 2] = n2;
+        lst[j0 + 3] = n3;
+      }
+      const int ks = (int)((k - 1) & 3);
+      const uint64_t mk = ks == 0 ? n0 : (ks == 1 ? n1 : (ks == 2 ? n2 : n3));
+      const uint64_t kth = shfl64(mk, col + 16 * (int)((k - 1) >> 2));
+      if (kth) {
+        const float ks_ = key_score(kth);
+        th_s = ks_ > th_s ? ks_ : th_s;
+      }
+    }
+  }
+}
+
 template <int D>
 struct MfShape {
   static constexpr int T = D / 32;                        // 32-k MFMA steps per row
   static constexpr int CS4 = (D % 256 == 0) ? 4 : 2;      // 128-B pieces per row per chunk
   static constexpr int CT = CS4 * 2;                      // 32-k steps per chunk
   static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
-  static constexpr int CHUNK_BYTES = CS4 * 4 * 1024;      // 32 rows x CS4*128 B
+  static constexpr int PIECES = CS4 * 4;                  // 1 KiB LDS-DMA pieces per chunk
+  static constexpr int PPW = PIECES / kMfWaves;           // pieces per wave per chunk
+  static constexpr int CHUNK_BYTES = PIECES * 1024;       // 32 rows x CS4*128 B
   static constexpr int NSLOT = kMfRingBytes / CHUNK_BYTES;
   static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
-  static constexpr int PPW = CS4 * 4 / kMfWaves;          // LDS-DMA pieces per wave per chunk
-  static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + kMfLists * 8;
+  static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + kMfListBytes;
   static_assert(D % 256 == 0 || D % 128 == 0, "MFMA scan needs D % 128 == 0");
-  static_assert(PPW >= 1, "one LDS-DMA piece per wave at least");
+  static_assert(PPW >= 1 && PPW * kMfWaves == PIECES, "pieces split evenly over waves");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-// MODE: 0 = main pass; 3 = sample pass (same code, separate symbol so the
-// two launches are told apart in rocprof); ablation builds only
+// MODE: 0 = main pass (candidate buffers), 3 = sample pass (tile maxima), 8 =
+// main pass with sorted lists (overflow fallback). Ablation builds only
 // (tools/ablate_mfma.hip): 1 = no top-k epilogue, 2 = LDS-DMA stream only,
-// 4 = MFMA + LDS reads + barriers with no DMA, 5 = 4 without barriers.
-template <int D, int MODE = 0>
-__global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(
-    const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t row_base,
-    uint32_t rows_per_wg, uint32_t max_tiles, const uint16_t* __restrict__ Q,
-    uint32_t nq_valid, uint32_t k, const uint64_t* __restrict__ init_th, uint32_t init_stride,
-    uint64_t* __restrict__ out) {
+// 4 = MFMA + LDS reads + barriers with no DMA, 5 = 4 without barriers, 6 =
+// threshold filter only (never keeps a row), 7 = 1 with one A-fragment read
+// per chunk. VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1.
+template <int D, int MODE = 0, int VAR = 0>
+__global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a) {
   using S = MfShape<D>;
+  constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
+  constexpr bool kLists = MODE == 3 || MODE == 8;
+  constexpr bool kCand = MODE == 0;
+  constexpr int PPW = S::PPW;
+  constexpr int kPD0 = (VAR & 64) ? 3 : ((VAR & 32) ? 2 : 1);
+  constexpr int kPD = ((S::CPT * S::CT) % (kPD0 + 1) == 0) ? kPD0 : 1;
+  if (a.run_if && *a.run_if == 0) return;  // fallback launch with nothing to redo
   // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
-  // The four lanes of a query hand list entries to each other through LDS
-  // inside one wave with no barrier: volatile keeps every access in program
-  // order (a wave's DS instructions execute in order), so the compiler cannot
-  // forward a stale entry across the insert passes.
-  // The pointer must stay in the LDS address space: a generic volatile pointer
-  // becomes flat_load/flat_store + vmcnt(0), which drains the DMA ring.
   lds_vu64_t* lists = (lds_vu64_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES);
+  uint32_t* counts = (uint32_t*)(smem + S::NSLOT * S::CHUNK_BYTES);  // MODE 0 (aliases lists)
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15;  // MFMA column (query in group) / A-fragment row
   const int kq = lane >> 4;   // 8-element k slice; C rows 4kq .. 4kq+3
-  const uint32_t wr0 = blockIdx.x * rows_per_wg;
-  const uint32_t wr1 = (uint64_t)wr0 + rows_per_wg < n_rows ? wr0 + rows_per_wg : n_rows;
+  const uint32_t k = a.k;
+  const uint32_t wr0 = blockIdx.x * a.rows_per_wg;
+  const uint32_t wr1 =
+      (uint64_t)wr0 + a.rows_per_wg < a.n_rows ? wr0 + a.rows_per_wg : a.n_rows;
   uint32_t ntiles = (wr1 - wr0 + 31) / 32;
-  if (max_tiles && ntiles > max_tiles) ntiles = max_tiles;
+  if (a.max_tiles && ntiles > a.max_tiles) ntiles = a.max_tiles;
   const uint32_t nchunks = ntiles * S::CPT;
 
-  for (int i = threadIdx.x; i < kMfLists; i += kMfThreads) lists[i] = 0;
+  if constexpr (kLists)
+    for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += kMfThreads) lists[i] = 0;
+  if constexpr (kCand)
+    for (int i = threadIdx.x; i < (int)kMfmaQueries; i += kMfThreads) counts[i] = 0;
 
   // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
   bf16x8_t qf[2][S::T];
   uint32_t ql[2];
   bool qvalid[2];
-  uint64_t th[2];
-  float th_s[2];
+  float th_s[2];  // admit rows whose score reaches th_s
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     ql[g] = (uint32_t)(w * 32 + g * 16 + col);
-    qvalid[g] = ql[g] < nq_valid;
-    const uint4* qrow = (const uint4*)(Q + (size_t)ql[g] * D);
+    qvalid[g] = ql[g] < a.nq_valid;
+    const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
 #pragma unroll
     for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
-    const uint64_t it = (init_th && qvalid[g]) ? init_th[(size_t)ql[g] * init_stride] : 0;
-    th[g] = it ? it - 1 : 0;  // admit the bound itself ("key > th")
+    const uint64_t it = (a.init_th && qvalid[g]) ? a.init_th[(size_t)ql[g] * a.init_stride] : 0;
     th_s[g] = it ? key_score(it) : -INFINITY;
   }
 
@@ -652,30 +738,33 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(
   // rg*8+7, bytes [128*s4, 128*s4+128) of each; lane -> (row lane>>3,
   // 16-B position lane&7 holding chunk (lane&7) ^ swz). The per-lane part of
   // each piece's address is a loop-invariant 32-bit offset; the per-chunk part
-  // is a scalar base. Tiles past the last row read the collection's 32 rows
-  // of allocation padding (vs_engine.cpp grow()) and are masked in the
-  // epilogue.
+  // is a scalar base advanced chunk by chunk (the chunk issued at step c is
+  // c + AHEAD). Tiles past the last row read the collection's 32 rows of
+  // allocation padding (vs_engine.cpp grow()) and are masked in the epilogue.
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  uint32_t loff[S::PPW];
+  uint32_t loff[PPW];
 #pragma unroll
-  for (int i = 0; i < S::PPW; ++i) {
+  for (int i = 0; i < PPW; ++i) {
     const int b = w + kMfWaves * i;
     const int s4l = b >> 2, rg = b & 3;
     const int g_ri = lane >> 3, c16 = (lane & 7) ^ mf_swz(g_ri, rg);
     loff[i] = (uint32_t)(((rg * 8 + g_ri) * D + s4l * 64 + c16 * 8) * 2);
   }
-  const unsigned char* xw = (const unsigned char*)(X + (size_t)wr0 * D);
-  auto issue = [&](uint32_t c) {
-    const uint32_t t = c / S::CPT;
-    const uint32_t u = c - t * S::CPT;
-    const unsigned char* base = xw + ((size_t)t * 32 * D + u * S::CS4 * 64) * 2;
-    const uint32_t sb = lds_base + (c % S::NSLOT) * S::CHUNK_BYTES;
+  const unsigned char* xnext = (const unsigned char*)(a.X + (size_t)wr0 * D);  // next chunk to issue
+  uint32_t unext = 0;     // its chunk index within the tile
+  uint32_t snext = 0;     // its ring slot byte offset
+  auto issue_next = [&]() {
 #pragma unroll
-    for (int i = 0; i < S::PPW; ++i) {
+    for (int i = 0; i < PPW; ++i) {
       const int b = w + kMfWaves * i;
       const int s4l = b >> 2, rg = b & 3;
-      glds16(base, loff[i], __builtin_amdgcn_readfirstlane(sb + (s4l * 4 + rg) * 1024));
+      glds16(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
     }
+    const bool last = unext == S::CPT - 1;
+    xnext += last ? (size_t)(32 * D - (S::CPT - 1) * S::CS4 * 64) * 2 : (size_t)S::CS4 * 128;
+    unext = last ? 0 : unext + 1;
+    snext = snext + S::CHUNK_BYTES == (uint32_t)(S::NSLOT * S::CHUNK_BYTES) ? 0
+                                                                           : snext + S::CHUNK_BYTES;
   };
 
   // A operand read offsets: half hr (tile rows 16hr..16hr+15), lane reads row
@@ -687,63 +776,86 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) off[hr][tt] = rg * 1024 + ri * 128 + (((4 * tt + kq) ^ sw) << 4);
   }
-
   auto lds_a = [&](const unsigned char* sb, int s, int hr) -> bf16x8_t {
     return __builtin_bit_cast(bf16x8_t, *(const uint4*)(sb + (s >> 1) * 4096 + off[hr][s & 1]));
   };
 
-  __syncthreads();  // lists initialised
-  for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
-    if (c < nchunks && MODE < 4) issue(c);
+  __syncthreads();  // lists / counts initialised
+  if constexpr (kDma)
+    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
+      if (c < nchunks) issue_next();
   // publish chunk 0
   if ((uint32_t)S::AHEAD <= nchunks)
-    wait_vmcnt<S::PPW * (S::AHEAD - 1)>();
+    wait_vmcnt<PPW * (S::AHEAD - 1)>();
   else
     wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  // Chunk c is published one barrier early (at c-1), so its first A fragments
-  // are read before the barrier that publishes chunk c+1: the LDS latency at
-  // the head of every chunk hides under that barrier instead of stalling the
-  // first MFMAs of all eight lock-stepped waves.
+  // A fragments are read PD 32-k steps ahead of their MFMAs, across chunk
+  // boundaries inside a tile: chunk c+1 is published by the barrier at the
+  // head of chunk c, so the reads for the first PD steps of chunk c+1 are
+  // issued during the last steps of chunk c. A tile's first PD steps are
+  // read after the previous tile's epilogue, before the first barrier (its
+  // chunk was published one barrier earlier), so no fragment is live across
+  // the epilogue. NB = PD + 1 register sets rotate with the step index,
+  // which repeats every tile because NB divides the steps per tile.
+  constexpr int STEPS = S::CPT * S::CT;
+  constexpr int NB = kPD + 1;
+  static_assert(STEPS % NB == 0, "A-fragment ring must divide the steps per tile");
+  uint32_t scur = 0;  // ring slot byte offset of chunk c
   for (uint32_t t = 0; t < ntiles; ++t) {
     f32x4_t acc[2][2] = {{{}, {}}, {{}, {}}};  // [row half][query group]
+    bf16x8_t afr[NB][2];
 #pragma unroll
     for (int u = 0; u < S::CPT; ++u) {
       const uint32_t c = t * S::CPT + u;
-      const unsigned char* sb = smem + (c % S::NSLOT) * S::CHUNK_BYTES;
-      bf16x8_t a0, a1;
-      if constexpr (MODE != 2) {
-        a0 = lds_a(sb, 0, 0);
-        a1 = lds_a(sb, 0, 1);
+      const uint32_t snxt =
+          scur + S::CHUNK_BYTES == (uint32_t)(S::NSLOT * S::CHUNK_BYTES) ? 0 : scur + S::CHUNK_BYTES;
+      const unsigned char* sb = smem + scur;
+      const unsigned char* sbn = smem + snxt;
+      if (MODE != 2 && u == 0) {
+#pragma unroll
+        for (int p = 0; p < kPD; ++p)
+#pragma unroll
+          for (int hr = 0; hr < 2; ++hr) afr[p][hr] = lds_a(sb, p, hr);
       }
       __builtin_amdgcn_sched_barrier(0);
       // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
-      if constexpr (MODE < 4) {
+      if constexpr (kDma) {
         if (c + S::AHEAD <= nchunks)
-          wait_vmcnt<S::PPW * (S::AHEAD - 2)>();
+          wait_vmcnt<PPW * (S::AHEAD - 2)>();
         else
           wait_vmcnt<0>();
       }
       if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
       __builtin_amdgcn_sched_barrier(0);
-      if (MODE < 4 && c + S::AHEAD < nchunks) issue(c + S::AHEAD);
+      if (kDma && c + S::AHEAD < nchunks) issue_next();
       if constexpr (MODE != 2) {
 #pragma unroll
         for (int s = 0; s < S::CT; ++s) {
+          const int sig = u * S::CT + s;
+          // prefetch step sig + PD (this chunk or the next one)
+          if (MODE != 7 && sig + kPD < STEPS) {
+            const int sp = s + kPD;
+#pragma unroll
+            for (int hr = 0; hr < 2; ++hr)
+              afr[(sig + kPD) % NB][hr] =
+                  sp < S::CT ? lds_a(sb, sp, hr) : lds_a(sbn, sp - S::CT, hr);
+          }
 #pragma unroll
           for (int hr = 0; hr < 2; ++hr) {
-            const bf16x8_t a = s == 0 ? (hr == 0 ? a0 : a1) : lds_a(sb, s, hr);
+            const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][hr];
 #pragma unroll
             for (int g = 0; g < 2; ++g)
-              acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[g][u * S::CT + s],
+              acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][u * S::CT + s],
                                                                    acc[hr][g], 0, 0, 0);
           }
         }
       }
+      scur = snxt;
     }
-    if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) {
+    if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 7) {
       asm volatile("" ::"v"(acc[0][0][0]), "v"(acc[1][1][3]), "v"(acc[0][1][2]),
                    "v"(acc[1][0][1]));
       continue;
@@ -767,52 +879,83 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(
             if (row < wr1 && acc[hr][g][i] > mx) mx = acc[hr][g][i];
           }
       }
-      if (__any(qvalid[g] && mx >= th_s[g])) {
+      // sample pass: one candidate per (tile, query), the tile maximum
+      float lvl = th_s[g];
+      if constexpr (MODE == 3) {
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        lvl = mx > lvl ? mx : lvl;
+      }
+      if constexpr (MODE == 6) {
+        asm volatile("" ::"v"(mx));
+        continue;
+      }
+      if (__any(qvalid[g] && mx >= lvl)) {
+        uint32_t m = 0;
 #pragma unroll
         for (int hr = 0; hr < 2; ++hr)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const uint32_t row = trow0 + 16 * hr + 4 * kq + i;
-            const bool p = qvalid[g] && (full || row < wr1) && acc[hr][g][i] >= th_s[g];
-            if (__any(p)) {
-              for (int pp = 0; pp < 4; ++pp) {
-                if (p && kq == pp) {
-                  const uint64_t key = make_key(acc[hr][g][i], row_base + row);
-                  const uint32_t q = ql[g];
-                  if (key > th[g] && key > lists[(k - 1) * kMfmaQueries + q]) {
-                    int j = (int)k - 1;
-                    while (j > 0) {
-                      const uint64_t prev = lists[(j - 1) * kMfmaQueries + q];
-                      if (prev >= key) break;
-                      lists[j * kMfmaQueries + q] = prev;
-                      --j;
-                    }
-                    lists[j * kMfmaQueries + q] = key;
-                  }
-                }
-              }
-              const uint64_t kth = lists[(k - 1) * kMfmaQueries + ql[g]];
-              if (kth > th[g]) {
-                th[g] = kth;
-                th_s[g] = key_score(kth);
+            const bool p = qvalid[g] && (full || row < wr1) && acc[hr][g][i] >= lvl;
+            m |= (uint32_t)p << (hr * 4 + i);
+          }
+        auto key_of = [&](int b) -> uint64_t {
+          float sc = acc[0][g][0];
+#pragma unroll
+          for (int bb = 1; bb < 8; ++bb) sc = b == bb ? acc[bb >> 2][g][bb & 3] : sc;
+          const uint32_t row = trow0 + 16 * (b >> 2) + 4 * kq + (b & 3);
+          return make_key(sc, a.row_base + row);
+        };
+        if constexpr (kCand) {
+          const uint32_t n = (uint32_t)__popc(m);
+          if (n) {
+            const uint32_t pos = __hip_atomic_fetch_add(counts + ql[g], n, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (pos + n > a.cand_cap) {
+              *a.overflow = 1u;
+            } else {
+              uint64_t* dst =
+                  a.cand + ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * a.cand_cap + pos;
+              while (m) {
+                const int b = __builtin_ctz(m);
+                m &= m - 1;
+                *dst++ = key_of(b);
               }
             }
           }
+        } else {
+          mf_insert(m, key_of, lists + (size_t)ql[g] * kMfListLen, k, lane, col, kq, th_s[g]);
+        }
       }
     }
   }
-  // each wave owns its queries' lists: no barrier needed before the write-out
+  // each wave owns its queries' lists / counters: no barrier before the write-out
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
-    for (uint32_t j = kq; j < k; j += 4)
-      out[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * k + j] = lists[j * kMfmaQueries + ql[g]];
+  for (int g = 0; g < 2; ++g) {
+    if constexpr (kCand) {
+      if (kq == 0) {
+        const uint32_t n = __hip_atomic_load(counts + ql[g], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        a.cand_cnt[(size_t)blockIdx.x * kMfmaQueries + ql[g]] = n < a.cand_cap ? n : a.cand_cap;
+      }
+    } else if constexpr (kLists) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t j = (uint32_t)(4 * kq + t);
+        if (j < k)
+          a.lists[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * k + j] =
+              lists[(size_t)ql[g] * kMfListLen + j];
+      }
+    }
+  }
 }
 
 bool mfma_supported(uint32_t dim) { return dim == 768 || dim == 512 || dim == 384 || dim == 256; }
 
 void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg) {
   const int cus = g_cu_count ? g_cu_count : device_cu_count();
-  uint64_t want = (uint64_t)cus;
+  uint64_t want = (uint64_t)cus < kMfmaMaxLists ? (uint64_t)cus : kMfmaMaxLists;
   const uint64_t tiles = ((uint64_t)n_rows + 31) / 32;
   if (want > tiles) want = tiles;
   if (want < 1) want = 1;
@@ -829,42 +972,134 @@ uint32_t mfma_max_lists(uint32_t n_rows) {
   return nwg;
 }
 
-hipError_t launch_mfma(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
-                       const uint16_t* Q, uint32_t nq_valid, uint32_t k, uint32_t max_tiles,
-                       const uint64_t* init_th, uint32_t init_stride, uint64_t* out,
-                       uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
-  if (k == 0 || k > kMfmaMaxK || n_rows == 0 || nq_valid == 0 || nq_valid > kMfmaQueries)
-    return hipErrorInvalidValue;
-  uint32_t nwg, rpw;
-  mfma_grid(n_rows, &nwg, &rpw);
-  if (nwg > max_lists) return hipErrorInvalidValue;
-  *nlists = nwg;
-  dim3 grid(nwg), block(kMfThreads);
-#define VS_MFMA_CASE(DD)                                                                     \
-  case DD:                                                                                   \
-    if (max_tiles)                                                                           \
-      hipLaunchKernelGGL((mfma_topk_kernel<DD, 3>), grid, block, 0, st, X, n_rows, row_base, \
-                         rpw, max_tiles, Q, nq_valid, k, init_th, init_stride, out);         \
-    else                                                                                     \
-      hipLaunchKernelGGL((mfma_topk_kernel<DD, 0>), grid, block, 0, st, X, n_rows, row_base, \
-                         rpw, 0u, Q, nq_valid, k, init_th, init_stride, out);                \
-    break;
-  switch (dim) {
-    VS_MFMA_CASE(768)
-    VS_MFMA_CASE(512)
-    VS_MFMA_CASE(384)
-    VS_MFMA_CASE(256)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef VS_MFMA_CASE
-  return hipGetLastError();
-}
-
 uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
   uint32_t nwg, rpw;
   mfma_grid(n_rows, &nwg, &rpw);
   return (rpw + 31) / 32;
+}
+
+template <int MODE>
+static hipError_t mfma_launch_mode(uint32_t dim, uint32_t nwg, const MfArgs& a, hipStream_t st) {
+  dim3 grid(nwg), block(kMfThreads);
+  switch (dim) {
+    case 768: hipLaunchKernelGGL((mfma_topk_kernel<768, MODE>), grid, block, 0, st, a); break;
+    case 512: hipLaunchKernelGGL((mfma_topk_kernel<512, MODE>), grid, block, 0, st, a); break;
+    case 384: hipLaunchKernelGGL((mfma_topk_kernel<384, MODE>), grid, block, 0, st, a); break;
+    case 256: hipLaunchKernelGGL((mfma_topk_kernel<256, MODE>), grid, block, 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static bool mfma_args_ok(uint32_t dim, uint32_t n_rows, uint32_t nq_valid, uint32_t k) {
+  return mfma_supported(dim) && k >= 1 && k <= kMfmaMaxK && n_rows > 0 && nq_valid >= 1 &&
+         nq_valid <= kMfmaQueries;
+}
+
+hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
+                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+                              uint32_t k, uint32_t max_tiles, uint64_t* lists,
+                              uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || max_tiles == 0) return hipErrorInvalidValue;
+  MfArgs a{};
+  mfma_grid(n_rows, nlists, &a.rows_per_wg);
+  if (*nlists > max_lists) return hipErrorInvalidValue;
+  a.X = X, a.Q = Q, a.lists = lists, a.n_rows = n_rows, a.row_base = row_base;
+  a.max_tiles = max_tiles, a.nq_valid = nq_valid, a.k = k;
+  return mfma_launch_mode<3>(dim, *nlists, a, st);
+}
+
+hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+                             uint32_t k, const uint64_t* init_th, uint32_t init_stride,
+                             const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
+                             uint32_t* nlists, hipStream_t st) {
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k)) return hipErrorInvalidValue;
+  MfArgs a{};
+  mfma_grid(n_rows, nlists, &a.rows_per_wg);
+  if (*nlists > max_lists) return hipErrorInvalidValue;
+  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.lists = lists;
+  a.run_if = run_if, a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
+  return mfma_launch_mode<8>(dim, *nlists, a, st);
+}
+
+hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                            const uint16_t* Q, uint32_t nq_valid, uint32_t k,
+                            const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
+                            uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
+                            uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap == 0) return hipErrorInvalidValue;
+  MfArgs a{};
+  mfma_grid(n_rows, nlists, &a.rows_per_wg);
+  if (*nlists > max_lists) return hipErrorInvalidValue;
+  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = cand;
+  a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
+  a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
+  return mfma_launch_mode<0>(dim, *nlists, a, st);
+}
+
+// ---------------------------------------------------------------------------
+// select: top-k of the main pass's per-workgroup candidate buffers
+// ---------------------------------------------------------------------------
+// One workgroup per query: the (few) candidates of all workgroups are
+// gathered into LDS, sorted (bitonic, descending) and the first k written.
+// Capacity covers every buffer full (kMfmaSelCap >= nwg * cand_cap).
+constexpr int kSelThreads = 512;
+
+__device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, int nthreads) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n_pow2 / 2; i += nthreads) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const uint64_t x = buf[lo], y = buf[hi];
+        if ((x < y) == desc) {
+          buf[lo] = y;
+          buf[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
+    const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
+    uint32_t cap, uint32_t k, uint64_t* __restrict__ out) {
+  __shared__ uint64_t buf[kMfmaSelCap];
+  __shared__ uint32_t lcnt[kMfmaMaxLists];
+  __shared__ uint32_t total;
+  const uint32_t q = blockIdx.x;
+  if (threadIdx.x == 0) total = 0;
+  for (uint32_t l = threadIdx.x; l < nwg; l += kSelThreads) lcnt[l] = cnt[(size_t)l * kMfmaQueries + q];
+  __syncthreads();
+  const uint32_t slots = nwg * cap;
+  for (uint32_t i = threadIdx.x; i < slots; i += kSelThreads) {
+    const uint32_t l = i / cap, j = i - l * cap;
+    if (j < lcnt[l]) {
+      const uint64_t x = cand[((size_t)l * kMfmaQueries + q) * cap + j];
+      buf[atomicAdd(&total, 1u)] = x;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = total;
+  int p2 = 1;
+  while ((uint32_t)p2 < n) p2 <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+  __syncthreads();
+  if (p2 > 1) bitonic_sort_desc_n(buf, p2, kSelThreads);
+  for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < n ? buf[j] : 0;
+}
+
+hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st) {
+  if (nwg == 0 || nwg > kMfmaMaxLists || (uint64_t)nwg * cap > kMfmaSelCap || k == 0 ||
+      k > kMfmaMaxK || nq == 0 || nq > kMfmaQueries)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_cand_kernel, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt, nwg,
+                     cap, k, out);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -898,7 +1133,10 @@ __device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
 
 __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
     const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
-    uint32_t kin, uint32_t k, uint64_t* __restrict__ out) {
+    uint32_t kin, uint32_t k, const uint32_t* __restrict__ run_if, uint32_t* __restrict__ ran,
+    uint64_t* __restrict__ out) {
+  if (run_if && *run_if == 0) return;  // fallback launch with nothing to redo
+  if (ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ran, 1u);
   __shared__ uint64_t buf[kMergeCap];
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t cnt;
@@ -960,10 +1198,10 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
 
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out,
-                        hipStream_t st) {
+                        hipStream_t st, const uint32_t* run_if, uint32_t* ran) {
   if (k == 0 || k > kMaxK || nq == 0 || L == 0 || kin == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(merge_keys_kernel, dim3(nq), dim3(kMergeThreads), 0, st, lists, L,
-                     lstride, qstride, kin, k, out);
+                     lstride, qstride, kin, k, run_if, ran, out);
   return hipGetLastError();
 }
 

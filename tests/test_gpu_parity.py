@@ -106,6 +106,51 @@ def test_mfma_batched(engine, orc, corpora, nq, k):
     _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
 
 
+@pytest.fixture(scope="module")
+def corpus_fast(engine, orc):
+    """200k x 768 bf16: >= 8 tiles per workgroup, so batched searches take the
+    sample pass + candidate-buffer main pass (vs_engine.cpp search_core)."""
+    n, dim = 200_000, 768
+    engine.create_collection("fast768", dim, 0, 1, n)
+    engine.generate("fast768", n, orc.SEED_CORPUS)
+    return "fast768", orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+
+
+@pytest.mark.parametrize("nq,k", [(2, 10), (256, 10), (300, 16), (77, 1), (256, 5)])
+def test_mfma_candidate_path(engine, orc, corpus_fast, nq, k):
+    import json
+    name, X = corpus_fast
+    before = json.loads(engine.health())["mfma_fallbacks"]
+    Q = orc.generate(orc.SEED_QUERY, 1000, nq, 768)
+    s, r, c = engine.search(name, Q, k)
+    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    # random unit rows never overflow the candidate buffers
+    assert json.loads(engine.health())["mfma_fallbacks"] == before
+
+
+def test_mfma_overflow_fallback(engine, orc):
+    """Adversarial ties: 70k rows, the first 40k identical. Every identical row
+    reaches the sample bound of the queries that match it, the candidate
+    buffers overflow, and the sorted-list pass must give the exact answer
+    (ties -> lowest rows) for those queries and for the others alike."""
+    import json
+    n, dim = 70_000, 768
+    base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
+    base[:40_000] = base[12_345]
+    engine.create_collection("ties", dim, 0, 1, n)
+    engine.upsert("ties", np.arange(n), base)
+    X = orc.preprocess(base, True, True)
+    Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 7, 40, dim),
+                        base[12_345:12_346] * 3.0])
+    before = json.loads(engine.health())["mfma_fallbacks"]
+    for k in (10, 16):
+        s, r, c = engine.search("ties", Q, k)
+        assert r[0].tolist() == list(range(k)) and r[-1].tolist() == list(range(k))
+        _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    assert json.loads(engine.health())["mfma_fallbacks"] >= before + 2
+    engine.drop_collection("ties")
+
+
 def test_fp32_batched(engine, orc, corpora):
     name, X = corpora[0]
     Q = orc.generate(orc.SEED_QUERY, 500, 5, 768)
