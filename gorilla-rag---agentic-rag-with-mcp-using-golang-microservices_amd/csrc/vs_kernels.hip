@@ -546,8 +546,11 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // workgroup's tiles, keeping per query the top k of the TILE MAXIMA (mf_insert
 // lists). Those are k distinct rows with scores >= the merged k-th key, so it
 // lower-bounds the global k-th key: rows under it can never enter the result.
-constexpr int kMfThreads = 512;
-constexpr int kMfWaves = kMfThreads / 64;
+// Query groups (16 queries each) per wave: G = 2 -> 8 waves of 32 queries
+// (two per SIMD); G = 4 -> 4 waves of 64 queries (one per SIMD, 512-register
+// budget), which halves the LDS reads per MFMA (each A fragment feeds 4).
+constexpr int kMfG = 2;
+constexpr int mf_waves(int g) { return 16 / g; }
 constexpr int kMfListLen = (int)kMfmaMaxK;                      // entries per query list
 constexpr int kMfListBytes = (int)kMfmaQueries * kMfListLen * 8;  // 32 KiB
 constexpr int kMfRingBytes = 112 * 1024;
@@ -599,6 +602,17 @@ __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
       "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
+// Ablation only (MODE 11): the same LDS-DMA instruction moving 4 B per lane.
+__device__ __forceinline__ void glds4(const void* sbase, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(sbase), "s"(lds)
       : "memory");
@@ -662,20 +676,20 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
   }
 }
 
-template <int D>
+template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8>
 struct MfShape {
   static constexpr int T = D / 32;                        // 32-k MFMA steps per row
   static constexpr int CS4 = (D % 256 == 0) ? 4 : 2;      // 128-B pieces per row per chunk
   static constexpr int CT = CS4 * 2;                      // 32-k steps per chunk
   static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
   static constexpr int PIECES = CS4 * 4;                  // 1 KiB LDS-DMA pieces per chunk
-  static constexpr int PPW = PIECES / kMfWaves;           // pieces per wave per chunk
+  static constexpr int PPW = PIECES / WAVES;              // pieces per wave per chunk
   static constexpr int CHUNK_BYTES = PIECES * 1024;       // 32 rows x CS4*128 B
-  static constexpr int NSLOT = kMfRingBytes / CHUNK_BYTES;
+  static constexpr int NSLOT = RING / CHUNK_BYTES;
   static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
-  static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + kMfListBytes;
+  static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + TAIL;  // ring + lists / counters
   static_assert(D % 256 == 0 || D % 128 == 0, "MFMA scan needs D % 128 == 0");
-  static_assert(PPW >= 1 && PPW * kMfWaves == PIECES, "pieces split evenly over waves");
+  static_assert(PPW >= 1 && PPW * WAVES == PIECES, "pieces split evenly over waves");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -684,16 +698,27 @@ struct MfShape {
 // (tools/ablate_mfma.hip): 1 = no top-k epilogue, 2 = LDS-DMA stream only,
 // 4 = MFMA + LDS reads + barriers with no DMA, 5 = 4 without barriers, 6 =
 // threshold filter only (never keeps a row), 7 = 1 with one A-fragment read
-// per chunk. VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1.
-template <int D, int MODE = 0, int VAR = 0>
-__global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a) {
-  using S = MfShape<D>;
+// per chunk, 10 = 1 reading only half the A fragments (the compiler then
+// merges the two row halves' MFMA chains: invalid as a timing), 11 = 1 with
+// 4-B LDS-DMA (a quarter of the bytes, same instructions). VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1;
+// VAR 128: each step's reads and MFMAs pinned in program order; VAR 512:
+// the chunk's LDS-DMA pieces spread over its steps instead of at its head.
+template <int D, int MODE = 0, int VAR = 0, int G = kMfG>
+__global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_kernel(
+    const MfArgs a) {
+  constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
+  static_assert(WAVES * QPW == (int)kMfmaQueries, "one launch covers kMfmaQueries");
+  // VAR 256: a 144 KiB ring (more chunks in flight) where no LDS lists are kept
+  constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 3 && MODE != 8;
+  using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
+                    kBigRing ? (int)kMfmaQueries * 4 : kMfListBytes, WAVES>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 3 || MODE == 8;
   constexpr bool kCand = MODE == 0;
   constexpr int PPW = S::PPW;
   constexpr int kPD0 = (VAR & 64) ? 3 : ((VAR & 32) ? 2 : 1);
   constexpr int kPD = ((S::CPT * S::CT) % (kPD0 + 1) == 0) ? kPD0 : 1;
+  constexpr bool kPin = (VAR & 128) != 0;  // keep each step's reads + MFMAs in program order
   if (a.run_if && *a.run_if == 0) return;  // fallback launch with nothing to redo
   // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
@@ -714,18 +739,18 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
   const uint32_t nchunks = ntiles * S::CPT;
 
   if constexpr (kLists)
-    for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += kMfThreads) lists[i] = 0;
+    for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += THREADS) lists[i] = 0;
   if constexpr (kCand)
-    for (int i = threadIdx.x; i < (int)kMfmaQueries; i += kMfThreads) counts[i] = 0;
+    for (int i = threadIdx.x; i < (int)kMfmaQueries; i += THREADS) counts[i] = 0;
 
   // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
-  bf16x8_t qf[2][S::T];
-  uint32_t ql[2];
-  bool qvalid[2];
-  float th_s[2];  // admit rows whose score reaches th_s
+  bf16x8_t qf[G][S::T];
+  uint32_t ql[G];
+  bool qvalid[G];
+  float th_s[G];  // admit rows whose score reaches th_s
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    ql[g] = (uint32_t)(w * 32 + g * 16 + col);
+  for (int g = 0; g < G; ++g) {
+    ql[g] = (uint32_t)(w * QPW + g * 16 + col);
     qvalid[g] = ql[g] < a.nq_valid;
     const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
 #pragma unroll
@@ -745,26 +770,34 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
   uint32_t loff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int b = w + kMfWaves * i;
+    const int b = w + WAVES * i;
     const int s4l = b >> 2, rg = b & 3;
     const int g_ri = lane >> 3, c16 = (lane & 7) ^ mf_swz(g_ri, rg);
     loff[i] = (uint32_t)(((rg * 8 + g_ri) * D + s4l * 64 + c16 * 8) * 2);
   }
+  constexpr bool kSpread = (VAR & 512) != 0;  // pieces spread over the chunk's steps
   const unsigned char* xnext = (const unsigned char*)(a.X + (size_t)wr0 * D);  // next chunk to issue
   uint32_t unext = 0;     // its chunk index within the tile
   uint32_t snext = 0;     // its ring slot byte offset
-  auto issue_next = [&]() {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int b = w + kMfWaves * i;
-      const int s4l = b >> 2, rg = b & 3;
+  auto issue_piece = [&](int i) {
+    const int b = w + WAVES * i;
+    const int s4l = b >> 2, rg = b & 3;
+    if constexpr (MODE == 11)
+      glds4(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
+    else
       glds16(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
-    }
+  };
+  auto advance = [&]() {
     const bool last = unext == S::CPT - 1;
     xnext += last ? (size_t)(32 * D - (S::CPT - 1) * S::CS4 * 64) * 2 : (size_t)S::CS4 * 128;
     unext = last ? 0 : unext + 1;
     snext = snext + S::CHUNK_BYTES == (uint32_t)(S::NSLOT * S::CHUNK_BYTES) ? 0
                                                                            : snext + S::CHUNK_BYTES;
+  };
+  auto issue_next = [&]() {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) issue_piece(i);
+    advance();
   };
 
   // A operand read offsets: half hr (tile rows 16hr..16hr+15), lane reads row
@@ -780,6 +813,11 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
     return __builtin_bit_cast(bf16x8_t, *(const uint4*)(sb + (s >> 1) * 4096 + off[hr][s & 1]));
   };
 
+  // The query fragments and bounds are loads the compiler's waitcnt pass
+  // tracks; drain them here with the builtin (which the pass sees), so it
+  // does not place vmcnt waits for them inside the loop, where the hardware
+  // counter also holds the ring's LDS-DMA pieces (invisible to the pass).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
   __syncthreads();  // lists / counts initialised
   if constexpr (kDma)
     for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
@@ -805,7 +843,11 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
   static_assert(STEPS % NB == 0, "A-fragment ring must divide the steps per tile");
   uint32_t scur = 0;  // ring slot byte offset of chunk c
   for (uint32_t t = 0; t < ntiles; ++t) {
-    f32x4_t acc[2][2] = {{{}, {}}, {{}, {}}};  // [row half][query group]
+    f32x4_t acc[2][G];  // [row half][query group]
+#pragma unroll
+    for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[hr][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     bf16x8_t afr[NB][2];
 #pragma unroll
     for (int u = 0; u < S::CPT; ++u) {
@@ -818,7 +860,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
 #pragma unroll
         for (int p = 0; p < kPD; ++p)
 #pragma unroll
-          for (int hr = 0; hr < 2; ++hr) afr[p][hr] = lds_a(sb, p, hr);
+          for (int hr = 0; hr < (MODE == 10 ? 1 : 2); ++hr) afr[p][hr] = lds_a(sb, p, hr);
       }
       __builtin_amdgcn_sched_barrier(0);
       // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
@@ -830,7 +872,8 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
       }
       if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
       __builtin_amdgcn_sched_barrier(0);
-      if (kDma && c + S::AHEAD < nchunks) issue_next();
+      const bool refill = kDma && c + S::AHEAD < nchunks;
+      if (!kSpread && refill) issue_next();
       if constexpr (MODE != 2) {
 #pragma unroll
         for (int s = 0; s < S::CT; ++s) {
@@ -839,32 +882,46 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
           if (MODE != 7 && sig + kPD < STEPS) {
             const int sp = s + kPD;
 #pragma unroll
-            for (int hr = 0; hr < 2; ++hr)
+            for (int hr = 0; hr < (MODE == 10 ? 1 : 2); ++hr)
               afr[(sig + kPD) % NB][hr] =
                   sp < S::CT ? lds_a(sb, sp, hr) : lds_a(sbn, sp - S::CT, hr);
           }
+          if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int hr = 0; hr < 2; ++hr) {
-            const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][hr];
+            const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][MODE == 10 ? 0 : hr];
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
+            for (int g = 0; g < G; ++g)
               acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][u * S::CT + s],
                                                                    acc[hr][g], 0, 0, 0);
+          }
+          if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+          if constexpr (kSpread) {
+            // piece i after step i * CT / PPW (the last one also advances)
+#pragma unroll
+            for (int i = 0; i < PPW; ++i)
+              if (s == (i * S::CT) / PPW && refill) {
+                issue_piece(i);
+                if (i == PPW - 1) advance();
+              }
           }
         }
       }
       scur = snxt;
     }
-    if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 7) {
-      asm volatile("" ::"v"(acc[0][0][0]), "v"(acc[1][1][3]), "v"(acc[0][1][2]),
-                   "v"(acc[1][0][1]));
+    if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 7 || MODE == 10 ||
+                  MODE == 11) {
+#pragma unroll
+      for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+        for (int g = 0; g < G; ++g) asm volatile("" ::"v"(acc[hr][g][hr * 2 + (g & 1)]));
       continue;
     }
     // epilogue: acc[hr][g][i] = score(row trow0 + 16hr + 4kq + i, query ql[g])
     const uint32_t trow0 = wr0 + t * 32;
     const bool full = trow0 + 32 <= wr1;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < G; ++g) {
       float mx = -INFINITY;
       if (full) {
         mx = fmax3(fmax3(acc[0][g][0], acc[0][g][1], acc[0][g][2]),
@@ -932,7 +989,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void mfma_topk_kernel(const MfArgs a
   }
   // each wave owns its queries' lists / counters: no barrier before the write-out
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     if constexpr (kCand) {
       if (kq == 0) {
         const uint32_t n = __hip_atomic_load(counts + ql[g], __ATOMIC_RELAXED,
@@ -980,7 +1037,7 @@ uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
 
 template <int MODE>
 static hipError_t mfma_launch_mode(uint32_t dim, uint32_t nwg, const MfArgs& a, hipStream_t st) {
-  dim3 grid(nwg), block(kMfThreads);
+  dim3 grid(nwg), block(64 * mf_waves(kMfG));
   switch (dim) {
     case 768: hipLaunchKernelGGL((mfma_topk_kernel<768, MODE>), grid, block, 0, st, a); break;
     case 512: hipLaunchKernelGGL((mfma_topk_kernel<512, MODE>), grid, block, 0, st, a); break;

@@ -27,12 +27,13 @@ struct Ctx {
   hipEvent_t a, b;
 };
 
-template <int MODE, int VAR>
+template <int MODE, int VAR, int G = 2>
 static float run(const Ctx& c, bool bound) {
   MfArgs a = c.args;
   if (!bound) a.init_th = nullptr;
   hipEventRecord(c.a, 0);
-  hipLaunchKernelGGL((mfma_topk_kernel<768, MODE, VAR>), dim3(c.nwg), dim3(kMfThreads), 0, 0, a);
+  hipLaunchKernelGGL((mfma_topk_kernel<768, MODE, VAR, G>), dim3(c.nwg), dim3(64 * mf_waves(G)), 0,
+                     0, a);
   hipEventRecord(c.b, 0);
   hipEventSynchronize(c.b);
   float ms = 0;
@@ -94,16 +95,25 @@ int main(int argc, char** argv) {
   c.a = a;
   c.b = b;
   std::vector<Arm> arms = {
-      {"main cand", run<0, 0>, true, {}},
-      {"main cand v32", run<0, 32>, true, {}},
-      {"main lists", run<8, 0>, true, {}},
-      {"filter-only", run<6, 0>, true, {}},
-      {"no-epilogue", run<1, 0>, false, {}},
-      {"no-epi v32", run<1, 32>, false, {}},
-      {"dma+mfma noLDS", run<7, 0>, false, {}},
-      {"dma-only", run<2, 0>, false, {}},
-      {"mfma+bar", run<4, 0>, false, {}},
+      {"main cand G2", run<0, 0, 2>, true, {}},
+      {"main G2 pin pd2", run<0, 160, 2>, true, {}},
+      {"no-epi G2", run<1, 0, 2>, false, {}},
+      {"no-epi G2 spread", run<1, 512, 2>, false, {}},
+      {"main cand G4 pd2", run<0, 160, 4>, true, {}},
+      {"main G4 pd2 spread", run<0, 160 + 512, 4>, true, {}},
+      {"no-epi G4 pd2", run<1, 160, 4>, false, {}},
+      {"no-epi G4 pd2 spread", run<1, 160 + 512, 4>, false, {}},
+      {"no-epi G4 pd3 spread", run<1, 192 + 512, 4>, false, {}},
+      {"mfma+bar G4 pd2", run<4, 160, 4>, false, {}},
+      {"dma-only G4", run<2, 0, 4>, false, {}},
   };
+
+
+
+
+
+
+
 
 
 
