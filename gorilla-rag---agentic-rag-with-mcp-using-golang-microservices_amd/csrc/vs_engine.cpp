@@ -96,7 +96,9 @@ struct vs_engine {
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
   DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
+  DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
   DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
+  uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
   std::vector<uint64_t> h_keys;
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
@@ -163,6 +165,158 @@ int grow(vs_engine* eng, Collection& c, uint64_t need) {
   return VS_OK;
 }
 
+// Single-query scans (GEMV path) of preprocessed fp32 queries qp[q0 .. q0+n)
+// -> keys d_keys[i * k], one scan + merge per query.
+int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
+                uint64_t* d_keys) {
+  const uint32_t dim = c.dim;
+  const bool bf16 = c.dtype == VS_DTYPE_BF16;
+  const uint32_t n_rows = (uint32_t)c.rows;
+  const uint32_t row_base = (uint32_t)c.row_base;
+  if (bf16)
+    VS_HIP(vsk::launch_round_bf16(qp + (size_t)q0 * dim, (uint64_t)n * dim,
+                                  qp + (size_t)q0 * dim, eng->stream),
+           "round query");
+  const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
+  const size_t lbytes = (size_t)maxl * k * 8;
+  if (eng->lists.bytes < lbytes) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
+  }
+  for (uint32_t i = q0; i < q0 + n; ++i) {
+    uint32_t L = 0;
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_gemv(c.data, bf16, dim, n_rows, row_base, qp + (size_t)i * dim, k,
+                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+           "gemv scan");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+    VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
+                             d_keys + (size_t)(i - q0) * k, eng->stream),
+           "merge");
+    VS_HIP(ev_end(eng, eng->merge_ev), "event");
+  }
+  return VS_OK;
+}
+
+// Batched bf16 scan on MFMA, 256 queries per pass:
+//  1. sample pass over 1/64 of every workgroup's tiles -> top-k of the tile
+//     maxima -> per-query lower bound on the global k-th key;
+//  2. main pass: rows reaching the bound -> candidate buffers -> select;
+//  3. if a candidate buffer overflowed (adversarial ties): redo the pass
+//     exactly -- the sorted-list pass + merge for k <= 16 (device-side, no
+//     host sync: both launches are no-ops unless the flag is set), the GEMV
+//     path for larger k (after a host check of the flag).
+int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
+                uint64_t* d_keys) {
+  const uint32_t dim = c.dim;
+  const uint32_t n_rows = (uint32_t)c.rows;
+  const uint32_t row_base = (uint32_t)c.row_base;
+  const uint32_t P = vsk::kMfmaQueries;
+  const uint32_t npass = (nq + P - 1) / P;
+  const uint32_t maxl = vsk::mfma_max_lists(n_rows);
+  const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
+  // the candidate pass needs the sample bound from a few tiles per workgroup;
+  // small collections take the sorted-list pass (k <= 16) or the GEMV path
+  const bool fast = tpw >= 8;
+  if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys);
+  const uint32_t st = vsk::mfma_sample_tiles(n_rows);
+  const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
+  const size_t bbytes = (size_t)P * dim * 2;
+  const size_t lbytes = (size_t)maxl * P * std::min(k, vsk::kMfmaListMaxK) * 8;
+  const size_t sbytes = (size_t)P * k * 8;
+  const size_t cbytes = (size_t)maxl * P * cap * 8;
+  const size_t scbytes = (size_t)maxl * P * st * 8;
+  const size_t nbytes = (size_t)maxl * P * 4;
+  if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes ||
+      eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
+      eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes ||
+      eng->scand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
+    VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
+    VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
+    VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
+    VS_HIP(eng->scand.ensure(scbytes), "alloc sample candidate scratch");
+    VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
+    VS_HIP(eng->scand_cnt.ensure(nbytes), "alloc sample candidate counts");
+    VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
+    if (eng->fallbacks.bytes < 4) {
+      VS_HIP(eng->fallbacks.ensure(4), "alloc fallback counter");
+      VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
+    }
+  }
+  const uint16_t* X = (const uint16_t*)c.data;
+  uint64_t* lists = eng->lists.as<uint64_t>();
+  uint32_t* ovf = eng->overflow.as<uint32_t>();
+  uint16_t* qb = eng->q_bf16.as<uint16_t>();
+  for (uint32_t p = 0; p < npass; ++p) {
+    const uint32_t q0 = p * P;
+    const uint32_t nv = std::min(P, nq - q0);
+    uint64_t* out = d_keys + (size_t)q0 * k;
+    if (nv < P)
+      VS_HIP(hipMemsetAsync(qb + (size_t)nv * dim, 0, (size_t)(P - nv) * dim * 2, eng->stream),
+             "pad queries");
+    VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
+           "queries to bf16");
+    uint32_t L = 0;
+    if (!fast) {
+      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
+                                    lists, maxl, &L, eng->stream),
+             "mfma scan (lists)");
+      VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream),
+             "merge");
+      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+      continue;
+    }
+    // 1. sample pass -> bound keys skeys[q * k + k - 1]
+    uint64_t* skeys = eng->sample_keys.as<uint64_t>();
+    VS_HIP(vsk::launch_mfma_sample(X, dim, n_rows, row_base, qb, nv, k, st,
+                                   eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), maxl,
+                                   &L, eng->stream),
+           "mfma sample scan");
+    VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, st, nv,
+                              k, skeys, eng->stream),
+           "sample select");
+    const uint64_t* init = skeys + (k - 1);
+    // 2. main pass -> candidates -> select
+    VS_HIP(hipMemsetAsync(ovf, 0, 4, eng->stream), "clear overflow flag");
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
+                                 eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(), ovf,
+                                 maxl, &L, eng->stream),
+           "mfma scan");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+    VS_HIP(vsk::launch_select(eng->cand.as<uint64_t>(), eng->cand_cnt.as<uint32_t>(), L, cap, nv,
+                              k, out, eng->stream),
+           "select");
+    VS_HIP(ev_end(eng, eng->merge_ev), "event");
+    // 3. overflow fallback
+    if (k <= vsk::kMfmaListMaxK) {
+      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
+                                    maxl, &L, eng->stream),
+             "mfma scan (fallback)");
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream, ovf,
+                               eng->fallbacks.as<uint32_t>()),
+             "merge (fallback)");
+    } else {
+      uint32_t h_ovf = 0;
+      VS_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, eng->stream), "flag D2H");
+      VS_HIP(hipStreamSynchronize(eng->stream), "flag sync");
+      if (h_ovf) {
+        int rc = search_gemv(eng, c, qp, q0, nv, k, out);
+        if (rc != VS_OK) return rc;
+        eng->host_fallbacks++;
+      }
+    }
+  }
+  return VS_OK;
+}
+
 // Core search on device data. d_q: nq x dim fp32 on this device, ordered on
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
@@ -177,8 +331,6 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   }
   if (c.rows >= 0xFFFFFFFFull || c.row_base + c.rows >= 0xFFFFFFFFull)
     return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
-  const uint32_t n_rows = (uint32_t)c.rows;
-  const uint32_t row_base = (uint32_t)c.row_base;
 
   // 1. query preprocessing (cosine normalise) -> q_pre (fp32)
   const size_t qbytes = (size_t)nq * dim * 4;
@@ -191,121 +343,8 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
          "query preprocess");
 
   const bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
-  if (use_mfma) {
-    const uint32_t P = vsk::kMfmaQueries;
-    const uint32_t npass = (nq + P - 1) / P;
-    const uint32_t maxl = vsk::mfma_max_lists(n_rows);
-    const uint32_t cap = vsk::kMfmaCandCap;
-    const size_t lbytes = (size_t)maxl * P * k * 8;
-    const size_t bbytes = (size_t)P * dim * 2;
-    const size_t sbytes = (size_t)P * k * 8;
-    const size_t cbytes = (size_t)maxl * P * cap * 8;
-    const size_t nbytes = (size_t)maxl * P * 4;
-    if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes ||
-        eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
-        eng->cand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
-      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-      VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
-      VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
-      VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
-      VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
-      VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
-      VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
-      if (eng->fallbacks.bytes < 4) {
-        VS_HIP(eng->fallbacks.ensure(4), "alloc fallback counter");
-        VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
-      }
-    }
-    const uint16_t* X = (const uint16_t*)c.data;
-    uint64_t* lists = eng->lists.as<uint64_t>();
-    uint32_t* ovf = eng->overflow.as<uint32_t>();
-    // The candidate pass needs a lower bound from the sample pass: a few
-    // tiles per workgroup at least. Small collections (< 8 tiles per
-    // workgroup) take the sorted-list pass directly.
-    const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
-    const bool fast = tpw >= 8;
-    for (uint32_t p = 0; p < npass; ++p) {
-      const uint32_t q0 = p * P;
-      const uint32_t nv = std::min(P, nq - q0);
-      uint16_t* qb = eng->q_bf16.as<uint16_t>();
-      uint64_t* out = d_keys + (size_t)q0 * k;
-      if (nv < P)
-        VS_HIP(hipMemsetAsync(qb + (size_t)nv * dim, 0, (size_t)(P - nv) * dim * 2,
-                              eng->stream),
-               "pad queries");
-      VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
-             "queries to bf16");
-      uint32_t L = 0;
-      if (!fast) {
-        VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-        VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
-                                      lists, maxl, &L, eng->stream),
-               "mfma scan (lists)");
-        VS_HIP(ev_end(eng, eng->scan_ev), "event");
-        VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-        VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream),
-               "merge");
-        VS_HIP(ev_end(eng, eng->merge_ev), "event");
-        continue;
-      }
-      // 1. sample pass: top-k of tile maxima over the first 1/64 of every
-      //    workgroup's tiles; its merged k-th key lower-bounds the global one
-      uint64_t* skeys = eng->sample_keys.as<uint64_t>();
-      VS_HIP(vsk::launch_mfma_sample(X, dim, n_rows, row_base, qb, nv, k,
-                                     std::max<uint32_t>(1, tpw / 64), lists, maxl, &L,
-                                     eng->stream),
-             "mfma sample scan");
-      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, skeys, eng->stream),
-             "sample merge");
-      const uint64_t* init = skeys + (k - 1);
-      // 2. main pass: survivors of the bound -> candidate buffers -> select
-      VS_HIP(hipMemsetAsync(ovf, 0, 4, eng->stream), "clear overflow flag");
-      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
-                                   eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(),
-                                   ovf, maxl, &L, eng->stream),
-             "mfma scan");
-      VS_HIP(ev_end(eng, eng->scan_ev), "event");
-      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-      VS_HIP(vsk::launch_select(eng->cand.as<uint64_t>(), eng->cand_cnt.as<uint32_t>(), L, cap,
-                                nv, k, out, eng->stream),
-             "select");
-      VS_HIP(ev_end(eng, eng->merge_ev), "event");
-      // 3. overflow fallback (adversarial inputs: many rows at or above the
-      //    bound): the sorted-list pass + merge, both no-ops unless *ovf != 0
-      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
-                                    maxl, &L, eng->stream),
-             "mfma scan (fallback)");
-      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream, ovf,
-                               eng->fallbacks.as<uint32_t>()),
-             "merge (fallback)");
-    }
-    return VS_OK;
-  }
-
-  // GEMV path, one query per scan
-  if (bf16)
-    VS_HIP(vsk::launch_round_bf16(qp, (uint64_t)nq * dim, qp, eng->stream), "round query");
-  const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
-  const size_t lbytes = (size_t)maxl * k * 8;
-  if (eng->lists.bytes < lbytes) {
-    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-    VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
-  }
-  for (uint32_t i = 0; i < nq; ++i) {
-    uint32_t L = 0;
-    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-    VS_HIP(vsk::launch_gemv(c.data, bf16, dim, n_rows, row_base, qp + (size_t)i * dim, k,
-                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
-           "gemv scan");
-    VS_HIP(ev_end(eng, eng->scan_ev), "event");
-    VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-    VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
-                             d_keys + (size_t)i * k, eng->stream),
-           "merge");
-    VS_HIP(ev_end(eng, eng->merge_ev), "event");
-  }
-  return VS_OK;
+  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys);
+  return search_gemv(eng, c, qp, 0, nq, k, d_keys);
 }
 
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
@@ -695,6 +734,7 @@ int vs_health(vs_engine* eng, char* buf, size_t len) {
       e = hipMemcpyAsync(&fallbacks, eng->fallbacks.p, 4, hipMemcpyDeviceToHost, eng->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(eng->stream);
     }
+    fallbacks += eng->host_fallbacks;
     if (e != hipSuccess) {
       status = "degraded";
       err = hipGetErrorString(e);

@@ -8,15 +8,20 @@ namespace vsk {
 
 // Queries handled by one launch of the MFMA scan (8 waves x 32 queries).
 constexpr uint32_t kMfmaQueries = 256;
-// Largest k the MFMA scan keeps in LDS; larger k uses the GEMV scan.
-constexpr uint32_t kMfmaMaxK = 16;
+// Largest k of the batched MFMA scan (candidate path); larger k uses the
+// GEMV scan per query. The sorted-list pass (overflow fallback) keeps
+// kMfmaListMaxK keys per query in LDS.
+constexpr uint32_t kMfmaMaxK = 128;
+constexpr uint32_t kMfmaListMaxK = 16;
 // Largest k any scan supports (GEMV register lists: 16 entries per lane).
 constexpr uint32_t kMaxK = 1024;
-// MFMA main pass: workgroups per launch (<= CUs), candidate slots per
-// (workgroup, query), and the select kernel's LDS capacity (all slots full).
+// MFMA passes: workgroups per launch (<= CUs), most candidate slots per
+// (workgroup, query), sample-pass tiles per workgroup, and the select
+// kernel's LDS buffer (candidates are streamed through it in chunks).
 constexpr uint32_t kMfmaMaxLists = 256;
-constexpr uint32_t kMfmaCandCap = 64;
-constexpr uint32_t kMfmaSelCap = kMfmaMaxLists * kMfmaCandCap;
+constexpr uint32_t kMfmaMaxCandCap = 1024;
+constexpr uint32_t kMfmaMaxSampleTiles = 64;
+constexpr uint32_t kMfmaSelBuf = 8192;
 
 // Preprocess n fp32 vectors (n x dim, device) and store them as the
 // collection dtype into dst rows: dst_rows[i] if non-null, else dst0 + i.
@@ -42,21 +47,24 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 
 // Batched bf16 scan on MFMA with fused top-k. Q is
-// kMfmaQueries x dim bf16 (zero-padded), nq_valid <= kMfmaQueries; one
-// workgroup per CU streams a contiguous row range (nlists workgroups).
-//  * sample pass: first max_tiles 32-row tiles of every workgroup, top-k of
-//    the tile maxima per query -> lists[nlists][kMfmaQueries][k] (sorted);
+// kMfmaQueries x dim bf16 (zero-padded), nq_valid <= kMfmaQueries, k <=
+// kMfmaMaxK; one workgroup per CU streams a contiguous row range (nlists
+// workgroups).
+//  * sample pass: first max_tiles 32-row tiles of every workgroup; each
+//    tile's maximum per query -> cand[nlists][kMfmaQueries][max_tiles] with
+//    counts cand_cnt; launch_select(.., k, ..) then gives per query the top k
+//    of those maxima, whose k-th key lower-bounds the global k-th key;
 //  * main pass: every row, survivors of the per-query lower bound
 //    init_th[q * init_stride] appended to cand[nlists][kMfmaQueries][cap]
-//    with counts cand_cnt[nlists][kMfmaQueries]; sets *overflow = 1 when a
-//    buffer would overflow (the caller then runs the lists pass);
-//  * lists pass: the main pass with per-query sorted lists in LDS (any
-//    input), written like the sample pass; a no-op unless run_if is null or
-//    *run_if != 0.
+//    with counts cand_cnt; sets *overflow = 1 when a buffer would overflow
+//    (the caller then redoes the batch exactly: lists pass or GEMV);
+//  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
+//    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; a no-op
+//    unless run_if is null or *run_if != 0.
 bool mfma_supported(uint32_t dim);
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
-                              uint32_t k, uint32_t max_tiles, uint64_t* lists,
+                              uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
                               uint32_t max_lists, uint32_t* nlists, hipStream_t st);
 hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                             const uint16_t* Q, uint32_t nq_valid, uint32_t k,
@@ -68,9 +76,14 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st);
-// Top-k of the main pass's candidates for queries 0 .. nq-1 -> out[nq][k].
+// Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap]
+// (counts cand_cnt) for queries 0 .. nq-1 -> out[nq][k], sorted, 0-padded.
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
                          uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st);
+// Sample tiles per workgroup, and the main pass's candidate capacity per
+// (workgroup, query) sized from the expected survivors of the sample bound.
+uint32_t mfma_sample_tiles(uint32_t n_rows);
+uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles);
 uint32_t mfma_max_lists(uint32_t n_rows);
 uint32_t mfma_tiles_per_wg(uint32_t n_rows);
 void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);

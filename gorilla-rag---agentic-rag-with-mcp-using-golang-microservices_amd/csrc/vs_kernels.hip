@@ -551,10 +551,10 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // budget), which halves the LDS reads per MFMA (each A fragment feeds 4).
 constexpr int kMfG = 2;
 constexpr int mf_waves(int g) { return 16 / g; }
-constexpr int kMfListLen = (int)kMfmaMaxK;                      // entries per query list
+constexpr int kMfListLen = (int)kMfmaListMaxK;                  // entries per query list
 constexpr int kMfListBytes = (int)kMfmaQueries * kMfListLen * 8;  // 32 KiB
 constexpr int kMfRingBytes = 112 * 1024;
-static_assert(kMfmaMaxK == 16, "list insert assumes 4 lanes x 4 entries per query");
+static_assert(kMfmaListMaxK == 16, "list insert assumes 4 lanes x 4 entries per query");
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
@@ -597,14 +597,23 @@ __device__ __forceinline__ void wait_vmcnt() {
 // ds_read of the ring; completion is counted by wait_vmcnt<N>() by hand.
 // M0 is written and restored inside the statement (§5.7: M0 is reserved).
 // Address = wave-uniform 64-bit base (SGPRs) + per-lane 32-bit byte offset.
+template <bool NT = false>
 __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds) {
   unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds)
+        : "memory");
 }
 
 // Ablation only (MODE 11): the same LDS-DMA instruction moving 4 B per lane.
@@ -702,19 +711,20 @@ struct MfShape {
 // merges the two row halves' MFMA chains: invalid as a timing), 11 = 1 with
 // 4-B LDS-DMA (a quarter of the bytes, same instructions). VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1;
 // VAR 128: each step's reads and MFMAs pinned in program order; VAR 512:
-// the chunk's LDS-DMA pieces spread over its steps instead of at its head.
+// the chunk's LDS-DMA pieces spread over its steps instead of at its head;
+// VAR 1024: non-temporal (nt) LDS-DMA loads of the corpus stream.
 template <int D, int MODE = 0, int VAR = 0, int G = kMfG>
 __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
   constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
   static_assert(WAVES * QPW == (int)kMfmaQueries, "one launch covers kMfmaQueries");
-  // VAR 256: a 144 KiB ring (more chunks in flight) where no LDS lists are kept
-  constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 3 && MODE != 8;
+  // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
+  constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
-                    kBigRing ? (int)kMfmaQueries * 4 : kMfListBytes, WAVES>;
+                    MODE == 8 ? kMfListBytes : (int)kMfmaQueries * 4, WAVES>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
-  constexpr bool kLists = MODE == 3 || MODE == 8;
-  constexpr bool kCand = MODE == 0;
+  constexpr bool kLists = MODE == 8;
+  constexpr bool kCand = MODE == 0 || MODE == 3;
   constexpr int PPW = S::PPW;
   constexpr int kPD0 = (VAR & 64) ? 3 : ((VAR & 32) ? 2 : 1);
   constexpr int kPD = ((S::CPT * S::CT) % (kPD0 + 1) == 0) ? kPD0 : 1;
@@ -724,7 +734,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
   lds_vu64_t* lists = (lds_vu64_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES);
-  uint32_t* counts = (uint32_t*)(smem + S::NSLOT * S::CHUNK_BYTES);  // MODE 0 (aliases lists)
+  uint32_t* counts = (uint32_t*)(smem + S::NSLOT * S::CHUNK_BYTES);  // MODE 0 / 3
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -785,7 +795,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
     if constexpr (MODE == 11)
       glds4(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
     else
-      glds16(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
+      glds16<(VAR & 1024) != 0>(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
   };
   auto advance = [&]() {
     const bool last = unext == S::CPT - 1;
@@ -970,7 +980,9 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
             const uint32_t pos = __hip_atomic_fetch_add(counts + ql[g], n, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
             if (pos + n > a.cand_cap) {
-              *a.overflow = 1u;
+              // main pass: the caller re-runs the batch exactly; sample pass:
+              // dropping tile maxima only lowers the bound (still valid)
+              if constexpr (MODE == 0) *a.overflow = 1u;
             } else {
               uint64_t* dst =
                   a.cand + ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * a.cand_cap + pos;
@@ -1055,14 +1067,16 @@ static bool mfma_args_ok(uint32_t dim, uint32_t n_rows, uint32_t nq_valid, uint3
 
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
-                              uint32_t k, uint32_t max_tiles, uint64_t* lists,
+                              uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
                               uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || max_tiles == 0) return hipErrorInvalidValue;
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || max_tiles == 0 || max_tiles > kMfmaMaxCandCap)
+    return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.lists = lists, a.n_rows = n_rows, a.row_base = row_base;
-  a.max_tiles = max_tiles, a.nq_valid = nq_valid, a.k = k;
+  a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = max_tiles;
+  a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
+  a.k = k;
   return mfma_launch_mode<3>(dim, *nlists, a, st);
 }
 
@@ -1071,7 +1085,7 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k)) return hipErrorInvalidValue;
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || k > kMfmaListMaxK) return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
@@ -1085,7 +1099,8 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
                             const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
                             uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
                             uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap == 0) return hipErrorInvalidValue;
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap == 0 || cand_cap > kMfmaMaxCandCap)
+    return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
@@ -1095,12 +1110,37 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
   return mfma_launch_mode<0>(dim, *nlists, a, st);
 }
 
+uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
+  uint32_t nwg, rpw;
+  mfma_grid(n_rows, &nwg, &rpw);
+  const double tpw = (rpw + 31) / 32;
+  // expected survivors of the sample bound per (workgroup, query): the bound
+  // is the k-th of ~k / f rows (f = sampled fraction), spread over nwg
+  const double e = (double)k * tpw / (double)(sample_tiles ? sample_tiles : 1) / nwg;
+  const double want = 3.0 * e + 32.0;
+  uint32_t cap = 64;
+  while (cap < want && cap < kMfmaMaxCandCap) cap <<= 1;
+  return cap;
+}
+
+uint32_t mfma_sample_tiles(uint32_t n_rows) {
+  const uint32_t tpw = mfma_tiles_per_wg(n_rows);
+  uint32_t st = tpw / 64;
+  if (st < 1) st = 1;
+  if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;
+  return st;
+}
+
 // ---------------------------------------------------------------------------
-// select: top-k of the main pass's per-workgroup candidate buffers
+// select: top-k of per-workgroup candidate buffers
 // ---------------------------------------------------------------------------
-// One workgroup per query: the (few) candidates of all workgroups are
-// gathered into LDS, sorted (bitonic, descending) and the first k written.
-// Capacity covers every buffer full (kMfmaSelCap >= nwg * cand_cap).
+// One workgroup per query. First bound: the k-th largest of the per-buffer
+// maxima (k keys of k distinct rows) -- no key below it can be in the top k,
+// which leaves a few dozen of the usual hundreds of candidates. The valid
+// candidates of all workgroups (prefix sum of the counts) are then streamed
+// through an LDS buffer that also holds the running top-k: keys reaching the
+// bound are appended, and the buffer is sorted (bitonic, descending)
+// whenever a chunk added something. Any total is handled.
 constexpr int kSelThreads = 512;
 
 __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, int nthreads) {
@@ -1124,35 +1164,65 @@ __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, i
 __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
     uint32_t cap, uint32_t k, uint64_t* __restrict__ out) {
-  __shared__ uint64_t buf[kMfmaSelCap];
-  __shared__ uint32_t lcnt[kMfmaMaxLists];
-  __shared__ uint32_t total;
+  __shared__ uint64_t buf[kMfmaSelBuf];
+  __shared__ uint64_t lmax[kMfmaMaxLists];
+  __shared__ uint32_t pre[kMfmaMaxLists + 1];
+  __shared__ uint32_t fill;
   const uint32_t q = blockIdx.x;
-  if (threadIdx.x == 0) total = 0;
-  for (uint32_t l = threadIdx.x; l < nwg; l += kSelThreads) lcnt[l] = cnt[(size_t)l * kMfmaQueries + q];
-  __syncthreads();
-  const uint32_t slots = nwg * cap;
-  for (uint32_t i = threadIdx.x; i < slots; i += kSelThreads) {
-    const uint32_t l = i / cap, j = i - l * cap;
-    if (j < lcnt[l]) {
-      const uint64_t x = cand[((size_t)l * kMfmaQueries + q) * cap + j];
-      buf[atomicAdd(&total, 1u)] = x;
-    }
+  for (uint32_t l = threadIdx.x; l < kMfmaMaxLists; l += kSelThreads) {
+    uint32_t c = l < nwg ? cnt[(size_t)l * kMfmaQueries + q] : 0;
+    c = c < cap ? c : cap;
+    uint64_t m = 0;
+    const uint64_t* lst = cand + ((size_t)l * kMfmaQueries + q) * cap;
+    for (uint32_t j = 0; j < c; ++j) m = lst[j] > m ? lst[j] : m;
+    lmax[l] = m;
+    if (l < nwg) pre[l + 1] = c;
   }
   __syncthreads();
-  const uint32_t n = total;
-  int p2 = 1;
-  while ((uint32_t)p2 < n) p2 <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+  bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+  if (threadIdx.x == 0) {
+    pre[0] = 0;
+    for (uint32_t l = 0; l < nwg; ++l) pre[l + 1] += pre[l];
+  }
   __syncthreads();
-  if (p2 > 1) bitonic_sort_desc_n(buf, p2, kSelThreads);
-  for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < n ? buf[j] : 0;
+  const uint32_t total = pre[nwg];
+  const uint32_t chunk = kMfmaSelBuf - k;
+  // admit keys > thr (0 marks an empty slot)
+  uint64_t thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+  uint32_t nR = 0;  // running top-k in buf[0, nR)
+  for (uint32_t base = 0; base < total; base += chunk) {
+    if (threadIdx.x == 0) fill = nR;
+    __syncthreads();
+    const uint32_t end = base + chunk < total ? base + chunk : total;
+    for (uint32_t i = base + threadIdx.x; i < end; i += kSelThreads) {
+      uint32_t lo = 0, hi = nwg;  // last l with pre[l] <= i
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= i) lo = mid; else hi = mid;
+      }
+      const uint64_t x = cand[((size_t)lo * kMfmaQueries + q) * cap + (i - pre[lo])];
+      if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
+    }
+    __syncthreads();
+    const uint32_t c = fill;
+    if (c > nR) {
+      int p2 = 1;
+      while ((uint32_t)p2 < c) p2 <<= 1;
+      for (uint32_t i = c + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+      __syncthreads();
+      bitonic_sort_desc_n(buf, p2, kSelThreads);
+      nR = c < k ? c : k;
+      if (nR == k && buf[k - 1] > thr) thr = buf[k - 1];
+    }
+    __syncthreads();
+  }
+  for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
 }
 
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
                          uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st) {
-  if (nwg == 0 || nwg > kMfmaMaxLists || (uint64_t)nwg * cap > kMfmaSelCap || k == 0 ||
-      k > kMfmaMaxK || nq == 0 || nq > kMfmaQueries)
+  if (nwg == 0 || nwg > kMfmaMaxLists || cap == 0 || k == 0 || k > kMfmaMaxK || nq == 0 ||
+      nq > kMfmaQueries)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_cand_kernel, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt, nwg,
                      cap, k, out);

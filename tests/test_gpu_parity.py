@@ -116,7 +116,8 @@ def corpus_fast(engine, orc):
     return "fast768", orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
 
 
-@pytest.mark.parametrize("nq,k", [(2, 10), (256, 10), (300, 16), (77, 1), (256, 5)])
+@pytest.mark.parametrize("nq,k", [(2, 10), (256, 10), (300, 16), (77, 1), (256, 5), (256, 17),
+                                  (64, 50), (300, 100), (33, 128)])
 def test_mfma_candidate_path(engine, orc, corpus_fast, nq, k):
     import json
     name, X = corpus_fast
@@ -143,11 +144,11 @@ def test_mfma_overflow_fallback(engine, orc):
     Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 7, 40, dim),
                         base[12_345:12_346] * 3.0])
     before = json.loads(engine.health())["mfma_fallbacks"]
-    for k in (10, 16):
+    for k in (10, 16, 50):  # k <= 16: sorted-list pass; k > 16: GEMV re-run
         s, r, c = engine.search("ties", Q, k)
         assert r[0].tolist() == list(range(k)) and r[-1].tolist() == list(range(k))
         _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
-    assert json.loads(engine.health())["mfma_fallbacks"] >= before + 2
+    assert json.loads(engine.health())["mfma_fallbacks"] >= before + 3
     engine.drop_collection("ties")
 
 

@@ -53,8 +53,8 @@ int main(int argc, char** argv) {
   const int reps = argc > 2 ? atoi(argv[2]) : 8;
   const uint32_t k = 10;
   uint16_t *X, *Q;
-  uint64_t *out, *skeys, *cand;
-  uint32_t *cnt, *ovf;
+  uint64_t *out, *skeys, *cand, *scand;
+  uint32_t *cnt, *scnt, *ovf;
   CK(hipMalloc(&X, ((size_t)n + 32) * 768 * 2));
   CK(hipMemset(X, 0, ((size_t)n + 32) * 768 * 2));
   CK(hipMalloc(&Q, 256 * 768 * 2));
@@ -65,7 +65,10 @@ int main(int argc, char** argv) {
   uint32_t rpw;
   mfma_grid(n, &c.nwg, &rpw);
   CK(hipMalloc(&out, (size_t)c.nwg * 256 * k * 8));
-  CK(hipMalloc(&cand, (size_t)c.nwg * 256 * kMfmaCandCap * 8));
+  const uint32_t st = mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
+  CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 8));
+  CK(hipMalloc(&scand, (size_t)c.nwg * 256 * st * 8));
+  CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4));
   CK(hipMalloc(&ovf, 4));
   CK(hipMemset(ovf, 0, 4));
@@ -79,8 +82,8 @@ int main(int argc, char** argv) {
   std::vector<float> ts;
   for (int r = 0; r < reps; ++r) {
     hipEventRecord(a, 0);
-    CK(launch_mfma_sample(X, 768, n, 0, Q, 256, k, tpw / 64 ? tpw / 64 : 1, out, c.nwg, &L, 0));
-    CK(launch_merge(out, L, (uint64_t)256 * k, k, 256, k, k, skeys, 0));
+    CK(launch_mfma_sample(X, 768, n, 0, Q, 256, k, st, scand, scnt, c.nwg, &L, 0));
+    CK(launch_select(scand, scnt, L, st, 256, k, skeys, 0));
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms = 0;
@@ -90,23 +93,21 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   MfArgs& g = c.args;
   g.X = X, g.Q = Q, g.init_th = skeys + (k - 1), g.init_stride = k, g.lists = out;
-  g.cand = cand, g.cand_cnt = cnt, g.overflow = ovf, g.cand_cap = kMfmaCandCap;
+  g.cand = cand, g.cand_cnt = cnt, g.overflow = ovf, g.cand_cap = cap;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
   std::vector<Arm> arms = {
       {"main cand G2", run<0, 0, 2>, true, {}},
-      {"main G2 pin pd2", run<0, 160, 2>, true, {}},
+      {"main cand G2 nt", run<0, 1024, 2>, true, {}},
       {"no-epi G2", run<1, 0, 2>, false, {}},
-      {"no-epi G2 spread", run<1, 512, 2>, false, {}},
-      {"main cand G4 pd2", run<0, 160, 4>, true, {}},
-      {"main G4 pd2 spread", run<0, 160 + 512, 4>, true, {}},
-      {"no-epi G4 pd2", run<1, 160, 4>, false, {}},
-      {"no-epi G4 pd2 spread", run<1, 160 + 512, 4>, false, {}},
-      {"no-epi G4 pd3 spread", run<1, 192 + 512, 4>, false, {}},
-      {"mfma+bar G4 pd2", run<4, 160, 4>, false, {}},
-      {"dma-only G4", run<2, 0, 4>, false, {}},
+      {"no-epi G2 nt", run<1, 1024, 2>, false, {}},
+      {"dma-only", run<2, 0, 2>, false, {}},
+      {"dma-only nt", run<2, 1024, 2>, false, {}},
+      {"dma-only big", run<2, 256, 2>, false, {}},
+      {"dma-only big nt", run<2, 256 + 1024, 2>, false, {}},
   };
+
 
 
 
@@ -136,7 +137,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
   uint64_t tot = 0, mx = 0;
   for (uint32_t v : hc) tot += v, mx = v > mx ? v : mx;
-  printf("grid %u WGs x %u rows, sample tiles/wg %u, overflow %u, candidates/query %.1f, max per buffer %lu\n",
-         c.nwg, rpw, tpw / 64, of, (double)tot / 256, (unsigned long)mx);
+  printf("cap %u; grid %u WGs x %u rows, sample tiles/wg %u, overflow %u, candidates/query %.1f, max per buffer %lu\n",
+         cap, c.nwg, rpw, st, of, (double)tot / 256, (unsigned long)mx);
   return 0;
 }
