@@ -37,6 +37,29 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
   return v;
 }
+// Wave sum on the VALU (no LDS-path shuffles): DPP xor-1 / xor-2 / half-row
+// and row mirrors leave every lane of 16-lane row r holding the row sum S_r
+// (symmetric pairs: bit-identical in all lanes), then (S_0 + S_1) + (S_2 +
+// S_3) from four readlanes -- wave-uniform by construction. (The gfx950
+// permlane16/32_swap builtins were miscompiled by this hipcc: the second
+// result aliased the first; tools/test_dpp.hip.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  const float s0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float s1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float s3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return (s0 + s1) + (s2 + s3);
+}
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
@@ -225,6 +248,11 @@ constexpr int kGemvThreads = 512;
 constexpr int kGemvWaves = kGemvThreads / 64;
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+// non-temporal loads: 75.5% -> 81-86% of 8 TB/s on 10M x 768 bf16 and
+// 1M x 768 fp32 (tools/ablate_gemv.hip). VAR 2 (DPP wave
+// sum) measured within noise of the shuffle sum.
+constexpr int kGemvVar = 1;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // Rows of D elements are cut into 16-byte chunks; one wave covers RB whole
 // rows per step with J chunks per lane (RB*CPR == 64*J), so every load is a
@@ -291,7 +319,9 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
   }
 }
 
-template <int D, bool BF16, int KPL>
+// VAR (ablation knobs, tools/ablate_gemv.hip): 1 = non-temporal loads,
+// 2 = DPP/permlane wave sum, 4 = loads two steps ahead instead of one.
+template <int D, bool BF16, int KPL, int VAR = kGemvVar>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, uint32_t k, uint32_t rows_per_wave,
@@ -322,24 +352,37 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   const char* X = (const char*)Xv;
 
   if (lo < hi) {
-    uint4 cur[S::J], nxt[S::J];
+    constexpr bool kNT = (VAR & 1) != 0, kDpp = (VAR & 2) != 0;
+    constexpr int DEPTH = (VAR & 4) ? 2 : 1;
+    uint4 buf[DEPTH + 1][S::J];
     auto load = [&](uint4* dst, uint32_t r0) {
 #pragma unroll
       for (int j = 0; j < S::J; ++j) {
         uint32_t row = r0 + rowsel[j];
         row = row < hi ? row : hi - 1;
-        dst[j] = *(const uint4*)(X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16);
+        const char* p = X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16;
+        if constexpr (kNT) {
+          const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+          dst[j] = uint4{v[0], v[1], v[2], v[3]};
+        } else {
+          dst[j] = *(const uint4*)p;
+        }
       }
     };
-    load(cur, lo);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const uint32_t r0 = lo + d * S::RB;
+      load(buf[d], r0 < hi ? r0 : lo);
+    }
     for (uint32_t r = lo; r < hi; r += S::RB) {
-      load(nxt, r + S::RB < hi ? r + S::RB : r);
+      const uint32_t rn = r + DEPTH * S::RB;
+      load(buf[DEPTH], rn < hi ? rn : r);
       float p[S::RB];
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) p[b] = 0.f;
 #pragma unroll
       for (int j = 0; j < S::J; ++j) {
-        const float d = chunk_dot<BF16>(cur[j], qv[j]);
+        const float d = chunk_dot<BF16>(buf[0][j], qv[j]);
         if constexpr (S::RB == 1) {
           p[0] += d;
         } else {
@@ -349,7 +392,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
       }
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) {
-        const float s = wave_sum(p[b]);
+        const float s = kDpp ? wave_sum_dpp(p[b]) : wave_sum(p[b]);
         const uint32_t row = r + b;
         if (row < hi) {
           const uint64_t key = make_key(s, row_base + row);
@@ -360,7 +403,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
         }
       }
 #pragma unroll
-      for (int j = 0; j < S::J; ++j) cur[j] = nxt[j];
+      for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int j = 0; j < S::J; ++j) buf[d][j] = buf[d + 1][j];
     }
   }
   gemv_emit<KPL>(L, theta, k, lane, w, out);
@@ -384,8 +429,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
   for (uint32_t r = lo; r < hi; ++r) {
     float p = 0.f;
     for (uint32_t d = lane; d < dim; d += 64) {
-      const float x = BF16 ? vs::bf16_to_f32(((const uint16_t*)Xv)[(size_t)r * dim + d])
-                           : ((const float*)Xv)[(size_t)r * dim + d];
+      const float x =
+          BF16 ? vs::bf16_to_f32(__builtin_nontemporal_load((const uint16_t*)Xv + (size_t)r * dim + d))
+               : __builtin_nontemporal_load((const float*)Xv + (size_t)r * dim + d);
       p = fmaf(x, q[d], p);
     }
     const float s = wave_sum(p);
@@ -1295,13 +1341,21 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
     if (threadIdx.x == 0) cnt = nR;
     __syncthreads();
     const uint64_t end = base + chunk < total ? base + chunk : total;
-    for (uint64_t i = base + threadIdx.x; i < end; i += kMergeThreads) {
-      const uint32_t l = (uint32_t)(i / kin), j = (uint32_t)(i - (uint64_t)l * kin);
-      const uint64_t x = lists[l * lstride + q * qstride + j];
-      if (x > thr) {
-        const uint32_t idx = atomicAdd(&cnt, 1u);
-        buf[idx] = x;
+    // 8 independent loads in flight per thread, then the (rare) appends
+    for (uint64_t i0 = base + threadIdx.x; i0 < end; i0 += 8 * kMergeThreads) {
+      uint64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kMergeThreads;
+        x[u] = 0;
+        if (i < end) {
+          const uint32_t l = (uint32_t)(i / kin), j = (uint32_t)(i - (uint64_t)l * kin);
+          x[u] = lists[l * lstride + q * qstride + j];
+        }
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (x[u] > thr) buf[atomicAdd(&cnt, 1u)] = x[u];
     }
     __syncthreads();
     const uint32_t c = cnt;
