@@ -89,7 +89,9 @@ struct EventPair {
 struct vs_engine {
   int device = 0;
   uint32_t flags = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t own = nullptr;     // the engine's stream
+  hipStream_t stream = nullptr;  // the stream device work is enqueued on now (own or a caller's)
+  hipEvent_t xev = nullptr;      // orders a newly used stream after the previous one
   std::string device_name;
   std::mutex map_mu;
   std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
@@ -102,6 +104,7 @@ struct vs_engine {
   std::vector<uint64_t> h_keys;
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
+  std::vector<hipEvent_t> ev_pool;  // recycled timing events (none created on the hot path)
   double scan_ms = 0, merge_ms = 0;
   uint64_t scan_n = 0, merge_n = 0;
 };
@@ -116,20 +119,41 @@ std::shared_ptr<Collection> find_coll(vs_engine* eng, const char* name) {
 
 hipError_t set_dev(vs_engine* eng) { return hipSetDevice(eng->device); }
 
+// Makes `s` the engine's current stream (work_mu held). Work enqueued on s
+// is ordered after everything enqueued so far on the previous stream, so the
+// scratch buffers are never used by two streams at once; a caller that keeps
+// using one stream (a serving loop on torch's current stream) pays nothing.
+hipError_t use_stream(vs_engine* eng, hipStream_t s) {
+  if (s == eng->stream) return hipSuccess;
+  hipError_t e = hipEventRecord(eng->xev, eng->stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->xev, 0);
+  if (e == hipSuccess) eng->stream = s;
+  return e;
+}
+
 bool timing_on(vs_engine* eng) { return (eng->flags & VS_FLAG_TIMING) != 0; }
 
+bool timing_wanted(vs_engine* eng, const std::vector<EventPair>& v) {
+  return timing_on(eng) && (&v == &eng->scan_ev || (eng->flags & VS_FLAG_TIMING_MERGE));
+}
+
 hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
-  if (!timing_on(eng)) return hipSuccess;
+  if (!timing_wanted(eng, v)) return hipSuccess;
   EventPair p{};
-  hipError_t e = hipEventCreate(&p.a);
-  if (e != hipSuccess) return e;
-  e = hipEventCreate(&p.b);
-  if (e != hipSuccess) return e;
+  for (hipEvent_t* ev : {&p.a, &p.b}) {
+    if (!eng->ev_pool.empty()) {
+      *ev = eng->ev_pool.back();
+      eng->ev_pool.pop_back();
+    } else {
+      hipError_t e = hipEventCreate(ev);
+      if (e != hipSuccess) return e;
+    }
+  }
   v.push_back(p);
   return hipEventRecord(p.a, eng->stream);
 }
 hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
-  if (!timing_on(eng) || v.empty()) return hipSuccess;
+  if (!timing_wanted(eng, v) || v.empty()) return hipSuccess;
   return hipEventRecord(v.back().b, eng->stream);
 }
 
@@ -222,25 +246,25 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
-  const size_t bbytes = (size_t)P * dim * 2;
   const size_t lbytes = (size_t)maxl * P * std::min(k, vsk::kMfmaListMaxK) * 8;
   const size_t sbytes = (size_t)P * k * 8;
   const size_t cbytes = (size_t)maxl * P * cap * 8;
-  const size_t scbytes = (size_t)maxl * P * st * 8;
-  const size_t nbytes = (size_t)maxl * P * 4;
-  if (eng->lists.bytes < lbytes || eng->q_bf16.bytes < bbytes ||
-      eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
+  const size_t scbytes = (size_t)maxl * P * 4 * st * 8;
+  const size_t nbytes = (size_t)maxl * P * 4 * 4;
+  if (eng->lists.bytes < lbytes || eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
       eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes ||
       eng->scand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
-    VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
     VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
     VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
     VS_HIP(eng->scand.ensure(scbytes), "alloc sample candidate scratch");
     VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
     VS_HIP(eng->scand_cnt.ensure(nbytes), "alloc sample candidate counts");
-    VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
+    if (eng->overflow.bytes < 4) {
+      VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
+      VS_HIP(hipMemsetAsync(eng->overflow.p, 0, 4, eng->stream), "clear overflow flag");
+    }
     if (eng->fallbacks.bytes < 4) {
       VS_HIP(eng->fallbacks.ensure(4), "alloc fallback counter");
       VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
@@ -249,16 +273,11 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint16_t* X = (const uint16_t*)c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
   uint32_t* ovf = eng->overflow.as<uint32_t>();
-  uint16_t* qb = eng->q_bf16.as<uint16_t>();
   for (uint32_t p = 0; p < npass; ++p) {
     const uint32_t q0 = p * P;
     const uint32_t nv = std::min(P, nq - q0);
     uint64_t* out = d_keys + (size_t)q0 * k;
-    if (nv < P)
-      VS_HIP(hipMemsetAsync(qb + (size_t)nv * dim, 0, (size_t)(P - nv) * dim * 2, eng->stream),
-             "pad queries");
-    VS_HIP(vsk::launch_to_bf16(qp + (size_t)q0 * dim, (uint64_t)nv * dim, qb, eng->stream),
-           "queries to bf16");
+    const uint16_t* qb = eng->q_bf16.as<uint16_t>() + (size_t)q0 * dim;
     uint32_t L = 0;
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
@@ -278,12 +297,11 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                    eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), maxl,
                                    &L, eng->stream),
            "mfma sample scan");
-    VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, st, nv,
-                              k, skeys, eng->stream),
-           "sample select");
+    VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, 4 * st,
+                              nv, k, skeys, eng->stream, ovf),
+           "sample select (clears the overflow flag)");
     const uint64_t* init = skeys + (k - 1);
     // 2. main pass -> candidates -> select
-    VS_HIP(hipMemsetAsync(ovf, 0, 4, eng->stream), "clear overflow flag");
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
                                  eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(), ovf,
@@ -339,10 +357,22 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     VS_HIP(eng->q_pre.ensure(qbytes), "alloc query scratch");
   }
   float* qp = eng->q_pre.as<float>();
-  VS_HIP(vsk::launch_preprocess(d_q, nq, dim, cosine, false, qp, nullptr, 0, eng->stream),
-         "query preprocess");
-
   const bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
+  // the MFMA path reads a bf16 copy, 256 queries per pass (rows past nq are
+  // padding: finite, and masked by the kernels)
+  uint16_t* qb = nullptr;
+  if (use_mfma) {
+    const uint32_t P = vsk::kMfmaQueries;
+    const size_t bbytes = (size_t)((nq + P - 1) / P) * P * dim * 2;
+    if (eng->q_bf16.bytes < bbytes) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->q_bf16.ensure(bbytes), "alloc bf16 query scratch");
+      VS_HIP(hipMemsetAsync(eng->q_bf16.p, 0, bbytes, eng->stream), "zero bf16 queries");
+    }
+    qb = eng->q_bf16.as<uint16_t>();
+  }
+  VS_HIP(vsk::launch_preprocess(d_q, nq, dim, cosine, false, qp, nullptr, 0, eng->stream, qb),
+         "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys);
   return search_gemv(eng, c, qp, 0, nq, k, d_keys);
 }
@@ -395,7 +425,9 @@ int vs_open(const vs_config* cfg, vs_engine** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
     eng->device_name = std::string(prop.name) + " " + prop.gcnArchName;
-  VS_HIP(hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking), "stream");
+  VS_HIP(hipStreamCreateWithFlags(&eng->own, hipStreamNonBlocking), "stream");
+  eng->stream = eng->own;
+  VS_HIP(hipEventCreateWithFlags(&eng->xev, hipEventDisableTiming), "event");
   vsk::device_cu_count();
   *out = eng.release();
   return VS_OK;
@@ -413,8 +445,11 @@ void vs_close(vs_engine* eng) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
   }
+  for (hipEvent_t ev : eng->ev_pool) (void)hipEventDestroy(ev);
   eng->colls.clear();
-  (void)hipStreamDestroy(eng->stream);
+  (void)hipStreamSynchronize(eng->own);
+  if (eng->xev) (void)hipEventDestroy(eng->xev);
+  (void)hipStreamDestroy(eng->own);
   delete eng;
 }
 
@@ -442,6 +477,7 @@ int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim, int met
   if (capacity_hint) {
     std::unique_lock<std::shared_mutex> wl(c->mu);
     std::lock_guard<std::mutex> g(eng->work_mu);
+    VS_HIP(use_stream(eng, eng->own), "stream order");
     int rc = grow(eng, *c, capacity_hint);
     if (rc != VS_OK) {
       std::lock_guard<std::mutex> g2(eng->map_mu);
@@ -481,6 +517,7 @@ int vs_collection_drop(vs_engine* eng, const char* name) {
   std::unique_lock<std::shared_mutex> wl(c->mu);
   std::lock_guard<std::mutex> g(eng->work_mu);
   (void)set_dev(eng);
+  VS_HIP(use_stream(eng, eng->own), "stream order");
   (void)hipStreamSynchronize(eng->stream);
   return VS_OK;  // memory released with the last reference
 }
@@ -520,6 +557,7 @@ int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim_in,
   if (expect >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
   int rc = grow(eng, *c, expect);
   if (rc != VS_OK) return rc;
   const uint64_t m = keep_idx.size();
@@ -566,6 +604,7 @@ int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed) {
   if (c->rows + n >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
   int rc = grow(eng, *c, c->rows + n);
   if (rc != VS_OK) return rc;
   VS_HIP(vsk::launch_generate(seed, c->row_base + c->rows, n, c->dim,
@@ -599,6 +638,7 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, f
   if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
   const size_t count = (size_t)n * c->dim;
   if (c->dtype == VS_DTYPE_F32) {
     VS_HIP(hipMemcpyAsync(out, (const char*)c->data + first * c->row_bytes(), count * 4,
@@ -632,6 +672,7 @@ int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t n
   std::shared_lock<std::shared_mutex> rl(c->mu);
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
   const size_t qbytes = (size_t)nq * c->dim * 4;
   const size_t kbytes = (size_t)nq * k * 8;
   if (eng->q_in.bytes < qbytes || eng->keys.bytes < kbytes) {
@@ -667,18 +708,9 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
   std::shared_lock<std::shared_mutex> rl(c->mu);
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
-  hipStream_t cs = (hipStream_t)stream;
-  hipEvent_t ev;
-  VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
-  VS_HIP(hipEventRecord(ev, cs), "event record");
-  VS_HIP(hipStreamWaitEvent(eng->stream, ev, 0), "stream wait");
-  int rc = search_core(eng, *c, d_queries, nq, k, d_keys);
-  if (rc == VS_OK) {
-    VS_HIP(hipEventRecord(ev, eng->stream), "event record");
-    VS_HIP(hipStreamWaitEvent(cs, ev, 0), "stream wait");
-  }
-  (void)hipEventDestroy(ev);
-  return rc;
+  // enqueue on the caller's stream (ordered after the engine's previous work)
+  VS_HIP(use_stream(eng, (hipStream_t)stream), "stream order");
+  return search_core(eng, *c, d_queries, nq, k, d_keys);
 }
 
 int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
@@ -757,15 +789,15 @@ int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double*
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(hipDeviceSynchronize(), "timing sync");
-  auto drain = [](std::vector<EventPair>& v, double& acc, uint64_t& n) {
+  auto drain = [eng](std::vector<EventPair>& v, double& acc, uint64_t& n) {
     for (auto& p : v) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
         acc += ms;
         ++n;
       }
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
+      eng->ev_pool.push_back(p.a);
+      eng->ev_pool.push_back(p.b);
     }
     v.clear();
   };

@@ -24,11 +24,12 @@ constexpr uint32_t kMfmaMaxSampleTiles = 64;
 constexpr uint32_t kMfmaSelBuf = 8192;
 
 // Preprocess n fp32 vectors (n x dim, device) and store them as the
-// collection dtype into dst rows: dst_rows[i] if non-null, else dst0 + i.
+// collection dtype into dst rows: dst_rows[i] if non-null, else dst0 + i;
+// also_bf16 (nullable) receives a bf16 copy at the same rows.
 hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
                              bool cosine, bool bf16, void* dst,
                              const uint64_t* dst_rows, uint64_t dst0,
-                             hipStream_t st);
+                             hipStream_t st, uint16_t* also_bf16 = nullptr);
 
 // Generate n synthetic unit rows with global numbers grow0 .. grow0+n-1 and
 // store them into dst rows dst0 .. (bf16 or fp32), or as fp32 when f32_out.
@@ -51,13 +52,15 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 // kMfmaMaxK; one workgroup per CU streams a contiguous row range (nlists
 // workgroups).
 //  * sample pass: first max_tiles 32-row tiles of every workgroup; each
-//    tile's maximum per query -> cand[nlists][kMfmaQueries][max_tiles] with
-//    counts cand_cnt; launch_select(.., k, ..) then gives per query the top k
-//    of those maxima, whose k-th key lower-bounds the global k-th key;
+//    tile's maximum per query -> cand[nlists][kMfmaQueries][4 * max_tiles]
+//    with counts cand_cnt; launch_select(.., cap = 4 * max_tiles, k, ..) then
+//    gives per query the top k of those maxima, whose k-th key lower-bounds
+//    the global k-th key;
 //  * main pass: every row, survivors of the per-query lower bound
 //    init_th[q * init_stride] appended to cand[nlists][kMfmaQueries][cap]
-//    with counts cand_cnt; sets *overflow = 1 when a buffer would overflow
-//    (the caller then redoes the batch exactly: lists pass or GEMV);
+//    (cap % 4 == 0: quarter j is lane j's, counts cand_cnt[nlists][256][4]);
+//    sets *overflow = 1 when a quarter would overflow (the caller then
+//    redoes the batch exactly: lists pass or GEMV);
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
 //    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; a no-op
 //    unless run_if is null or *run_if != 0.
@@ -76,10 +79,14 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st);
-// Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap]
-// (counts cand_cnt) for queries 0 .. nq-1 -> out[nq][k], sorted, 0-padded.
+// Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap] (4
+// quarters, counts cand_cnt[nwg][kMfmaQueries][4]) for queries 0 .. nq-1 ->
+// out[nq][k], sorted, 0-padded.
+// *clear (nullable) is zeroed by the launch (the main pass's overflow flag,
+// folded in to save a launch).
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st);
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
+                         uint32_t* clear = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows);

@@ -129,7 +129,8 @@ struct WaveList {
 template <bool BF16>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     const float* __restrict__ in, uint32_t n, uint32_t dim, int cosine,
-    void* __restrict__ dst, const uint64_t* __restrict__ dst_rows, uint64_t dst0) {
+    void* __restrict__ dst, const uint64_t* __restrict__ dst_rows, uint64_t dst0,
+    uint16_t* __restrict__ also_bf16) {
   const int lane = threadIdx.x & 63;
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
@@ -150,21 +151,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
       ((uint16_t*)dst)[row * dim + d] = vs::f32_to_bf16(y);
     else
       ((float*)dst)[row * dim + d] = y;
+    if (also_bf16) also_bf16[row * dim + d] = vs::f32_to_bf16(y);
   }
 }
 
 hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
                              bool cosine, bool bf16, void* dst,
                              const uint64_t* dst_rows, uint64_t dst0,
-                             hipStream_t st) {
+                             hipStream_t st, uint16_t* also_bf16) {
   if (n == 0) return hipSuccess;
   dim3 grid((n + 3) / 4), block(256);
   if (bf16)
     hipLaunchKernelGGL(preprocess_kernel<true>, grid, block, 0, st, in, n, dim,
-                       (int)cosine, dst, dst_rows, dst0);
+                       (int)cosine, dst, dst_rows, dst0, also_bf16);
   else
     hipLaunchKernelGGL(preprocess_kernel<false>, grid, block, 0, st, in, n, dim,
-                       (int)cosine, dst, dst_rows, dst0);
+                       (int)cosine, dst, dst_rows, dst0, also_bf16);
   return hipGetLastError();
 }
 
@@ -610,8 +612,9 @@ struct MfArgs {
   const uint16_t* Q;        // kMfmaQueries x D bf16 (zero-padded)
   const uint64_t* init_th;  // nullable: per-query lower-bound keys at [q * init_stride]
   uint64_t* lists;          // MODE 3 / 8: [nwg][kMfmaQueries][k] sorted keys
-  uint64_t* cand;           // MODE 0: [nwg][kMfmaQueries][cand_cap] unsorted keys
-  uint32_t* cand_cnt;       // MODE 0: [nwg][kMfmaQueries] keys in each buffer
+  uint64_t* cand;           // MODE 0 / 3: [nwg][kMfmaQueries][cand_cap] unsorted keys;
+                            // quarter kq of a query's buffer belongs to its lane kq
+  uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys in each quarter
   uint32_t* overflow;       // MODE 0: set to 1 when a buffer would overflow
   const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
-                    MODE == 8 ? kMfListBytes : (int)kMfmaQueries * 4, WAVES>;
+                    MODE == 8 ? kMfListBytes : 16, WAVES>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 8;
   constexpr bool kCand = MODE == 0 || MODE == 3;
@@ -780,7 +783,6 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
   lds_vu64_t* lists = (lds_vu64_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES);
-  uint32_t* counts = (uint32_t*)(smem + S::NSLOT * S::CHUNK_BYTES);  // MODE 0 / 3
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -796,16 +798,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
 
   if constexpr (kLists)
     for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += THREADS) lists[i] = 0;
-  if constexpr (kCand)
-    for (int i = threadIdx.x; i < (int)kMfmaQueries; i += THREADS) counts[i] = 0;
 
   // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
   bf16x8_t qf[G][S::T];
   uint32_t ql[G];
   bool qvalid[G];
-  float th_s[G];  // admit rows whose score reaches th_s
+  float th_s[G];     // admit rows whose score reaches th_s
+  uint32_t cnt[G];   // keys this lane appended to its quarter of the query's buffer
 #pragma unroll
   for (int g = 0; g < G; ++g) {
+    cnt[g] = 0;
     ql[g] = (uint32_t)(w * QPW + g * 16 + col);
     qvalid[g] = ql[g] < a.nq_valid;
     const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
@@ -1021,17 +1023,18 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
           return make_key(sc, a.row_base + row);
         };
         if constexpr (kCand) {
+          // lane-private quarter of the buffer: no atomics, fire-and-forget stores
           const uint32_t n = (uint32_t)__popc(m);
+          const uint32_t sub = a.cand_cap >> 2;
           if (n) {
-            const uint32_t pos = __hip_atomic_fetch_add(counts + ql[g], n, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (pos + n > a.cand_cap) {
+            if (cnt[g] + n > sub) {
               // main pass: the caller re-runs the batch exactly; sample pass:
               // dropping tile maxima only lowers the bound (still valid)
               if constexpr (MODE == 0) *a.overflow = 1u;
             } else {
-              uint64_t* dst =
-                  a.cand + ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * a.cand_cap + pos;
+              uint64_t* dst = a.cand + ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * a.cand_cap +
+                              (uint32_t)kq * sub + cnt[g];
+              cnt[g] += n;
               while (m) {
                 const int b = __builtin_ctz(m);
                 m &= m - 1;
@@ -1049,11 +1052,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if constexpr (kCand) {
-      if (kq == 0) {
-        const uint32_t n = __hip_atomic_load(counts + ql[g], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        a.cand_cnt[(size_t)blockIdx.x * kMfmaQueries + ql[g]] = n < a.cand_cap ? n : a.cand_cap;
-      }
+      a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] = cnt[g];
     } else if constexpr (kLists) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1120,7 +1119,7 @@ hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = max_tiles;
+  a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = 4 * max_tiles;
   a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
   a.k = k;
   return mfma_launch_mode<3>(dim, *nlists, a, st);
@@ -1145,7 +1144,8 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
                             const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
                             uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
                             uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap == 0 || cand_cap > kMfmaMaxCandCap)
+  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
+      cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
@@ -1170,8 +1170,13 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
 }
 
 uint32_t mfma_sample_tiles(uint32_t n_rows) {
+  // Survivors of the bound per (wave, tile) ~ 32 k / (st * nwg): independent
+  // of the collection size, so small shards sample at least min(8, tpw / 8)
+  // tiles (the main pass's epilogue then stays rare), large ones 1/64.
   const uint32_t tpw = mfma_tiles_per_wg(n_rows);
   uint32_t st = tpw / 64;
+  const uint32_t floor_st = tpw / 8 < 8 ? tpw / 8 : 8;
+  if (st < floor_st) st = floor_st;
   if (st < 1) st = 1;
   if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;
   return st;
@@ -1209,29 +1214,36 @@ __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, i
 
 __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
-    uint32_t cap, uint32_t k, uint64_t* __restrict__ out) {
+    uint32_t cap, uint32_t k, uint32_t* __restrict__ clear, uint64_t* __restrict__ out) {
+  if (clear && blockIdx.x == 0 && threadIdx.x == 0) *clear = 0u;  // a later launch's flag
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
-  __shared__ uint32_t pre[kMfmaMaxLists + 1];
+  __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint32_t fill;
   const uint32_t q = blockIdx.x;
+  const uint32_t sub = cap >> 2, nl = 4 * nwg;  // a buffer = 4 lane quarters
   for (uint32_t l = threadIdx.x; l < kMfmaMaxLists; l += kSelThreads) {
-    uint32_t c = l < nwg ? cnt[(size_t)l * kMfmaQueries + q] : 0;
-    c = c < cap ? c : cap;
     uint64_t m = 0;
-    const uint64_t* lst = cand + ((size_t)l * kMfmaQueries + q) * cap;
-    for (uint32_t j = 0; j < c; ++j) m = lst[j] > m ? lst[j] : m;
+    if (l < nwg) {
+      const uint64_t* lst = cand + ((size_t)l * kMfmaQueries + q) * cap;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint32_t c = cnt[((size_t)l * kMfmaQueries + q) * 4 + s];
+        c = c < sub ? c : sub;
+        for (uint32_t j = 0; j < c; ++j) m = lst[s * sub + j] > m ? lst[s * sub + j] : m;
+        pre[4 * l + s + 1] = c;
+      }
+    }
     lmax[l] = m;
-    if (l < nwg) pre[l + 1] = c;
   }
   __syncthreads();
   bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
   if (threadIdx.x == 0) {
     pre[0] = 0;
-    for (uint32_t l = 0; l < nwg; ++l) pre[l + 1] += pre[l];
+    for (uint32_t l = 0; l < nl; ++l) pre[l + 1] += pre[l];
   }
   __syncthreads();
-  const uint32_t total = pre[nwg];
+  const uint32_t total = pre[nl];
   const uint32_t chunk = kMfmaSelBuf - k;
   // admit keys > thr (0 marks an empty slot)
   uint64_t thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
@@ -1241,12 +1253,13 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     __syncthreads();
     const uint32_t end = base + chunk < total ? base + chunk : total;
     for (uint32_t i = base + threadIdx.x; i < end; i += kSelThreads) {
-      uint32_t lo = 0, hi = nwg;  // last l with pre[l] <= i
+      uint32_t lo = 0, hi = nl;  // last quarter list with pre[lo] <= i
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (pre[mid] <= i) lo = mid; else hi = mid;
       }
-      const uint64_t x = cand[((size_t)lo * kMfmaQueries + q) * cap + (i - pre[lo])];
+      const uint64_t x =
+          cand[((size_t)(lo >> 2) * kMfmaQueries + q) * cap + (lo & 3) * sub + (i - pre[lo])];
       if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
     }
     __syncthreads();
@@ -1266,12 +1279,13 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
 }
 
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st) {
-  if (nwg == 0 || nwg > kMfmaMaxLists || cap == 0 || k == 0 || k > kMfmaMaxK || nq == 0 ||
-      nq > kMfmaQueries)
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
+                         uint32_t* clear) {
+  if (nwg == 0 || nwg > kMfmaMaxLists || cap < 4 || cap % 4 || k == 0 || k > kMfmaMaxK ||
+      nq == 0 || nq > kMfmaQueries)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_cand_kernel, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt, nwg,
-                     cap, k, out);
+                     cap, k, clear, out);
   return hipGetLastError();
 }
 

@@ -39,6 +39,7 @@ class ShardedSearch:
     local_search: Callable
     merge: Callable
     group: Optional[object] = None
+    _gather_bufs: Optional[dict] = None  # all-gather outputs, reused per shape
 
     def search(self, queries, k: int):
         import torch
@@ -50,25 +51,47 @@ class ShardedSearch:
         P = dist.get_world_size(self.group)
         local = local.contiguous()
         # concatenated along dim 0 (the form every backend accepts), viewed as [P, nq, k]
-        flat = torch.empty((P * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                           device=local.device)
+        shape = (P * local.shape[0],) + tuple(local.shape[1:])
+        if self._gather_bufs is None:
+            self._gather_bufs = {}
+        key = (shape, local.dtype, str(local.device))
+        flat = self._gather_bufs.get(key)
+        if flat is None:
+            flat = self._gather_bufs[key] = torch.empty(shape, dtype=local.dtype,
+                                                        device=local.device)
         dist.all_gather_into_tensor(flat, local, group=self.group)
         return self.merge(flat.view((P,) + tuple(local.shape)), k)
 
 
-def engine_callables(engine, collection: str, dim: int, stream_fn: Callable[[], int]):
-    """Binds ShardedSearch to the HIP engine (device tensors, caller's stream)."""
+def engine_callables(engine, collection: str, dim: int, stream_fn: Callable[[], int],
+                     reuse: bool = False):
+    """Binds ShardedSearch to the HIP engine (device tensors, caller's stream).
+
+    With ``reuse`` the result tensors are cached per shape and overwritten by
+    the next call (a serving loop that consumes each result before issuing
+    the next search); otherwise every call returns fresh tensors."""
     import torch
+
+    cache = {}
+
+    def buf(tag, shape, device):
+        if not reuse:
+            return torch.empty(shape, dtype=torch.int64, device=device)
+        key = (tag, shape, str(device))
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.empty(shape, dtype=torch.int64, device=device)
+        return t
 
     def local_search(queries, k):
         nq = queries.shape[0]
-        out = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+        out = buf("local", (nq, k), queries.device)
         engine.search_keys(collection, queries.data_ptr(), nq, dim, k, out.data_ptr(), stream_fn())
         return out
 
     def merge(gathered, k):
         P, nq, kin = gathered.shape
-        out = torch.empty((nq, k), dtype=torch.int64, device=gathered.device)
+        out = buf("merged", (nq, k), gathered.device)
         engine.merge_keys(gathered.data_ptr(), P, nq, kin, k, out.data_ptr(), stream_fn())
         return out
 

@@ -77,8 +77,12 @@ typedef struct vs_config {
   uint32_t flags; /* VS_FLAG_* */
 } vs_config;
 
-/* Record HIP events around every scan/merge launch (read with vs_timing). */
+/* Record HIP events around every scan launch (read with vs_timing). */
 #define VS_FLAG_TIMING 1u
+/* ... and around every merge / select launch too. Each event record costs a
+ * few microseconds of device idle between launches, so the benchmark times
+ * scans only. */
+#define VS_FLAG_TIMING_MERGE 2u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 
@@ -197,8 +201,9 @@ int vs_health(vs_engine* eng, char* buf, size_t len);
 /* Thread-local message of the last failure ("" if none). */
 const char* vs_last_error(void);
 
-/* With VS_FLAG_TIMING: average device duration (ms) of scan and merge kernel
- * launches recorded since the last reset, and their counts. Blocks until the
+/* With VS_FLAG_TIMING (and VS_FLAG_TIMING_MERGE): average device duration
+ * (ms) of scan (and merge) kernel launches recorded since the last reset, and
+ * their counts. Blocks until the
  * recorded work is done. reset != 0 clears the accumulators afterwards. */
 int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count,
               double* merge_ms_avg, uint64_t* merge_count, int reset);

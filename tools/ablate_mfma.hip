@@ -67,9 +67,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&out, (size_t)c.nwg * 256 * k * 8));
   const uint32_t st = mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
   CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 8));
-  CK(hipMalloc(&scand, (size_t)c.nwg * 256 * st * 8));
-  CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4));
-  CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4));
+  CK(hipMalloc(&scand, (size_t)c.nwg * 256 * 4 * st * 8));
+  CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4 * 4));
+  CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
   CK(hipMalloc(&ovf, 4));
   CK(hipMemset(ovf, 0, 4));
   CK(hipMalloc(&skeys, (size_t)256 * k * 8));
@@ -83,7 +83,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     hipEventRecord(a, 0);
     CK(launch_mfma_sample(X, 768, n, 0, Q, 256, k, st, scand, scnt, c.nwg, &L, 0));
-    CK(launch_select(scand, scnt, L, st, 256, k, skeys, 0));
+    CK(launch_select(scand, scnt, L, 4 * st, 256, k, skeys, 0));
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms = 0;
@@ -98,15 +98,13 @@ int main(int argc, char** argv) {
   c.a = a;
   c.b = b;
   std::vector<Arm> arms = {
-      {"main cand G2", run<0, 0, 2>, true, {}},
-      {"main cand G2 nt", run<0, 1024, 2>, true, {}},
-      {"no-epi G2", run<1, 0, 2>, false, {}},
-      {"no-epi G2 nt", run<1, 1024, 2>, false, {}},
+      {"main cand", run<0, 0, 2>, true, {}},
+      {"no-epilogue", run<1, 0, 2>, false, {}},
       {"dma-only", run<2, 0, 2>, false, {}},
       {"dma-only nt", run<2, 1024, 2>, false, {}},
-      {"dma-only big", run<2, 256, 2>, false, {}},
-      {"dma-only big nt", run<2, 256 + 1024, 2>, false, {}},
+      {"mfma+bar", run<4, 0, 2>, false, {}},
   };
+
 
 
 
@@ -133,7 +131,7 @@ int main(int argc, char** argv) {
   }
   uint32_t of = 0;
   CK(hipMemcpy(&of, ovf, 4, hipMemcpyDeviceToHost));
-  std::vector<uint32_t> hc((size_t)c.nwg * 256);
+  std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
   uint64_t tot = 0, mx = 0;
   for (uint32_t v : hc) tot += v, mx = v > mx ? v : mx;
