@@ -236,7 +236,8 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t dim = c.dim;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
-  const uint32_t P = vsk::kMfmaQueries;
+  const uint32_t P = vsk::mfma_queries(dim);  // queries per pass
+  const uint32_t PS = vsk::kMfmaQueries;      // query stride of the pass buffers
   const uint32_t npass = (nq + P - 1) / P;
   const uint32_t maxl = vsk::mfma_max_lists(n_rows);
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
@@ -246,11 +247,11 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
-  const size_t lbytes = (size_t)maxl * P * std::min(k, vsk::kMfmaListMaxK) * 8;
-  const size_t sbytes = (size_t)P * k * 8;
-  const size_t cbytes = (size_t)maxl * P * cap * 8;
-  const size_t scbytes = (size_t)maxl * P * 4 * st * 8;
-  const size_t nbytes = (size_t)maxl * P * 4 * 4;
+  const size_t lbytes = (size_t)maxl * PS * std::min(k, vsk::kMfmaListMaxK) * 8;
+  const size_t sbytes = (size_t)PS * k * 8;
+  const size_t cbytes = (size_t)maxl * PS * cap * 8;
+  const size_t scbytes = (size_t)maxl * PS * 4 * st * 8;
+  const size_t nbytes = (size_t)maxl * PS * 4 * 4;
   if (eng->lists.bytes < lbytes || eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
       eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes ||
       eng->scand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
@@ -286,7 +287,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
              "mfma scan (lists)");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream),
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)PS * k, k, nv, k, k, out, eng->stream),
              "merge");
       VS_HIP(ev_end(eng, eng->merge_ev), "event");
       continue;
@@ -318,7 +319,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
                                     maxl, &L, eng->stream),
              "mfma scan (fallback)");
-      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)P * k, k, nv, k, k, out, eng->stream, ovf,
+      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)PS * k, k, nv, k, k, out, eng->stream, ovf,
                                eng->fallbacks.as<uint32_t>()),
              "merge (fallback)");
     } else {

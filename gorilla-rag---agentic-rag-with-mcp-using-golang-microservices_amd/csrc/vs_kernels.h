@@ -6,7 +6,8 @@
 
 namespace vsk {
 
-// Queries handled by one launch of the MFMA scan (8 waves x 32 queries).
+// Query slots of the MFMA scan's buffers (most queries one launch handles:
+// 8 waves x 32 at dim <= 768, 8 x 16 at dim 1024 / 1536; mfma_queries()).
 constexpr uint32_t kMfmaQueries = 256;
 // Largest k of the batched MFMA scan (candidate path); larger k uses the
 // GEMV scan per query. The sorted-list pass (overflow fallback) keeps
@@ -65,6 +66,7 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; a no-op
 //    unless run_if is null or *run_if != 0.
 bool mfma_supported(uint32_t dim);
+uint32_t mfma_queries(uint32_t dim);  // queries per launch at this dim
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,

@@ -595,10 +595,13 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // lists). Those are k distinct rows with scores >= the merged k-th key, so it
 // lower-bounds the global k-th key: rows under it can never enter the result.
 // Query groups (16 queries each) per wave: G = 2 -> 8 waves of 32 queries
-// (two per SIMD); G = 4 -> 4 waves of 64 queries (one per SIMD, 512-register
-// budget), which halves the LDS reads per MFMA (each A fragment feeds 4).
+// (two per SIMD, 256 queries per launch; D <= 768); G = 1 -> 8 waves of 16
+// queries (128 per launch: the B fragments of D = 1024 / 1536 then fit the
+// 256-register budget); G = 4 (ablation) -> 4 waves of 64 queries (one per
+// SIMD, 512-register budget), which halves the LDS reads per MFMA.
 constexpr int kMfG = 2;
-constexpr int mf_waves(int g) { return 16 / g; }
+constexpr int mf_waves(int g) { return g == 4 ? 4 : 8; }
+constexpr int mf_groups(int d) { return d <= 768 ? 2 : 1; }
 constexpr int kMfListLen = (int)kMfmaListMaxK;                  // entries per query list
 constexpr int kMfListBytes = (int)kMfmaQueries * kMfListLen * 8;  // 32 KiB
 constexpr int kMfRingBytes = 112 * 1024;
@@ -762,11 +765,12 @@ struct MfShape {
 // VAR 128: each step's reads and MFMAs pinned in program order; VAR 512:
 // the chunk's LDS-DMA pieces spread over its steps instead of at its head;
 // VAR 1024: non-temporal (nt) LDS-DMA loads of the corpus stream.
-template <int D, int MODE = 0, int VAR = 0, int G = kMfG>
+template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D)>
 __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
   constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
-  static_assert(WAVES * QPW == (int)kMfmaQueries, "one launch covers kMfmaQueries");
+  static_assert(WAVES * QPW <= (int)kMfmaQueries, "one launch covers <= kMfmaQueries");
+  static_assert(G * (D / 32) * 4 <= 192, "B fragments must fit the register budget");
   // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
@@ -1065,7 +1069,15 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   }
 }
 
-bool mfma_supported(uint32_t dim) { return dim == 768 || dim == 512 || dim == 384 || dim == 256; }
+bool mfma_supported(uint32_t dim) {
+  return dim == 768 || dim == 512 || dim == 384 || dim == 256 || dim == 128 || dim == 1024 ||
+         dim == 1536;
+}
+
+uint32_t mfma_queries(uint32_t dim) {
+  const int g = dim <= 768 ? 2 : 1;
+  return (uint32_t)(mf_waves(g) * 16 * g);
+}
 
 void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg) {
   const int cus = g_cu_count ? g_cu_count : device_cu_count();
@@ -1092,14 +1104,22 @@ uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
   return (rpw + 31) / 32;
 }
 
+template <int MODE, int D>
+static void mfma_launch_d(uint32_t nwg, const MfArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((mfma_topk_kernel<D, MODE>), dim3(nwg), dim3(64 * mf_waves(mf_groups(D))),
+                     0, st, a);
+}
+
 template <int MODE>
 static hipError_t mfma_launch_mode(uint32_t dim, uint32_t nwg, const MfArgs& a, hipStream_t st) {
-  dim3 grid(nwg), block(64 * mf_waves(kMfG));
   switch (dim) {
-    case 768: hipLaunchKernelGGL((mfma_topk_kernel<768, MODE>), grid, block, 0, st, a); break;
-    case 512: hipLaunchKernelGGL((mfma_topk_kernel<512, MODE>), grid, block, 0, st, a); break;
-    case 384: hipLaunchKernelGGL((mfma_topk_kernel<384, MODE>), grid, block, 0, st, a); break;
-    case 256: hipLaunchKernelGGL((mfma_topk_kernel<256, MODE>), grid, block, 0, st, a); break;
+    case 768: mfma_launch_d<MODE, 768>(nwg, a, st); break;
+    case 512: mfma_launch_d<MODE, 512>(nwg, a, st); break;
+    case 384: mfma_launch_d<MODE, 384>(nwg, a, st); break;
+    case 256: mfma_launch_d<MODE, 256>(nwg, a, st); break;
+    case 128: mfma_launch_d<MODE, 128>(nwg, a, st); break;
+    case 1024: mfma_launch_d<MODE, 1024>(nwg, a, st); break;
+    case 1536: mfma_launch_d<MODE, 1536>(nwg, a, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1107,7 +1127,7 @@ static hipError_t mfma_launch_mode(uint32_t dim, uint32_t nwg, const MfArgs& a, 
 
 static bool mfma_args_ok(uint32_t dim, uint32_t n_rows, uint32_t nq_valid, uint32_t k) {
   return mfma_supported(dim) && k >= 1 && k <= kMfmaMaxK && n_rows > 0 && nq_valid >= 1 &&
-         nq_valid <= kMfmaQueries;
+         nq_valid <= mfma_queries(dim);
 }
 
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
@@ -1170,13 +1190,11 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
 }
 
 uint32_t mfma_sample_tiles(uint32_t n_rows) {
-  // Survivors of the bound per (wave, tile) ~ 32 k / (st * nwg): independent
-  // of the collection size, so small shards sample at least min(8, tpw / 8)
-  // tiles (the main pass's epilogue then stays rare), large ones 1/64.
+  // 1/64 of every workgroup's tiles. (A floor of 8 tiles for small shards cut
+  // the survivors 4x at 1.25M rows but cost more in the sample pass than it
+  // saved in the main pass's epilogue: measured, r01.)
   const uint32_t tpw = mfma_tiles_per_wg(n_rows);
   uint32_t st = tpw / 64;
-  const uint32_t floor_st = tpw / 8 < 8 ? tpw / 8 : 8;
-  if (st < floor_st) st = floor_st;
   if (st < 1) st = 1;
   if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;
   return st;

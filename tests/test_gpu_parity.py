@@ -129,6 +129,21 @@ def test_mfma_candidate_path(engine, orc, corpus_fast, nq, k):
     assert json.loads(engine.health())["mfma_fallbacks"] == before
 
 
+@pytest.mark.parametrize("dim,nq,k", [(1024, 200, 10), (1536, 129, 50), (128, 256, 10),
+                                      (512, 300, 5)])
+def test_mfma_candidate_path_dims(engine, orc, dim, nq, k):
+    """Candidate path at other dims: 1024 / 1536 run 128 queries per launch."""
+    n = 100_000
+    name = f"fast{dim}"
+    engine.create_collection(name, dim, 0, 1, n)
+    engine.generate(name, n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 3000, nq, dim)
+    s, r, c = engine.search(name, Q, k)
+    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    engine.drop_collection(name)
+
+
 def test_mfma_overflow_fallback(engine, orc):
     """Adversarial ties: 70k rows, the first 40k identical. Every identical row
     reaches the sample bound of the queries that match it, the candidate
@@ -177,7 +192,7 @@ def test_golden_fixture_on_device(engine, orc):
         engine.drop_collection(name)
 
 
-@pytest.mark.parametrize("dim", [100, 384, 1024, 1536, 256])
+@pytest.mark.parametrize("dim", [100, 384, 1024, 1536, 256, 128, 512])
 @pytest.mark.parametrize("dtype", [0, 1])
 def test_other_dims(engine, orc, dim, dtype):
     n = 3001
