@@ -630,12 +630,13 @@ __device__ __forceinline__ int mf_swz(int ri, int rg) {
   return ((ri >> 1) & 3) | ((rg & 1) << 2);
 }
 
-// v_max3_f32 without the canonicalising v_max hipcc adds around fmaxf on
-// MFMA results (scores are finite).
+// max of three scores; hipcc forms one v_max3_f32 (checked in the .s). It
+// must stay compiler-visible, not inline asm: the hazard recognizer then
+// inserts the wait states an MFMA result needs before a VALU read (s_nop 5-7
+// on gfx950) -- an asm v_max3 read stale accumulators once the schedule
+// placed it right after the tile's last MFMA (r01).
 __device__ __forceinline__ float fmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
 }
 
 template <int N>
@@ -736,6 +737,11 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
     }
   }
 }
+
+template <bool B>
+struct MfFull {
+  static constexpr bool value = B;
+};
 
 template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8>
 struct MfShape {
@@ -904,7 +910,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   constexpr int NB = kPD + 1;
   static_assert(STEPS % NB == 0, "A-fragment ring must divide the steps per tile");
   uint32_t scur = 0;  // ring slot byte offset of chunk c
-  for (uint32_t t = 0; t < ntiles; ++t) {
+  // Candidate passes instantiate a tile's body twice: full 32-row tiles get a
+  // straight-line epilogue; the (at most one) partial last tile masks rows.
+  // The sorted-list pass keeps one body with a runtime test (its register
+  // allocation with the peeled form spilled; r01).
+  constexpr bool kPeel = MODE != 8;
+  auto tile = [&](uint32_t t, auto full_tag) {
     f32x4_t acc[2][G];  // [row half][query group]
 #pragma unroll
     for (int hr = 0; hr < 2; ++hr)
@@ -977,11 +988,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
       for (int hr = 0; hr < 2; ++hr)
 #pragma unroll
         for (int g = 0; g < G; ++g) asm volatile("" ::"v"(acc[hr][g][hr * 2 + (g & 1)]));
-      continue;
+      return;
     }
     // epilogue: acc[hr][g][i] = score(row trow0 + 16hr + 4kq + i, query ql[g])
     const uint32_t trow0 = wr0 + t * 32;
-    const bool full = trow0 + 32 <= wr1;
+    const bool full = kPeel ? decltype(full_tag)::value : trow0 + 32 <= wr1;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float mx = -INFINITY;
@@ -1051,6 +1062,14 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
         }
       }
     }
+  };
+  uint32_t nfull = (wr1 - wr0) / 32;
+  if (nfull > ntiles) nfull = ntiles;
+  if constexpr (kPeel) {
+    for (uint32_t t = 0; t < nfull; ++t) tile(t, MfFull<true>{});
+    for (uint32_t t = nfull; t < ntiles; ++t) tile(t, MfFull<false>{});
+  } else {
+    for (uint32_t t = 0; t < ntiles; ++t) tile(t, MfFull<false>{});
   }
   // each wave owns its queries' lists / counters: no barrier before the write-out
 #pragma unroll
