@@ -174,7 +174,7 @@ def main():
     if args.rows:
         n_full = args.rows
     lo, hi = shard.shard_range(n_full, world, rank)
-    eng = pkg.VectorEngine(device=local, timing=True)
+    eng = pkg.VectorEngine(device=local, timing=True, timing_sample=True)
     coll = "bench"
     eng.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else pkg.METRIC_COSINE,
                           pkg.DTYPE_BF16 if dtype == "bf16" else pkg.DTYPE_F32, hi - lo, lo)

@@ -107,6 +107,8 @@ struct vs_engine {
   std::vector<hipEvent_t> ev_pool;  // recycled timing events (none created on the hot path)
   double scan_ms = 0, merge_ms = 0;
   uint64_t scan_n = 0, merge_n = 0;
+  uint64_t scan_tick = 0;   // scan launches seen (VS_FLAG_TIMING_SAMPLE)
+  bool scan_skip = false;   // the current scan launch is not bracketed
 };
 
 namespace {
@@ -139,6 +141,10 @@ bool timing_wanted(vs_engine* eng, const std::vector<EventPair>& v) {
 
 hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
   if (!timing_wanted(eng, v)) return hipSuccess;
+  if (&v == &eng->scan_ev && (eng->flags & VS_FLAG_TIMING_SAMPLE)) {
+    eng->scan_skip = (eng->scan_tick++ & 3) != 0;  // bracket every 4th scan only
+    if (eng->scan_skip) return hipSuccess;
+  }
   EventPair p{};
   for (hipEvent_t* ev : {&p.a, &p.b}) {
     if (!eng->ev_pool.empty()) {
@@ -154,6 +160,8 @@ hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
 }
 hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
   if (!timing_wanted(eng, v) || v.empty()) return hipSuccess;
+  if (&v == &eng->scan_ev && (eng->flags & VS_FLAG_TIMING_SAMPLE) && eng->scan_skip)
+    return hipSuccess;
   return hipEventRecord(v.back().b, eng->stream);
 }
 
@@ -811,6 +819,7 @@ int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double*
   if (reset) {
     eng->scan_ms = eng->merge_ms = 0;
     eng->scan_n = eng->merge_n = 0;
+    eng->scan_tick = 0;  // the next scan is bracketed (VS_FLAG_TIMING_SAMPLE)
   }
   return VS_OK;
 }

@@ -743,10 +743,11 @@ struct MfFull {
   static constexpr bool value = B;
 };
 
-template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8>
+template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8, int CSX = 0>
 struct MfShape {
   static constexpr int T = D / 32;                        // 32-k MFMA steps per row
-  static constexpr int CS4 = (D % 256 == 0) ? 4 : 2;      // 128-B pieces per row per chunk
+  // 128-B pieces per row per chunk (CSX overrides: ablation of chunk sizes)
+  static constexpr int CS4 = CSX ? CSX : ((D % 256 == 0) ? 4 : 2);
   static constexpr int CT = CS4 * 2;                      // 32-k steps per chunk
   static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
   static constexpr int PIECES = CS4 * 4;                  // 1 KiB LDS-DMA pieces per chunk
@@ -756,6 +757,8 @@ struct MfShape {
   static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
   static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + TAIL;  // ring + lists / counters
   static_assert(D % 256 == 0 || D % 128 == 0, "MFMA scan needs D % 128 == 0");
+  static_assert(D % (64 * CS4) == 0, "whole chunks per tile");
+  static_assert(AHEAD >= 2, "at least two chunks in the ring ahead");
   static_assert(PPW >= 1 && PPW * WAVES == PIECES, "pieces split evenly over waves");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
@@ -779,8 +782,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
   static_assert(G * (D / 32) * 4 <= 192, "B fragments must fit the register budget");
   // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
+  // VAR 2048 / 4096: 24 / 48 KiB K-chunks (384 / 768 k of 32 rows) at D = 768
+  constexpr int kCsx = (VAR & 4096) ? 12 : ((VAR & 2048) ? 6 : 0);
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
-                    MODE == 8 ? kMfListBytes : 16, WAVES>;
+                    MODE == 8 ? kMfListBytes : 16, WAVES, kCsx>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 8;
   constexpr bool kCand = MODE == 0 || MODE == 3;
@@ -1222,13 +1227,16 @@ uint32_t mfma_sample_tiles(uint32_t n_rows) {
 // ---------------------------------------------------------------------------
 // select: top-k of per-workgroup candidate buffers
 // ---------------------------------------------------------------------------
-// One workgroup per query. First bound: the k-th largest of the per-buffer
+// One workgroup per query; thread t owns lane quarters t and t + 512 of the
+// 4 * nwg quarter lists. First bound: the k-th largest of the per-buffer
 // maxima (k keys of k distinct rows) -- no key below it can be in the top k,
-// which leaves a few dozen of the usual hundreds of candidates. The valid
-// candidates of all workgroups (prefix sum of the counts) are then streamed
-// through an LDS buffer that also holds the running top-k: keys reaching the
-// bound are appended, and the buffer is sorted (bitonic, descending)
-// whenever a chunk added something. Any total is handled.
+// which leaves a few dozen of the usual hundreds of candidates. Fast path:
+// every thread re-reads its own quarters and appends the keys above the bound
+// to an LDS buffer, which is sorted once. Only if more than kMfmaSelBuf keys
+// pass (adversarial ties) does the workgroup fall back to streaming all
+// candidates in chunks through the buffer (prefix sum of the counts; the
+// running top-k is re-sorted whenever a chunk added something). Any total is
+// handled.
 constexpr int kSelThreads = 512;
 
 __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, int nthreads) {
@@ -1249,6 +1257,31 @@ __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, i
   }
 }
 
+// max (or filtered append) over one quarter list, 4 loads in flight
+template <bool APPEND>
+__device__ __forceinline__ uint64_t sel_scan_quarter(const uint64_t* __restrict__ p, uint32_t c,
+                                                     uint64_t thr, uint64_t* buf,
+                                                     uint32_t* fill, uint32_t* spill) {
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < c; j += 4) {
+    uint64_t x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = j + u < c ? p[j + u] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (APPEND) {
+        if (x[u] > thr) {
+          const uint32_t pos = atomicAdd(fill, 1u);
+          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = x[u]; else *spill = 1u;
+        }
+      } else {
+        m = x[u] > m ? x[u] : m;
+      }
+    }
+  }
+  return m;
+}
+
 __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
     uint32_t cap, uint32_t k, uint32_t* __restrict__ clear, uint64_t* __restrict__ out) {
@@ -1256,61 +1289,87 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
-  __shared__ uint32_t fill;
+  __shared__ uint32_t fill, spill;
+  static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two quarters per thread");
   const uint32_t q = blockIdx.x;
   const uint32_t sub = cap >> 2, nl = 4 * nwg;  // a buffer = 4 lane quarters
-  for (uint32_t l = threadIdx.x; l < kMfmaMaxLists; l += kSelThreads) {
-    uint64_t m = 0;
-    if (l < nwg) {
-      const uint64_t* lst = cand + ((size_t)l * kMfmaQueries + q) * cap;
+  auto qptr = [&](uint32_t l) {
+    return cand + ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub;
+  };
+  uint32_t qc[2];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        uint32_t c = cnt[((size_t)l * kMfmaQueries + q) * 4 + s];
-        c = c < sub ? c : sub;
-        for (uint32_t j = 0; j < c; ++j) m = lst[s * sub + j] > m ? lst[s * sub + j] : m;
-        pre[4 * l + s + 1] = c;
-      }
-    }
-    lmax[l] = m;
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t l = threadIdx.x + r * kSelThreads;
+    uint32_t c = 0;
+    if (l < nl) c = cnt[((size_t)(l >> 2) * kMfmaQueries + q) * 4 + (l & 3)];
+    qc[r] = c < sub ? c : sub;
   }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t l = threadIdx.x + r * kSelThreads;
+    uint64_t m = sel_scan_quarter<false>(qptr(l), qc[r], 0, nullptr, nullptr, nullptr);
+#pragma unroll
+    for (int s = 1; s <= 2; s <<= 1) {  // the 4 quarters of a buffer are 4 adjacent lanes
+      const uint64_t o = __shfl_xor(m, s, 64);
+      m = o > m ? o : m;
+    }
+    if ((l & 3) == 0) lmax[l >> 2] = m;
+  }
+  if (threadIdx.x == 0) fill = 0, spill = 0;
   __syncthreads();
   bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
-  if (threadIdx.x == 0) {
-    pre[0] = 0;
-    for (uint32_t l = 0; l < nl; ++l) pre[l + 1] += pre[l];
-  }
-  __syncthreads();
-  const uint32_t total = pre[nl];
-  const uint32_t chunk = kMfmaSelBuf - k;
   // admit keys > thr (0 marks an empty slot)
   uint64_t thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+    sel_scan_quarter<true>(qptr(threadIdx.x + r * kSelThreads), qc[r], thr, buf, &fill, &spill);
+  __syncthreads();
   uint32_t nR = 0;  // running top-k in buf[0, nR)
-  for (uint32_t base = 0; base < total; base += chunk) {
-    if (threadIdx.x == 0) fill = nR;
-    __syncthreads();
-    const uint32_t end = base + chunk < total ? base + chunk : total;
-    for (uint32_t i = base + threadIdx.x; i < end; i += kSelThreads) {
-      uint32_t lo = 0, hi = nl;  // last quarter list with pre[lo] <= i
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= i) lo = mid; else hi = mid;
-      }
-      const uint64_t x =
-          cand[((size_t)(lo >> 2) * kMfmaQueries + q) * cap + (lo & 3) * sub + (i - pre[lo])];
-      if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
-    }
-    __syncthreads();
+  if (!spill) {
     const uint32_t c = fill;
-    if (c > nR) {
+    if (c) {
       int p2 = 1;
       while ((uint32_t)p2 < c) p2 <<= 1;
       for (uint32_t i = c + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
       __syncthreads();
       bitonic_sort_desc_n(buf, p2, kSelThreads);
       nR = c < k ? c : k;
-      if (nR == k && buf[k - 1] > thr) thr = buf[k - 1];
+    }
+  } else {
+    for (uint32_t l = threadIdx.x; l < nl; l += kSelThreads) pre[l + 1] = qc[l / kSelThreads];
+    if (threadIdx.x == 0) {
+      pre[0] = 0;
+      for (uint32_t l = 0; l < nl; ++l) pre[l + 1] += pre[l];
     }
     __syncthreads();
+    const uint32_t total = pre[nl];
+    const uint32_t chunk = kMfmaSelBuf - k;
+    for (uint32_t base = 0; base < total; base += chunk) {
+      if (threadIdx.x == 0) fill = nR;
+      __syncthreads();
+      const uint32_t end = base + chunk < total ? base + chunk : total;
+      for (uint32_t i = base + threadIdx.x; i < end; i += kSelThreads) {
+        uint32_t lo = 0, hi = nl;  // last quarter list with pre[lo] <= i
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= i) lo = mid; else hi = mid;
+        }
+        const uint64_t x = qptr(lo)[i - pre[lo]];
+        if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
+      }
+      __syncthreads();
+      const uint32_t c = fill;
+      if (c > nR) {
+        int p2 = 1;
+        while ((uint32_t)p2 < c) p2 <<= 1;
+        for (uint32_t i = c + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+        __syncthreads();
+        bitonic_sort_desc_n(buf, p2, kSelThreads);
+        nR = c < k ? c : k;
+        if (nR == k && buf[k - 1] > thr) thr = buf[k - 1];
+      }
+      __syncthreads();
+    }
   }
   for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
 }

@@ -34,6 +34,7 @@ DTYPE_F32 = 0
 DTYPE_BF16 = 1
 FLAG_TIMING = 1
 FLAG_TIMING_MERGE = 2
+FLAG_TIMING_SAMPLE = 4
 
 # Every function include/vsearch.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -127,10 +128,12 @@ def keys_decode(keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
 class VectorEngine:
     """One engine = one HIP device (vs_open). Mirrors the C-ABI 1:1."""
 
-    def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False):
+    def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False,
+                 timing_sample: bool = False):
         L = load_library()
         cfg = _Config(device, (FLAG_TIMING if timing else 0) |
-                      (FLAG_TIMING_MERGE if timing and timing_merge else 0))
+                      (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
+                      (FLAG_TIMING_SAMPLE if timing and timing_sample else 0))
         h = ctypes.c_void_p()
         _check(L.vs_open(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -83,6 +83,10 @@ typedef struct vs_config {
  * few microseconds of device idle between launches, so the benchmark times
  * scans only. */
 #define VS_FLAG_TIMING_MERGE 2u
+/* With VS_FLAG_TIMING: bracket only every 4th scan launch, starting with the
+ * first after a vs_timing reset (a sampled
+ * average that keeps the event gaps out of 3 of 4 steps). */
+#define VS_FLAG_TIMING_SAMPLE 4u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 

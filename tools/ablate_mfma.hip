@@ -51,6 +51,7 @@ struct Arm {
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)atol(argv[1]) : 10000000u;
   const int reps = argc > 2 ? atoi(argv[2]) : 8;
+  const uint32_t st_over = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;  // sample tiles override
   const uint32_t k = 10;
   uint16_t *X, *Q;
   uint64_t *out, *skeys, *cand, *scand;
@@ -65,7 +66,7 @@ int main(int argc, char** argv) {
   uint32_t rpw;
   mfma_grid(n, &c.nwg, &rpw);
   CK(hipMalloc(&out, (size_t)c.nwg * 256 * k * 8));
-  const uint32_t st = mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
+  const uint32_t st = st_over ? st_over : mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
   CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 8));
   CK(hipMalloc(&scand, (size_t)c.nwg * 256 * 4 * st * 8));
   CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4 * 4));
@@ -97,26 +98,17 @@ int main(int argc, char** argv) {
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
+  // An unrolled, predicated candidate append was no faster than the ctz loop;
+  // 4-16 sample tiles at 1.25M rows cut the candidates 2-8x but the main pass
+  // gained what the sample pass lost (argv[3] overrides the sample tiles).
+  // 24 / 48 KiB K-chunks (VAR 2048 / 4096, + 256 for the 144 KiB ring) were
+  // slower than 16 KiB at 10M rows (3.64-3.67 vs 3.48 ms); kept as arms.
   std::vector<Arm> arms = {
       {"main cand", run<0, 0, 2>, true, {}},
-      {"no-epilogue", run<1, 0, 2>, false, {}},
+      {"main 24K big", run<0, 2048 + 256, 2>, true, {}},
       {"dma-only", run<2, 0, 2>, false, {}},
-      {"dma-only nt", run<2, 1024, 2>, false, {}},
-      {"mfma+bar", run<4, 0, 2>, false, {}},
+      {"no-epilogue", run<1, 0, 2>, false, {}},
   };
-
-
-
-
-
-
-
-
-
-
-
-
-
   for (int r = 0; r < reps; ++r)
     for (auto& arm : arms) arm.t.push_back(arm.fn(c, arm.bound));
   CK(hipDeviceSynchronize());
