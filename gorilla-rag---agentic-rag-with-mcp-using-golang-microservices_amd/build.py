@@ -13,7 +13,8 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "lib", "libvsearch.so")
 SVC_LIB = os.path.join(HERE, "lib", "libvsearch_service.so")
-SVC_SOURCES = ["service/json.cpp", "service/vector_service.cpp"]
+SVC_SOURCES = ["service/json.cpp", "service/vector_service.cpp", "service/batcher.cpp",
+               "service/loadgen.cpp"]
 ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
@@ -53,12 +54,12 @@ def build(verbose: bool = False, force: bool = False) -> str:
         subprocess.run(cmd, check=True)
     # host-only service layer (the rag/vector-service handler mirror) over the C-ABI
     svc_srcs = [os.path.join(CSRC, x) for x in SVC_SOURCES]
-    svc_hdrs = [os.path.join(CSRC, "service", "json.h"),
+    svc_hdrs = [os.path.join(CSRC, "service", "json.h"), os.path.join(CSRC, "service", "batcher.h"),
                 os.path.join(ROOT, "include", "vsearch_service.h")]
     if force or _mtime(SVC_LIB) < max(_mtime(x) for x in svc_srcs + svc_hdrs + [LIB]):
         cmd = [os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-fPIC", "-Wall", "-shared",
                "-o", SVC_LIB, *svc_srcs, "-L" + os.path.dirname(LIB), "-lvsearch",
-               "-Wl,-rpath,$ORIGIN", "-Wl,-soname,libvsearch_service.so"]
+               "-pthread", "-Wl,-rpath,$ORIGIN", "-Wl,-soname,libvsearch_service.so"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -1,0 +1,135 @@
+// batcher.cpp — see batcher.h.
+#include "batcher.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <tuple>
+
+namespace vsbatch {
+
+namespace {
+// The engine's batched MFMA path serves k <= 128 (vs_kernels.h kMfmaMaxK);
+// larger k run the per-query GEMV path whatever the batch.
+constexpr uint32_t kMfmaMaxK = 128;
+}  // namespace
+
+struct Batcher::Req {
+  const std::string* coll;
+  const float* q;
+  uint32_t dim, k;
+  float* scores;
+  uint64_t* rows;
+  uint32_t* count;
+  int rc = VS_OK;
+  std::string err;
+  bool done = false;
+  std::condition_variable* cv = nullptr;  // the waiter's
+};
+
+Batcher::Batcher(vs_engine* eng, Options opt) : eng_(eng), opt_(opt) {
+  if (opt_.max_batch == 0) opt_.max_batch = 1;
+  worker_ = std::thread([this] { run(); });
+}
+
+Batcher::~Batcher() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+}
+
+int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint32_t k,
+                    float* scores, uint64_t* rows, uint32_t* count, std::string* err) {
+  std::condition_variable done_cv;
+  Req r{&coll, q, dim, k, scores, rows, count};
+  r.cv = &done_cv;
+  std::unique_lock<std::mutex> lk(mu_);
+  if (stop_) {
+    if (err) *err = "service is closing";
+    return VS_ERR_INVALID_ARG;
+  }
+  queue_.push_back(&r);
+  cv_.notify_all();
+  done_cv.wait(lk, [&] { return r.done; });
+  if (r.rc != VS_OK && err) *err = r.err;
+  return r.rc;
+}
+
+Stats Batcher::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  return stats_;
+}
+
+void Batcher::run() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+    if (queue_.empty()) break;  // stop_ and drained
+    if (opt_.max_wait_us && queue_.size() < opt_.max_batch && !stop_)
+      cv_.wait_for(lk, std::chrono::microseconds(opt_.max_wait_us),
+                   [&] { return stop_ || queue_.size() >= opt_.max_batch; });
+    // take everything queued: groups below split it into engine calls
+    std::vector<Req*> batch(queue_.begin(), queue_.end());
+    queue_.clear();
+    lk.unlock();
+    execute(batch);
+    lk.lock();
+    for (Req* r : batch) {
+      r->done = true;
+      r->cv->notify_one();
+    }
+  }
+}
+
+void Batcher::execute(std::vector<Req*>& batch) {
+  // group: collection, dim, k class (MFMA-eligible or not); arrival order kept
+  std::map<std::tuple<std::string, uint32_t, bool>, std::vector<Req*>> groups;
+  for (Req* r : batch) groups[{*r->coll, r->dim, r->k > kMfmaMaxK}].push_back(r);
+  std::vector<float> q, sc;
+  std::vector<uint64_t> rw;
+  std::vector<uint32_t> cn;
+  for (auto& kv : groups) {
+    const std::string& coll = std::get<0>(kv.first);
+    const uint32_t dim = std::get<1>(kv.first);
+    auto& reqs = kv.second;
+    for (size_t b0 = 0; b0 < reqs.size(); b0 += opt_.max_batch) {
+      const size_t nq = std::min<size_t>(opt_.max_batch, reqs.size() - b0);
+      uint32_t kmax = 1;
+      for (size_t i = 0; i < nq; ++i) kmax = std::max(kmax, reqs[b0 + i]->k);
+      q.resize(nq * dim);
+      for (size_t i = 0; i < nq; ++i)
+        std::memcpy(q.data() + i * dim, reqs[b0 + i]->q, (size_t)dim * 4);
+      sc.resize(nq * kmax);
+      rw.resize(nq * kmax);
+      cn.resize(nq);
+      const int rc = vs_search(eng_, coll.c_str(), q.data(), (uint32_t)nq, dim, kmax, sc.data(),
+                               rw.data(), cn.data());
+      const std::string err = rc == VS_OK ? std::string() : std::string(vs_last_error());
+      for (size_t i = 0; i < nq; ++i) {
+        Req* r = reqs[b0 + i];
+        r->rc = rc;
+        if (rc != VS_OK) {
+          r->err = err;
+          continue;
+        }
+        const uint32_t c = std::min(cn[i], r->k);  // top k = the first k of top kmax
+        std::memcpy(r->scores, sc.data() + i * kmax, (size_t)c * 4);
+        std::memcpy(r->rows, rw.data() + i * kmax, (size_t)c * 8);
+        *r->count = c;
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      stats_.requests += nq;
+      stats_.engine_calls += 1;
+      stats_.max_batch = std::max<uint64_t>(stats_.max_batch, nq);
+      int h = 0;
+      while (h < 9 && (size_t(2) << h) <= nq) ++h;
+      stats_.hist[h] += 1;
+    }
+  }
+}
+
+}  // namespace vsbatch

@@ -1,0 +1,79 @@
+// batcher.h — dynamic batcher for concurrent /search requests (SURVEY.md §8
+// (b) "Threading" and (f) rank 2).
+//
+// rag/vector-service answers every /search with one Points.Search call for
+// one query (rag/vector-service/main.go:249-254); net/http runs the handlers
+// concurrently (main.go:77). Here concurrent handlers hand their query to one
+// worker thread per service, which coalesces whatever is queued into a few
+// vs_search(nq > 1) calls: a batch of bf16 queries then takes the MFMA path
+// (one pass over the corpus for up to 256 queries) instead of nq GEMV passes.
+//
+// Exactness: requests of one collection are searched together with
+// k_max = the largest k among them, and each request keeps the first k of its
+// k_max results. The engine orders results by (score desc, row asc), a total
+// order, so that prefix is exactly the top k. Requests with k above the
+// engine's batched-MFMA limit (128) are grouped separately, so a single large
+// k never moves the small-k requests off the MFMA path.
+//
+// Batching policy: no timer by default. While the worker runs one batch, new
+// requests queue up and form the next one, so the batch size follows the
+// offered load (1 when idle, up to max_batch under load) and a lone request
+// waits for nothing. max_wait_us > 0 adds a linger before a non-full batch.
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/vsearch.h"
+
+namespace vsbatch {
+
+struct Options {
+  bool enabled = true;
+  uint32_t max_batch = 256;  // queries per engine call
+  uint32_t max_wait_us = 0;  // linger for a non-full batch (0 = none)
+};
+
+struct Stats {
+  uint64_t requests = 0;      // searches served through the batcher
+  uint64_t engine_calls = 0;  // vs_search calls they took
+  uint64_t max_batch = 0;     // largest nq of one call
+  uint64_t hist[10] = {};     // calls by nq: 1, 2-3, 4-7, ..., 256+
+};
+
+class Batcher {
+ public:
+  Batcher(vs_engine* eng, Options opt);
+  ~Batcher();  // drains the queue, then joins the worker
+  Batcher(const Batcher&) = delete;
+  Batcher& operator=(const Batcher&) = delete;
+
+  // Blocks until the request's batch ran. Same contract as vs_search for one
+  // query of `dim` floats: scores / rows hold k entries, *count the valid ones.
+  // On failure returns the engine's status with its message in *err.
+  int search(const std::string& coll, const float* q, uint32_t dim, uint32_t k, float* scores,
+             uint64_t* rows, uint32_t* count, std::string* err);
+
+  Stats stats();
+  const Options& options() const { return opt_; }
+
+ private:
+  struct Req;
+  void run();
+  void execute(std::vector<Req*>& batch);
+
+  vs_engine* eng_;
+  Options opt_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Req*> queue_;
+  bool stop_ = false;
+  Stats stats_;
+  std::thread worker_;
+};
+
+}  // namespace vsbatch

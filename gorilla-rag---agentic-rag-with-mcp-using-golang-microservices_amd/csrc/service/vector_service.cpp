@@ -8,6 +8,7 @@
 // gRPC error shape ("rpc error: code = ... desc = ...") is kept in the
 // messages, as the Go service surfaces err.Error() verbatim.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "../../../include/vsearch_service.h"
+#include "batcher.h"
 #include "json.h"
 
 using vsjson::Json;
@@ -28,10 +30,62 @@ struct CollState {
   std::string name;
   uint32_t dim = 0;
   std::shared_mutex mu;                              // upsert = writer, search = reader
-  std::unordered_map<std::string, uint64_t> row_of;  // canonical UUID -> row
-  std::vector<std::string> uuid_of;                  // row -> UUID
-  std::vector<Json> payload_of;                      // row -> payload (a decoded map)
+  // Rows [0, bulk) came from vsvc_bulk_generate: their UUIDs are synthetic
+  // and invertible (bulk_uuid / bulk_row), so no per-row host state exists
+  // for them; a payload upserted onto one lands in bulk_payload.
+  uint64_t bulk = 0, bulk_tag = 0;
+  std::unordered_map<uint64_t, Json> bulk_payload;
+  std::unordered_map<std::string, uint64_t> row_of;  // canonical UUID -> row (>= bulk)
+  std::vector<std::string> uuid_of;                  // row - bulk -> UUID
+  std::vector<Json> payload_of;                      // row - bulk -> payload (a decoded map)
+
+  uint64_t nrows() const { return bulk + uuid_of.size(); }
 };
+
+// Synthetic UUID of bulk row r: version 4, variant 10, the collection's
+// 48-bit tag in the first 12 hex digits and r in the last 62 bits.
+std::string bulk_uuid(uint64_t tag, uint64_t r) {
+  const uint64_t hi = (tag << 16) | 0x4000u, lo = 0x8000000000000000ull | r;
+  char b[40];
+  std::snprintf(b, sizeof(b), "%08x-%04x-%04x-%04x-%012llx", (unsigned)(hi >> 32),
+                (unsigned)((hi >> 16) & 0xFFFF), (unsigned)(hi & 0xFFFF), (unsigned)(lo >> 48),
+                (unsigned long long)(lo & 0xFFFFFFFFFFFFull));
+  return b;
+}
+
+// Inverse of bulk_uuid on a canonical UUID; false if it is not one of cs's.
+bool bulk_row(const CollState& cs, const std::string& canon, uint64_t* row) {
+  if (!cs.bulk || canon.size() != 36) return false;
+  uint64_t hi = 0, lo = 0;
+  int nd = 0;
+  for (char ch : canon) {
+    if (ch == '-') continue;
+    const int v = ch >= '0' && ch <= '9' ? ch - '0' : (ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : -1);
+    if (v < 0) return false;
+    uint64_t& w = nd < 16 ? hi : lo;
+    w = (w << 4) | (uint64_t)v;
+    ++nd;
+  }
+  if (nd != 32 || hi != ((cs.bulk_tag << 16) | 0x4000u) || (lo >> 62) != 2) return false;
+  const uint64_t r = lo & 0x3FFFFFFFFFFFFFFFull;
+  if (r >= cs.bulk) return false;
+  *row = r;
+  return true;
+}
+
+std::string uuid_at(const CollState& cs, uint64_t row) {
+  if (row < cs.bulk) return bulk_uuid(cs.bulk_tag, row);
+  return row < cs.nrows() ? cs.uuid_of[row - cs.bulk] : std::string();
+}
+
+const Json& payload_at(const CollState& cs, uint64_t row) {
+  static const Json kEmpty = Json::object();
+  if (row < cs.bulk) {
+    auto it = cs.bulk_payload.find(row);
+    return it == cs.bulk_payload.end() ? kEmpty : it->second;
+  }
+  return row < cs.nrows() ? cs.payload_of[row - cs.bulk] : kEmpty;
+}
 
 struct Response {
   int status = 200;
@@ -251,6 +305,8 @@ struct vsvc {
   std::vector<std::string> listed;  // the /collections reply (hard-coded in the reference)
   std::mutex mu;
   std::unordered_map<std::string, std::shared_ptr<CollState>> colls;
+  vsbatch::Options batch_opt;
+  std::unique_ptr<vsbatch::Batcher> batcher;  // coalesces concurrent /search (batcher.h)
 
   std::shared_ptr<CollState> find(const std::string& name) {
     std::lock_guard<std::mutex> g(mu);
@@ -337,12 +393,14 @@ Response handle_upsert(vsvc* svc, const std::string& method, const char* body, s
       return error_json("Failed to upsert: " + dim_error(cs->dim, vecs[i].size()), 500);
 
   std::unique_lock<std::shared_mutex> wl(cs->mu);
-  const uint64_t base = cs->uuid_of.size();
+  const uint64_t base = cs->nrows();
   std::unordered_map<std::string, uint64_t> fresh;  // new UUIDs of this batch
   std::vector<uint64_t> rows(n);
   for (size_t i = 0; i < n; ++i) {
     auto it = cs->row_of.find(canon[i]);
-    if (it != cs->row_of.end()) {
+    if (bulk_row(*cs, canon[i], &rows[i])) {
+      // a bulk-generated point, overwritten by its id
+    } else if (it != cs->row_of.end()) {
       rows[i] = it->second;
     } else {
       auto f = fresh.find(canon[i]);
@@ -361,12 +419,16 @@ Response handle_upsert(vsvc* svc, const std::string& method, const char* body, s
     int rc = vs_upsert(svc->eng, req.collection.c_str(), n, cs->dim, rows.data(), flat.data());
     if (rc != VS_OK) return error_json("Failed to upsert: " + grpc_error(rc, last_error()), 500);
   }
-  cs->uuid_of.resize(base + fresh.size());
-  cs->payload_of.resize(base + fresh.size());
+  cs->uuid_of.resize(base + fresh.size() - cs->bulk);
+  cs->payload_of.resize(base + fresh.size() - cs->bulk);
   for (size_t i = 0; i < n; ++i) {  // in request order: the last duplicate wins
+    if (rows[i] < cs->bulk) {
+      cs->bulk_payload[rows[i]] = payloads[i];
+      continue;
+    }
     cs->row_of[canon[i]] = rows[i];
-    cs->uuid_of[rows[i]] = canon[i];
-    cs->payload_of[rows[i]] = payloads[i];
+    cs->uuid_of[rows[i] - cs->bulk] = canon[i];
+    cs->payload_of[rows[i] - cs->bulk] = payloads[i];
   }
   wl.unlock();
 
@@ -393,7 +455,7 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   std::shared_lock<std::shared_mutex> rl(cs->mu);
   if (req.query.size() != cs->dim)
     return error_json("Search failed: " + dim_error(cs->dim, req.query.size()), 500);
-  const uint64_t rows = cs->uuid_of.size();
+  const uint64_t rows = cs->nrows();
   uint64_t k = std::min<uint64_t>(limit, std::max<uint64_t>(rows, 1));
   if (k > 1024)
     return error_json("Search failed: " + grpc_error(VS_ERR_INVALID_ARG,
@@ -403,9 +465,20 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   std::vector<float> scores(k);
   std::vector<uint64_t> hit_rows(k);
   uint32_t count = 0;
-  int rc = vs_search(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
-                     (uint32_t)k, scores.data(), hit_rows.data(), &count);
-  if (rc != VS_OK) return error_json("Search failed: " + grpc_error(rc, last_error()), 500);
+  // Points.Search: through the batcher (one engine call for all concurrent
+  // requests) or directly. The collection's read lock is held until the
+  // reply is encoded, so rows and UUIDs cannot change underneath.
+  int rc;
+  std::string err;
+  if (svc->batcher) {
+    rc = svc->batcher->search(req.collection, req.query.data(), cs->dim, (uint32_t)k,
+                              scores.data(), hit_rows.data(), &count, &err);
+  } else {
+    rc = vs_search(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim, (uint32_t)k,
+                   scores.data(), hit_rows.data(), &count);
+    if (rc != VS_OK) err = last_error();
+  }
+  if (rc != VS_OK) return error_json("Search failed: " + grpc_error(rc, err), 500);
 
   // SearchResponse{Results, Count}: struct fields in declaration order
   std::string out;
@@ -414,11 +487,11 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
     if (j) out.push_back(',');
     const uint64_t row = hit_rows[j];
     out.append("{\"id\":");
-    vsjson::encode_string(row < rows ? cs->uuid_of[row] : std::string(), &out);
+    vsjson::encode_string(uuid_at(*cs, row), &out);
     out.append(",\"score\":");
     vsjson::encode_float64((double)scores[j], &out);  // float64(hit.GetScore())
     out.append(",\"payload\":");
-    vsjson::encode(row < rows ? cs->payload_of[row] : Json::object(), &out);
+    vsjson::encode(payload_at(*cs, row), &out);
     out.push_back('}');
   }
   out.append("],\"count\":");
@@ -451,6 +524,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
     int metric, dtype;
   };
   std::vector<Spec> specs;
+  vsbatch::Options bopt;
   if (!config_json) {
     for (const char* n : {"regulatory_docs", "merchant_docs", "kyc_docs"})
       specs.push_back({n, 768, VS_METRIC_COSINE, VS_DTYPE_F32});
@@ -473,9 +547,26 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
       if (dt && dt->kind == Json::String && dt->str == "bf16") s.dtype = VS_DTYPE_BF16;
       specs.push_back(s);
     }
+    // {"batching": {"enabled": bool, "max_batch": n, "max_wait_us": n}}
+    if (const Json* b = cfg.get("batching")) {
+      if (b->kind != Json::Object) return VS_ERR_INVALID_ARG;
+      if (const Json* e = b->get("enabled")) {
+        if (e->kind != Json::Bool) return VS_ERR_INVALID_ARG;
+        bopt.enabled = e->b;
+      }
+      if (const Json* m = b->get("max_batch")) {
+        if (m->kind != Json::Number || m->num < 1 || m->num > 4096) return VS_ERR_INVALID_ARG;
+        bopt.max_batch = (uint32_t)m->num;
+      }
+      if (const Json* w = b->get("max_wait_us")) {
+        if (w->kind != Json::Number || w->num < 0 || w->num > 1e6) return VS_ERR_INVALID_ARG;
+        bopt.max_wait_us = (uint32_t)w->num;
+      }
+    }
   }
   auto svc = std::make_unique<vsvc>();
   svc->eng = eng;
+  svc->batch_opt = bopt;
   for (const auto& s : specs) {
     // initializeCollections: Get, and Create when NotFound (main.go:91-112)
     uint32_t dim = 0;
@@ -492,11 +583,63 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
     svc->colls[s.name] = cs;
     svc->listed.push_back(s.name);
   }
+  if (bopt.enabled) svc->batcher = std::make_unique<vsbatch::Batcher>(eng, bopt);
   *out = svc.release();
   return VS_OK;
 }
 
-void vsvc_close(vsvc* svc) { delete svc; }
+void vsvc_close(vsvc* svc) { delete svc; }  // the batcher drains and joins first
+
+int vsvc_bulk_generate(vsvc* svc, const char* coll, uint64_t n, uint64_t seed) {
+  if (!svc || !coll) return VS_ERR_INVALID_ARG;
+  auto cs = svc->find(coll);
+  if (!cs) return VS_ERR_NOT_FOUND;
+  if (n >= (1ull << 40)) return VS_ERR_INVALID_ARG;
+  std::unique_lock<std::shared_mutex> wl(cs->mu);
+  if (cs->nrows() != 0) return VS_ERR_EXISTS;  // bulk rows come first
+  const int rc = vs_generate(svc->eng, coll, n, seed);
+  if (rc != VS_OK) return rc;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the name, mixed with the seed
+  for (const char* p = coll; *p; ++p) h = (h ^ (uint8_t)*p) * 1099511628211ull;
+  h ^= seed + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  h = (h ^ (h >> 31)) * 0xBF58476D1CE4E5B9ull;
+  cs->bulk_tag = ((h ^ (h >> 29)) & 0xFFFFFFFFFFFFull) | 1u;
+  cs->bulk = n;
+  return VS_OK;
+}
+
+int vsvc_point_id(vsvc* svc, const char* coll, uint64_t row, char* buf, size_t len) {
+  if (!svc || !coll || !buf || len < 37) return VS_ERR_INVALID_ARG;
+  auto cs = svc->find(coll);
+  if (!cs) return VS_ERR_NOT_FOUND;
+  std::shared_lock<std::shared_mutex> rl(cs->mu);
+  if (row >= cs->nrows()) return VS_ERR_INVALID_ARG;
+  const std::string u = uuid_at(*cs, row);
+  std::memcpy(buf, u.c_str(), u.size() + 1);
+  return VS_OK;
+}
+
+int vsvc_stats(vsvc* svc, char** out) {
+  if (!svc || !out) return VS_ERR_INVALID_ARG;
+  vsbatch::Stats st;
+  if (svc->batcher) st = svc->batcher->stats();
+  Json o = Json::object();
+  Json b = Json::object();
+  b.obj.emplace_back("enabled", Json::boolean(svc->batcher != nullptr));
+  b.obj.emplace_back("max_batch", Json::number(svc->batch_opt.max_batch));
+  b.obj.emplace_back("max_wait_us", Json::number(svc->batch_opt.max_wait_us));
+  o.obj.emplace_back("batching", std::move(b));
+  o.obj.emplace_back("requests", Json::number((double)st.requests));
+  o.obj.emplace_back("engine_calls", Json::number((double)st.engine_calls));
+  o.obj.emplace_back("largest_call", Json::number((double)st.max_batch));
+  Json h = Json::array();
+  for (uint64_t v : st.hist) h.arr.push_back(Json::number((double)v));
+  o.obj.emplace_back("calls_by_log2_nq", std::move(h));
+  std::string s;
+  vsjson::encode(o, &s, false);
+  *out = dup_bytes(s);
+  return *out ? VS_OK : VS_ERR_OOM;
+}
 
 int vsvc_handle(vsvc* svc, const char* method, const char* path, const char* body,
                 size_t body_len, int* status, char** resp, size_t* resp_len,

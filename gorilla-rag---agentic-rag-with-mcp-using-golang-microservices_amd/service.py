@@ -40,6 +40,14 @@ def load_service_library(path: str = SVC_LIB_PATH):
     L.vsvc_reencode.restype = ctypes.c_int
     L.vsvc_validate.argtypes = [cp, cp, sz, ctypes.POINTER(vp)]
     L.vsvc_validate.restype = ctypes.c_int
+    L.vsvc_bulk_generate.argtypes = [vp, cp, ctypes.c_uint64, ctypes.c_uint64]
+    L.vsvc_bulk_generate.restype = ctypes.c_int
+    L.vsvc_point_id.argtypes = [vp, cp, ctypes.c_uint64, cp, sz]
+    L.vsvc_point_id.restype = ctypes.c_int
+    L.vsvc_stats.argtypes = [vp, ctypes.POINTER(vp)]
+    L.vsvc_stats.restype = ctypes.c_int
+    L.vsvc_loadgen.argtypes = [vp, cp, ctypes.POINTER(vp)]
+    L.vsvc_loadgen.restype = ctypes.c_int
     _svc = L
     return L
 
@@ -102,3 +110,29 @@ class VectorService:
         if rc != 0:
             raise VSError(rc, "vsvc_handle failed")
         return st.value, _take(self._L, out, n.value), ct.value.decode()
+
+    def bulk_generate(self, collection: str, n: int, seed: int) -> None:
+        """n synthetic device-generated points with synthetic UUIDs (empty collection)."""
+        _check(self._L.vsvc_bulk_generate(self._h, collection.encode(), n, seed))
+
+    def point_id(self, collection: str, row: int) -> str:
+        buf = ctypes.create_string_buffer(40)
+        _check(self._L.vsvc_point_id(self._h, collection.encode(), row, buf, 40))
+        return buf.value.decode()
+
+    def stats(self) -> dict:
+        """Batcher counters (vsvc_stats)."""
+        out = ctypes.c_void_p()
+        _check(self._L.vsvc_stats(self._h, ctypes.byref(out)))
+        return json.loads(_take(self._L, out))
+
+    def loadgen(self, collections, dim: int, clients: int = 16, seconds: float = 5.0,
+                k_min: int = 3, k_max: int = 50, queries: int = 256, seed: int = 1) -> dict:
+        """Closed-loop /search load (vsvc_loadgen): retrieval-service-shaped
+        requests from `clients` threads for `seconds`; returns QPS + latency."""
+        spec = json.dumps({"collections": list(collections), "dim": dim, "clients": clients,
+                           "seconds": seconds, "k_min": k_min, "k_max": k_max,
+                           "queries": queries, "seed": seed}).encode()
+        out = ctypes.c_void_p()
+        _check(self._L.vsvc_loadgen(self._h, spec, ctypes.byref(out)))
+        return json.loads(_take(self._L, out))

@@ -35,9 +35,39 @@ typedef struct vsvc vsvc;
  * the reference defaults (initializeCollections, main.go:80-119: collections
  * regulatory_docs, merchant_docs, kyc_docs, dim 768, Cosine, fp32) or
  * {"collections":[{"name":"..","dim":768,"metric":"Cosine"|"Dot",
- *  "dtype":"f32"|"bf16"}...]}. Existing collections are reused. */
+ *  "dtype":"f32"|"bf16"}...],
+ *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0}}.
+ * Existing collections are reused. Batching (on by default) coalesces
+ * concurrent /search requests into one engine call per collection
+ * (csrc/service/batcher.h); each request still gets exactly its own top k. */
 int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out);
 void vsvc_close(vsvc* svc);
+
+/* Bulk load for benchmarks and large corpora: appends n
+ * synthetic unit rows generated on the device (vs_generate, `seed`) to an
+ * EMPTY collection, with synthetic version-4 UUIDs (a per-collection tag and
+ * the row number, invertible, so no per-row host state is kept) and empty
+ * payloads. /search returns those ids; /upsert with one of them overwrites
+ * that row; new ids append after the bulk rows. VS_ERR_EXISTS if the
+ * collection already holds points. */
+int vsvc_bulk_generate(vsvc* svc, const char* coll, uint64_t n, uint64_t seed);
+/* The point id (canonical UUID, 36 chars + NUL) of `row` of `coll`. */
+int vsvc_point_id(vsvc* svc, const char* coll, uint64_t row, char* buf, size_t len);
+
+/* Batcher counters as JSON (*out malloc'd; free with vsvc_free):
+ * {"batching":{...},"requests":n,"engine_calls":n,"largest_call":n,
+ *  "calls_by_log2_nq":[nq=1, 2-3, 4-7, ..., 256-511, 512+]}. */
+int vsvc_stats(vsvc* svc, char** out);
+
+/* Closed-loop load generator: `clients` threads each send
+ * /search bodies shaped like rag/retrieval-service's searchVectorDB
+ * (main.go:221-226: {"collection","filter","query","top_k"}) through
+ * vsvc_handle, back to back, for `seconds`. spec_json:
+ * {"collections":["..",..],"dim":768,"clients":64,"seconds":5,"k_min":3,
+ *  "k_max":50,"queries":256,"seed":1}. *report (malloc'd) gets
+ * {"requests","errors","seconds","qps","lat_ms":{"p50","p90","p99","max"},
+ *  "first_error"}. Returns VS_OK or VS_ERR_INVALID_ARG for a bad spec. */
+int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report);
 
 /* Serves one HTTP request. Sets *status, *body (malloc'd, NUL-terminated;
  * free with vsvc_free) and *content_type (static string). Safe to call from

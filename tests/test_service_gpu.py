@@ -184,3 +184,139 @@ def test_concurrent_search_and_upsert(service, orc):
     st, body, _ = _post(service, "/search", {"collection": "merchant_docs", "query": X[399].tolist(),
                                              "top_k": 1})
     assert json.loads(body)["results"][0]["id"] == ids[399]
+
+
+# ------------------------------------------------------------ dynamic batcher
+_BATCH_CFG = {"collections": [{"name": "b16", "dim": 768, "metric": "Cosine", "dtype": "bf16"},
+                              {"name": "f32", "dim": 768, "metric": "Cosine", "dtype": "f32"}]}
+
+
+def _fill(s, orc, coll, n, seed, bf16):
+    X = orc.generate(seed, 0, n, 768)
+    ids = _ids(n, seed=seed)
+    for lo in range(0, n, 512):
+        st, body, _ = _post(s, "/upsert", {"collection": coll, "points": [
+            {"id": ids[i], "vector": X[i].tolist(), "payload": {"i": i}}
+            for i in range(lo, min(n, lo + 512))]})
+        assert st == 200, body
+    return orc.preprocess(X, True, bf16), ids
+
+
+@pytest.fixture(params=[0])
+def batch_service(pkg, svcmod, request):
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng, dict(_BATCH_CFG, batching={"max_wait_us": request.param}))
+    yield s
+    s.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("batch_service", [50_000], indirect=True)
+def test_batcher_concurrent_requests_exact(batch_service, orc):
+    """64 concurrent /search requests over two collections with mixed k
+    (including k > 128, the GEMV class) are coalesced into few engine calls,
+    and every reply is still that request's own exact top k. (Python clients
+    serialise on the GIL while they build their bodies, so the batcher
+    lingers 50 ms here to collect them.)"""
+    s = batch_service
+    data = {"b16": _fill(s, orc, "b16", 3000, 21, True), "f32": _fill(s, orc, "f32", 2000, 22, False)}
+    nreq = 64
+    Q = orc.generate(orc.SEED_QUERY, 500, nreq, 768)
+    ks = [1 + (7 * i) % 60 for i in range(nreq)]
+    ks[5], ks[40] = 200, 129
+    colls = ["b16" if i % 3 else "f32" for i in range(nreq)]
+    replies = [None] * nreq
+    gate = threading.Barrier(nreq)
+
+    def client(i):
+        gate.wait()
+        replies[i] = _post(s, "/search", {"collection": colls[i], "query": Q[i].tolist(),
+                                          "top_k": ks[i], "filter": None})
+
+    th = [threading.Thread(target=client, args=(i,)) for i in range(nreq)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i in range(nreq):
+        st, body, _ = replies[i]
+        assert st == 200, body
+        res = json.loads(body)
+        Xp, ids = data[colls[i]]
+        k = ks[i]
+        assert res["count"] == k == len(res["results"])
+        rows = np.array([[ids.index(r["id"]) for r in res["results"]]], np.uint64)
+        assert all(r["payload"] == {"i": int(rows[0, j])} for j, r in enumerate(res["results"]))
+        scores = np.array([[r["score"] for r in res["results"]]])
+        qp = orc.preprocess(Q[i:i + 1], True, colls[i] == "b16")
+        s32, s64, rr, cc = orc.search(Xp, qp, k)
+        resc = orc.rescore(Xp, qp, rows, np.array([k], np.uint32))
+        assert not orc.check_topk(scores, rows, np.array([k]), s64, rr, cc, resc, 1e-5), i
+    st = s.stats()
+    assert st["batching"]["enabled"] and st["requests"] >= nreq
+    assert st["engine_calls"] < st["requests"] and st["largest_call"] >= 2, st
+
+
+def test_batcher_disabled(pkg, svcmod, orc):
+    eng = pkg.VectorEngine(device=0)
+    cfg = dict(_BATCH_CFG, batching={"enabled": False})
+    s = svcmod.VectorService(eng, cfg)
+    try:
+        Xp, ids = _fill(s, orc, "b16", 300, 5, True)
+        st, body, _ = _post(s, "/search", {"collection": "b16", "query": Xp[7].tolist(), "top_k": 3})
+        assert st == 200 and json.loads(body)["results"][0]["id"] == ids[7]
+        assert s.stats() == {"batching": {"enabled": False, "max_batch": 256, "max_wait_us": 0},
+                             "requests": 0, "engine_calls": 0, "largest_call": 0,
+                             "calls_by_log2_nq": [0] * 10}
+    finally:
+        s.close()
+        eng.close()
+    with pytest.raises(Exception):
+        svcmod.VectorService(pkg.VectorEngine(device=0), dict(_BATCH_CFG, batching={"max_batch": 0}))
+
+
+def test_loadgen_closed_loop(batch_service, orc):
+    """C5-shaped load in miniature: 32 closed-loop clients, k in [3, 50],
+    two collections; no errors, and the batcher forms multi-query calls."""
+    s = batch_service
+    _fill(s, orc, "b16", 2000, 31, True)
+    _fill(s, orc, "f32", 1000, 32, False)
+    rep = s.loadgen(["b16", "f32"], 768, clients=32, seconds=1.5, k_min=3, k_max=50)
+    assert rep["errors"] == 0, rep["first_error"]
+    assert rep["requests"] > 100 and rep["qps"] > 0
+    assert rep["lat_ms"]["p50"] <= rep["lat_ms"]["p99"] <= rep["lat_ms"]["max"]
+    st = s.stats()
+    assert st["requests"] == rep["requests"] and st["largest_call"] >= 2, st
+
+
+def test_bulk_generate_ids_and_overwrite(batch_service, orc):
+    """vsvc_bulk_generate: device-generated points with synthetic v4 UUIDs,
+    searchable, overwritable by id; new ids append after them."""
+    import re
+    s = batch_service
+    n = 5000
+    s.bulk_generate("b16", n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, 768, bf16=True)
+    uid = s.point_id("b16", 123)
+    assert re.fullmatch(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}", uid)
+    assert len({s.point_id("b16", r) for r in (0, 1, 123, n - 1)}) == 4
+    st, body, _ = _post(s, "/search", {"collection": "b16", "query": X[123].tolist(), "top_k": 3})
+    res = json.loads(body)
+    assert st == 200 and res["results"][0]["id"] == uid and res["results"][0]["payload"] == {}
+    # overwrite the bulk point by its id (upper case in, canonical out)
+    st, body, _ = _post(s, "/upsert", {"collection": "b16", "points": [
+        {"id": uid.upper(), "vector": (-X[123]).tolist(), "payload": {"v": 1}}]})
+    assert st == 200, body
+    st, body, _ = _post(s, "/search", {"collection": "b16", "query": (-X[123]).tolist(), "top_k": 1})
+    r0 = json.loads(body)["results"][0]
+    assert r0["id"] == uid and r0["payload"] == {"v": 1}
+    # a new id appends at row n
+    new = _ids(1, seed=77)[0]
+    st, body, _ = _post(s, "/upsert", {"collection": "b16", "points": [
+        {"id": new, "vector": X[7].tolist(), "payload": {"new": True}}]})
+    assert st == 200 and s.point_id("b16", n) == new
+    st, body, _ = _post(s, "/search", {"collection": "b16", "query": X[7].tolist(), "top_k": 2})
+    got = {r["id"] for r in json.loads(body)["results"]}
+    assert got == {new, s.point_id("b16", 7)}
+    with pytest.raises(Exception):
+        s.bulk_generate("b16", 10, 1)  # only into an empty collection
