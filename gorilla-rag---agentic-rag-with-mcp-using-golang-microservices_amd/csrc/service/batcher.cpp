@@ -72,9 +72,23 @@ void Batcher::run() {
     if (opt_.max_wait_us && queue_.size() < opt_.max_batch && !stop_)
       cv_.wait_for(lk, std::chrono::microseconds(opt_.max_wait_us),
                    [&] { return stop_ || queue_.size() >= opt_.max_batch; });
-    // take everything queued: groups below split it into engine calls
-    std::vector<Req*> batch(queue_.begin(), queue_.end());
-    queue_.clear();
+    // One engine call per turn, for the group (collection, dim, k class) of
+    // the oldest queued request: all of that group's queued requests, up to
+    // max_batch, go together; other groups keep queueing meanwhile, so the
+    // next call of each collection finds its whole backlog (a group never
+    // waits behind more than one call of every other group: no starvation).
+    const Req* first = queue_.front();
+    std::vector<Req*> batch;
+    for (auto it = queue_.begin(); it != queue_.end() && batch.size() < opt_.max_batch;) {
+      Req* r = *it;
+      if (*r->coll == *first->coll && r->dim == first->dim &&
+          (r->k > kMfmaMaxK) == (first->k > kMfmaMaxK)) {
+        batch.push_back(r);
+        it = queue_.erase(it);
+      } else {
+        ++it;
+      }
+    }
     lk.unlock();
     execute(batch);
     lk.lock();

@@ -15,10 +15,13 @@
 // engine's batched-MFMA limit (128) are grouped separately, so a single large
 // k never moves the small-k requests off the MFMA path.
 //
-// Batching policy: no timer by default. While the worker runs one batch, new
-// requests queue up and form the next one, so the batch size follows the
-// offered load (1 when idle, up to max_batch under load) and a lone request
-// waits for nothing. max_wait_us > 0 adds a linger before a non-full batch.
+// Batching policy: no timer by default. Each turn the worker makes one engine
+// call for the group (collection, dim, k class) of the oldest queued request,
+// taking all of that group's queued requests (up to max_batch). While it runs,
+// new requests queue up, so the batch size follows the offered load (1 when
+// idle, up to max_batch under load), a lone request waits for nothing, and
+// with several collections each call finds its collection's whole backlog.
+// max_wait_us > 0 adds a linger before a non-full batch.
 #pragma once
 #include <condition_variable>
 #include <cstdint>
