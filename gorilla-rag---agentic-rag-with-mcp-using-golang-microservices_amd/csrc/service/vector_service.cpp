@@ -608,6 +608,104 @@ int vsvc_bulk_generate(vsvc* svc, const char* coll, uint64_t n, uint64_t seed) {
   return VS_OK;
 }
 
+// Sidecar of a collection snapshot: the host half of the store (UUIDs,
+// payloads, bulk range) as JSON; the rows go through vs_snapshot.
+//   {"bulk":n,"bulk_tag":t,"bulk_payload":[[row,{..}],..],"points":[["uuid",{..}],..]}
+// with points[i] = row bulk + i.
+int vsvc_snapshot(vsvc* svc, const char* dir) {
+  if (!svc || !dir) return VS_ERR_INVALID_ARG;
+  for (const std::string& name : svc->listed) {
+    auto cs = svc->find(name);
+    std::shared_lock<std::shared_mutex> rl(cs->mu);  // upserts wait
+    const std::string base = std::string(dir) + "/" + name;
+    int rc = vs_snapshot(svc->eng, name.c_str(), (base + ".vsnap").c_str());
+    if (rc != VS_OK) return rc;
+    std::string out = "{\"bulk\":" + std::to_string(cs->bulk) +
+                      ",\"bulk_tag\":" + std::to_string(cs->bulk_tag) + ",\"bulk_payload\":[";
+    bool first = true;
+    for (const auto& kv : cs->bulk_payload) {
+      out.append(first ? "[" : ",[");
+      first = false;
+      out.append(std::to_string(kv.first));
+      out.push_back(',');
+      vsjson::encode(kv.second, &out);
+      out.push_back(']');
+    }
+    out.append("],\"points\":[");
+    for (size_t i = 0; i < cs->uuid_of.size(); ++i) {
+      out.append(i ? ",[" : "[");
+      vsjson::encode_string(cs->uuid_of[i], &out);
+      out.push_back(',');
+      vsjson::encode(cs->payload_of[i], &out);
+      out.push_back(']');
+    }
+    out.append("]}\n");
+    const std::string tmp = base + ".points.json.tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    bool ok = f && std::fwrite(out.data(), 1, out.size(), f) == out.size();
+    if (f) ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), (base + ".points.json").c_str()) != 0)
+      return VS_ERR_IO;
+  }
+  return VS_OK;
+}
+
+int vsvc_restore(vsvc* svc, const char* dir) {
+  if (!svc || !dir) return VS_ERR_INVALID_ARG;
+  for (const std::string& name : svc->listed) {
+    auto cs = svc->find(name);
+    const std::string base = std::string(dir) + "/" + name;
+    FILE* f = std::fopen((base + ".points.json").c_str(), "rb");
+    if (!f) continue;  // nothing saved for this collection
+    std::string text;
+    char buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, n);
+    std::fclose(f);
+    Json side;
+    std::string err;
+    if (!vsjson::parse(text.data(), text.size(), &side, &err)) return VS_ERR_IO;
+    const Json* jb = side.get("bulk");
+    const Json* jt = side.get("bulk_tag");
+    const Json* jbp = side.get("bulk_payload");
+    const Json* jp = side.get("points");
+    if (!jb || jb->kind != Json::Number || !jt || jt->kind != Json::Number || !jbp ||
+        jbp->kind != Json::Array || !jp || jp->kind != Json::Array)
+      return VS_ERR_IO;
+    std::unique_lock<std::shared_mutex> wl(cs->mu);
+    if (cs->nrows() != 0) return VS_ERR_EXISTS;  // restore only into an empty service
+    uint32_t dim = 0;
+    int metric = 0, dtype = 0;
+    int rc = vs_collection_info(svc->eng, name.c_str(), &dim, nullptr, &metric, &dtype);
+    if (rc != VS_OK) return rc;
+    if ((rc = vs_collection_drop(svc->eng, name.c_str())) != VS_OK) return rc;
+    rc = vs_restore(svc->eng, name.c_str(), (base + ".vsnap").c_str());
+    uint64_t rows = 0;
+    uint32_t rdim = 0;
+    if (rc == VS_OK) rc = vs_collection_info(svc->eng, name.c_str(), &rdim, &rows, nullptr, nullptr);
+    const uint64_t bulk = (uint64_t)jb->num;
+    if (rc == VS_OK && (rdim != dim || rows != bulk + jp->arr.size())) rc = VS_ERR_IO;
+    if (rc != VS_OK) {  // leave the collection as it was: empty
+      (void)vs_collection_drop(svc->eng, name.c_str());
+      (void)vs_collection_create(svc->eng, name.c_str(), dim, metric, dtype, 0, 0);
+      return rc;
+    }
+    cs->bulk = bulk;
+    cs->bulk_tag = (uint64_t)jt->num;
+    for (const auto& e : jbp->arr)
+      if (e.kind == Json::Array && e.arr.size() == 2) cs->bulk_payload[(uint64_t)e.arr[0].num] = e.arr[1];
+    cs->uuid_of.reserve(jp->arr.size());
+    cs->payload_of.reserve(jp->arr.size());
+    for (const auto& e : jp->arr) {
+      if (e.kind != Json::Array || e.arr.size() != 2 || e.arr[0].kind != Json::String) return VS_ERR_IO;
+      cs->row_of[e.arr[0].str] = cs->bulk + cs->uuid_of.size();
+      cs->uuid_of.push_back(e.arr[0].str);
+      cs->payload_of.push_back(e.arr[1]);
+    }
+  }
+  return VS_OK;
+}
+
 int vsvc_point_id(vsvc* svc, const char* coll, uint64_t row, char* buf, size_t len) {
   if (!svc || !coll || !buf || len < 37) return VS_ERR_INVALID_ARG;
   auto cs = svc->find(coll);

@@ -34,6 +34,15 @@ VS_HD int32_t gen_int(uint64_t row_key, uint32_t col) {
                    (h >> 48)) - 131070;
 }
 
+// ---- snapshot checksum --------------------------------
+// H = sum over the little-endian 64-bit words w_i of a byte range (the last
+// one zero-padded) of splitmix64(w_i ^ (i * phi)), mod 2^64: position
+// dependent, order-free to sum, so a device reduction and a sequential host
+// loop agree bit for bit.
+VS_HD uint64_t snap_word(uint64_t w, uint64_t i) {
+  return splitmix64(w ^ (i * 0x9E3779B97F4A7C15ull));
+}
+
 // ---- bf16 ------------------------------------------------------------------
 VS_HD uint16_t f32_to_bf16(float f) {
   uint32_t u = __builtin_bit_cast(uint32_t, f);

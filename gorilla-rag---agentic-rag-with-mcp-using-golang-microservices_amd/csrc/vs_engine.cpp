@@ -100,6 +100,7 @@ struct vs_engine {
   DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
   DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
   DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
+  DevBuf scratch8;                  // u64 result of the snapshot checksum
   uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
   std::vector<uint64_t> h_keys;
   // timing
@@ -194,6 +195,63 @@ int grow(vs_engine* eng, Collection& c, uint64_t need) {
   if (c.data) (void)hipFree(c.data);
   c.data = nd;
   c.cap = ncap;
+  return VS_OK;
+}
+
+
+// ---- snapshot file format (include/vsearch.h vs_snapshot) -------------------
+struct SnapHeader {
+  char magic[8];  // "VSNAP01\0"
+  uint32_t version, header_bytes;
+  uint32_t dim;
+  int32_t metric, dtype;
+  uint32_t elem_bytes;
+  uint64_t rows, row_base, data_bytes;
+  uint64_t data_checksum;
+  uint64_t header_checksum;  // vs::snap_word sum over the 64 bytes above
+  uint8_t reserved[56];      // zero
+};
+static_assert(sizeof(SnapHeader) == 128, "snapshot header is 128 bytes");
+constexpr char kSnapMagic[8] = {'V', 'S', 'N', 'A', 'P', '0', '1', '\0'};
+constexpr size_t kSnapChunk = 64ull << 20;  // D2H / H2D staging per chunk
+
+uint64_t header_sum(const SnapHeader& h) {
+  uint64_t w[8], s = 0;
+  std::memcpy(w, &h, 64);
+  for (int i = 0; i < 8; ++i) s += vs::snap_word(w[i], (uint64_t)i);
+  return s;
+}
+
+struct PinnedPair {  // two staging buffers: one in flight, one on disk I/O
+  void* p[2] = {nullptr, nullptr};
+  ~PinnedPair() {
+    for (void* q : p)
+      if (q) (void)hipHostFree(q);
+  }
+  hipError_t alloc(size_t n) {
+    for (void*& q : p) {
+      hipError_t e = hipHostMalloc(&q, n, hipHostMallocDefault);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+};
+
+struct FileCloser {
+  FILE* f = nullptr;
+  ~FileCloser() {
+    if (f) std::fclose(f);
+  }
+};
+
+int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
+  VS_HIP(eng->scratch8.ensure(8), "alloc checksum");
+  VS_HIP(vsk::launch_checksum(c.data, c.rows * c.row_bytes(), eng->scratch8.as<uint64_t>(),
+                              eng->stream),
+         "checksum");
+  VS_HIP(hipMemcpyAsync(out, eng->scratch8.p, 8, hipMemcpyDeviceToHost, eng->stream),
+         "checksum D2H");
+  VS_HIP(hipStreamSynchronize(eng->stream), "checksum sync");
   return VS_OK;
 }
 
@@ -750,6 +808,142 @@ int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t
          "keys D2H");
   VS_HIP(hipStreamSynchronize(cs), "decode sync");
   decode_host(h.data(), nq, k, out_scores, out_rows, out_count);
+  return VS_OK;
+}
+
+int vs_checksum(vs_engine* eng, const char* coll, uint64_t* out) {
+  if (!eng || !out) return fail(VS_ERR_INVALID_ARG, "engine and out are required");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  return device_checksum(eng, *c, out);
+}
+
+int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
+  if (!eng || !path) return fail(VS_ERR_INVALID_ARG, "engine and path are required");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);  // upserts wait, searches proceed
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  SnapHeader h{};
+  std::memcpy(h.magic, kSnapMagic, 8);
+  h.version = 1;
+  h.header_bytes = sizeof(SnapHeader);
+  h.dim = c->dim;
+  h.metric = c->metric;
+  h.dtype = c->dtype;
+  h.elem_bytes = (uint32_t)c->elem();
+  h.rows = c->rows;
+  h.row_base = c->row_base;
+  h.data_bytes = c->rows * c->row_bytes();
+  int rc = device_checksum(eng, *c, &h.data_checksum);
+  if (rc != VS_OK) return rc;
+  h.header_checksum = header_sum(h);
+  const std::string tmp = std::string(path) + ".tmp";
+  FileCloser fc;
+  fc.f = std::fopen(tmp.c_str(), "wb");
+  if (!fc.f) return fail(VS_ERR_IO, "cannot open " + tmp + " for writing");
+  if (std::fwrite(&h, sizeof(h), 1, fc.f) != 1) return fail(VS_ERR_IO, "write failed: " + tmp);
+  PinnedPair pin;
+  const size_t chunk = std::min<size_t>(kSnapChunk, std::max<size_t>(h.data_bytes, 1));
+  VS_HIP(pin.alloc(chunk), "pinned staging");
+  // chunk i+1 is copied D2H while chunk i is written
+  const char* src = (const char*)c->data;
+  uint64_t nchunks = (h.data_bytes + chunk - 1) / chunk;
+  if (nchunks)
+    VS_HIP(hipMemcpyAsync(pin.p[0], src, std::min<uint64_t>(chunk, h.data_bytes),
+                          hipMemcpyDeviceToHost, eng->stream),
+           "snapshot D2H");
+  for (uint64_t i = 0; i < nchunks; ++i) {
+    const uint64_t off = i * chunk, n = std::min<uint64_t>(chunk, h.data_bytes - off);
+    VS_HIP(hipStreamSynchronize(eng->stream), "snapshot sync");
+    if (i + 1 < nchunks)
+      VS_HIP(hipMemcpyAsync(pin.p[(i + 1) & 1], src + off + n,
+                            std::min<uint64_t>(chunk, h.data_bytes - off - n),
+                            hipMemcpyDeviceToHost, eng->stream),
+             "snapshot D2H");
+    if (std::fwrite(pin.p[i & 1], 1, n, fc.f) != n) {
+      (void)hipStreamSynchronize(eng->stream);
+      return fail(VS_ERR_IO, "write failed: " + tmp);
+    }
+  }
+  const bool ok = std::fflush(fc.f) == 0 && std::fclose(fc.f) == 0;
+  fc.f = nullptr;
+  if (!ok || std::rename(tmp.c_str(), path) != 0)
+    return fail(VS_ERR_IO, std::string("cannot finish ") + path);
+  return VS_OK;
+}
+
+int vs_restore(vs_engine* eng, const char* coll, const char* path) {
+  if (!eng || !path || !coll || !*coll)
+    return fail(VS_ERR_INVALID_ARG, "engine, collection and path are required");
+  FileCloser fc;
+  fc.f = std::fopen(path, "rb");
+  if (!fc.f) return fail(VS_ERR_IO, std::string("cannot open ") + path);
+  SnapHeader h{};
+  if (std::fread(&h, sizeof(h), 1, fc.f) != 1 || std::memcmp(h.magic, kSnapMagic, 8) != 0 ||
+      h.version != 1 || h.header_bytes != sizeof(SnapHeader) || header_sum(h) != h.header_checksum)
+    return fail(VS_ERR_IO, std::string("not a vsearch snapshot (bad header): ") + path);
+  const uint32_t elem = h.dtype == VS_DTYPE_BF16 ? 2 : 4;
+  if (h.elem_bytes != elem || h.data_bytes != h.rows * h.dim * (uint64_t)elem)
+    return fail(VS_ERR_IO, std::string("inconsistent snapshot header: ") + path);
+  int rc = vs_collection_create(eng, coll, h.dim, h.metric, h.dtype, h.rows, h.row_base);
+  if (rc != VS_OK) return rc;
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_INTERNAL, "restored collection vanished");
+  std::unique_lock<std::shared_mutex> wl(c->mu);
+  uint64_t sum = 0;
+  int err = VS_OK;  // failures are undone after work_mu is released
+  std::string msg;
+  {
+    std::lock_guard<std::mutex> g(eng->work_mu);
+    hipError_t e = set_dev(eng);
+    if (e == hipSuccess) e = use_stream(eng, eng->own);
+    PinnedPair pin;
+    const size_t chunk = std::min<size_t>(kSnapChunk, std::max<size_t>(h.data_bytes, 1));
+    if (e == hipSuccess) e = pin.alloc(chunk);
+    // chunk i is read from disk while chunk i-1 is copied H2D
+    char* dst = (char*)c->data;
+    const uint64_t nchunks = (h.data_bytes + chunk - 1) / chunk;
+    for (uint64_t i = 0; i < nchunks && e == hipSuccess && err == VS_OK; ++i) {
+      const uint64_t off = i * chunk, n = std::min<uint64_t>(chunk, h.data_bytes - off);
+      if (i >= 2) e = hipStreamSynchronize(eng->stream);  // buffer i&1 free again
+      if (e != hipSuccess) break;
+      if (std::fread(pin.p[i & 1], 1, n, fc.f) != n) {
+        err = VS_ERR_IO;
+        msg = std::string("truncated snapshot: ") + path;
+        break;
+      }
+      e = hipMemcpyAsync(dst + off, pin.p[i & 1], n, hipMemcpyHostToDevice, eng->stream);
+    }
+    const hipError_t es = hipStreamSynchronize(eng->stream);  // staging is freed below
+    if (e == hipSuccess) e = es;
+    if (err == VS_OK && e != hipSuccess) {
+      err = VS_ERR_DEVICE;
+      msg = std::string("restore upload: ") + hipGetErrorString(e);
+    }
+    if (err == VS_OK) {
+      c->rows = h.rows;
+      err = device_checksum(eng, *c, &sum);
+      if (err != VS_OK) msg = vs_last_error();
+      else if (sum != h.data_checksum) {
+        err = VS_ERR_IO;
+        msg = std::string("snapshot checksum mismatch: ") + path;
+      }
+    }
+  }
+  wl.unlock();
+  if (err != VS_OK) {
+    (void)vs_collection_drop(eng, coll);
+    return fail(err, msg);
+  }
   return VS_OK;
 }
 

@@ -113,6 +113,9 @@ hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out,
 hipError_t launch_round_bf16(const float* in, uint64_t n, float* out,
                              hipStream_t st);
 
+// Snapshot checksum of nbytes at p (vs::snap_word summed) -> *d_out (device).
+hipError_t launch_checksum(const void* p, uint64_t nbytes, uint64_t* d_out, hipStream_t st);
+
 int device_cu_count();
 
 }  // namespace vsk

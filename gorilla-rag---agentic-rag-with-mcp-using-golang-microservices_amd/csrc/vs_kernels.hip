@@ -170,6 +170,46 @@ hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
   return hipGetLastError();
 }
 
+// Snapshot checksum: HBM-bound streaming reduction, 16-B loads, one 64-bit
+// atomic per wave. Algorithmic bytes = nbytes.
+typedef unsigned u32x4_ck __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void checksum_kernel(const u32x4_ck* __restrict__ p,
+                                                       uint64_t npairs, uint64_t nbytes,
+                                                       uint64_t* __restrict__ out) {
+  uint64_t s = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < npairs; j += stride) {
+    const u32x4_ck v = __builtin_nontemporal_load(p + j);
+    s += vs::snap_word(((uint64_t)v.y << 32) | v.x, 2 * j);
+    s += vs::snap_word(((uint64_t)v.w << 32) | v.z, 2 * j + 1);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // tail: < 16 bytes, words zero-padded
+    const unsigned char* b = (const unsigned char*)p;
+    for (uint64_t w = 2 * npairs; w * 8 < nbytes; ++w) {
+      uint64_t x = 0;
+      for (int i = 0; i < 8 && w * 8 + i < nbytes; ++i) x |= (uint64_t)b[w * 8 + i] << (8 * i);
+      s += vs::snap_word(x, w);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)out, (unsigned long long)s);
+}
+
+hipError_t launch_checksum(const void* p, uint64_t nbytes, uint64_t* d_out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(d_out, 0, 8, st);
+  if (e != hipSuccess || nbytes == 0) return e;
+  if ((uintptr_t)p % 16) return hipErrorInvalidValue;
+  const uint64_t npairs = nbytes / 16;
+  uint64_t blocks = (npairs + 255) / 256;
+  const uint64_t cap = (uint64_t)device_cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const u32x4_ck*)p,
+                     npairs, nbytes, d_out);
+  return hipGetLastError();
+}
+
 // Synthetic unit rows: x_d = m_d / sqrt(sum m^2) with m_d the Irwin-Hall
 // integers of vs::gen_int; the integer sum is exact and order-free, the
 // division and sqrt are correctly rounded fp64 ops, so host and device agree.

@@ -27,6 +27,7 @@ VS_ERR_OOM = -4
 VS_ERR_DEVICE = -5
 VS_ERR_EXISTS = -6
 VS_ERR_INTERNAL = -7
+VS_ERR_IO = -8
 
 METRIC_COSINE = 0
 METRIC_DOT = 1
@@ -43,6 +44,7 @@ EXPORTS = (
     "vs_generate_vectors",
     "vs_read_rows", "vs_search", "vs_search_keys", "vs_merge_keys",
     "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
+    "vs_snapshot", "vs_restore", "vs_checksum",
 )
 
 
@@ -89,6 +91,9 @@ def load_library(path: str = LIB_PATH):
         "vs_health": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "vs_last_error": ([], ctypes.c_char_p),
         "vs_timing": ([vp, vp, vp, vp, vp, i32], i32),
+        "vs_snapshot": ([vp, cp, cp], i32),
+        "vs_restore": ([vp, cp, cp], i32),
+        "vs_checksum": ([vp, cp, ctypes.POINTER(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -193,6 +198,21 @@ class VectorEngine:
                          stream: int = 0):
         _check(self._L.vs_generate_vectors(self._h, seed, row0, n, dim, ctypes.c_void_p(d_out),
                                            ctypes.c_void_p(stream)))
+
+    # snapshot / restore ---------------------------------
+    def snapshot(self, name: str, path: str):
+        """Write the collection's stored rows to `path` (vs_snapshot)."""
+        _check(self._L.vs_snapshot(self._h, name.encode(), os.fsencode(path)))
+
+    def restore(self, name: str, path: str):
+        """Create collection `name` from a snapshot file (vs_restore)."""
+        _check(self._L.vs_restore(self._h, name.encode(), os.fsencode(path)))
+
+    def checksum(self, name: str) -> int:
+        """Device checksum of the stored rows (vs_checksum)."""
+        out = ctypes.c_uint64()
+        _check(self._L.vs_checksum(self._h, name.encode(), ctypes.byref(out)))
+        return out.value
 
     def read_rows(self, name: str, first: int, n: int) -> np.ndarray:
         dim = self.collection_info(name)["dim"]

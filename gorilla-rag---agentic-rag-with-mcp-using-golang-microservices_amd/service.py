@@ -44,6 +44,10 @@ def load_service_library(path: str = SVC_LIB_PATH):
     L.vsvc_bulk_generate.restype = ctypes.c_int
     L.vsvc_point_id.argtypes = [vp, cp, ctypes.c_uint64, cp, sz]
     L.vsvc_point_id.restype = ctypes.c_int
+    L.vsvc_snapshot.argtypes = [vp, cp]
+    L.vsvc_snapshot.restype = ctypes.c_int
+    L.vsvc_restore.argtypes = [vp, cp]
+    L.vsvc_restore.restype = ctypes.c_int
     L.vsvc_stats.argtypes = [vp, ctypes.POINTER(vp)]
     L.vsvc_stats.restype = ctypes.c_int
     L.vsvc_loadgen.argtypes = [vp, cp, ctypes.POINTER(vp)]
@@ -114,6 +118,14 @@ class VectorService:
     def bulk_generate(self, collection: str, n: int, seed: int) -> None:
         """n synthetic device-generated points with synthetic UUIDs (empty collection)."""
         _check(self._L.vsvc_bulk_generate(self._h, collection.encode(), n, seed))
+
+    def snapshot(self, directory: str) -> None:
+        """Save every collection (rows + UUIDs + payloads) under `directory`."""
+        _check(self._L.vsvc_snapshot(self._h, os.fsencode(directory)))
+
+    def restore(self, directory: str) -> None:
+        """Load the collections saved under `directory` (service still empty)."""
+        _check(self._L.vsvc_restore(self._h, os.fsencode(directory)))
 
     def point_id(self, collection: str, row: int) -> str:
         buf = ctypes.create_string_buffer(40)

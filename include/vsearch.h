@@ -63,7 +63,8 @@ typedef enum vs_status {
   VS_ERR_OOM = -4,          /* device or host allocation failed */
   VS_ERR_DEVICE = -5,       /* HIP runtime error, or no usable GPU */
   VS_ERR_EXISTS = -6,       /* collection already exists */
-  VS_ERR_INTERNAL = -7
+  VS_ERR_INTERNAL = -7,
+  VS_ERR_IO = -8            /* snapshot file unreadable, unwritable or corrupt */
 } vs_status;
 
 /* Mirrors qdrant.Distance (main.go:108 uses Distance_Cosine). */
@@ -195,6 +196,29 @@ static inline float vs_key_score(uint64_t key) {
 static inline uint32_t vs_key_row(uint64_t key) {
   return 0xFFFFFFFFu - (uint32_t)key;
 }
+
+/* ---- snapshot / restore --------------------------------- */
+
+/* Replaces Qdrant's persistent volume (docker-compose.yml:9-10,14-15): the
+ * HBM-resident store is otherwise volatile. vs_snapshot writes a collection's
+ * rows, exactly as stored (preprocessed, fp32 or bf16), to `path`:
+ * a 128-byte header (magic "VSNAP01\0", version, dim, metric, dtype,
+ * element bytes, rows, row_base, data bytes, checksum of the data, checksum
+ * of the header) followed by rows x dim elements, row-major, little-endian.
+ * The checksum is vs_checksum's, computed on the device. Concurrent searches
+ * proceed; upserts wait. */
+int vs_snapshot(vs_engine* eng, const char* coll, const char* path);
+
+/* Creates collection `coll` (which must not exist) from a snapshot file,
+ * bit-exact, with capacity for its rows. The data checksum is recomputed on
+ * the device after the upload; on any mismatch or I/O error the collection
+ * is not created and VS_ERR_IO is returned. `row_base` is taken from the file. */
+int vs_restore(vs_engine* eng, const char* coll, const char* path);
+
+/* Checksum of a collection's stored rows (rows x dim elements as stored):
+ * sum over little-endian 64-bit words w_i of splitmix64(w_i ^ i * 0x9E37..15)
+ * mod 2^64 (vs_common.h snap_word; oracle/vsearch_oracle.c restates it). */
+int vs_checksum(vs_engine* eng, const char* coll, uint64_t* out);
 
 /* ---- health / errors / timing -------------------------------------------- */
 

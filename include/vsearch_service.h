@@ -51,6 +51,14 @@ void vsvc_close(vsvc* svc);
  * that row; new ids append after the bulk rows. VS_ERR_EXISTS if the
  * collection already holds points. */
 int vsvc_bulk_generate(vsvc* svc, const char* coll, uint64_t n, uint64_t seed);
+/* Snapshot / restore of the whole service: for every
+ * collection, <dir>/<name>.vsnap (vs_snapshot: the rows) and
+ * <dir>/<name>.points.json (UUIDs, payloads, bulk range). vsvc_restore loads
+ * every collection that has both files into a service whose collections are
+ * still empty (VS_ERR_EXISTS otherwise); a corrupt file leaves that
+ * collection empty and returns VS_ERR_IO. `dir` must exist. */
+int vsvc_snapshot(vsvc* svc, const char* dir);
+int vsvc_restore(vsvc* svc, const char* dir);
 /* The point id (canonical UUID, 36 chars + NUL) of `row` of `coll`. */
 int vsvc_point_id(vsvc* svc, const char* coll, uint64_t row, char* buf, size_t len);
 

@@ -60,6 +60,8 @@ def lib():
         L.oracle_cpu_scan.restype = i32
         L.oracle_f32_to_bf16.argtypes = [ctypes.c_float]
         L.oracle_f32_to_bf16.restype = ctypes.c_uint16
+        L.oracle_checksum.argtypes = [vp, u64]
+        L.oracle_checksum.restype = u64
         _lib = L
     return _lib
 
@@ -133,6 +135,12 @@ def cpu_scan(X_raw: np.ndarray, bf16: bool, Q: np.ndarray, k: int, threads: int 
 
 # --------------------------------------------------------------------------
 # independent numpy restatement (cross-check of the C oracle)
+def checksum(data: bytes) -> int:
+    """Snapshot data checksum (C restatement, vsearch_oracle.c oracle_checksum)."""
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    return int(lib().oracle_checksum(buf, len(data)))
+
+
 # --------------------------------------------------------------------------
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
@@ -253,3 +261,14 @@ def check_topk(dev_scores, dev_rows, dev_count, ref_s64, ref_rows, ref_count, re
         if c and len(set(int(x) for x in dev_rows[i, :c])) != c:
             bad.append(f"q{i}: duplicate rows returned")
     return bad
+
+
+def np_checksum(data: bytes) -> int:
+    """numpy restatement of the snapshot checksum (vectorised over words)."""
+    b = bytes(data)
+    b += b"\0" * (-len(b) % 8)
+    w = np.frombuffer(b, dtype="<u8").astype(np.uint64)
+    with np.errstate(over="ignore"):
+        i = np.arange(w.size, dtype=np.uint64)
+        h = _np_splitmix64(w ^ (i * np.uint64(0x9E3779B97F4A7C15)))
+        return int(np.sum(h, dtype=np.uint64))

@@ -321,3 +321,20 @@ int oracle_cpu_scan(const void* X, int bf16, uint64_t n, uint32_t dim, const flo
   free(cnts);
   return nth;
 }
+
+/* ---- snapshot checksum (include/vsearch.h vs_checksum) ----
+ * Not part of the reference (Qdrant's on-disk format is its own); restated
+ * from this repository's file-format definition: the sum mod 2^64 over the
+ * little-endian 64-bit words w_i of the byte range (last word zero-padded)
+ * of splitmix64(w_i ^ i * 0x9E3779B97F4A7C15). Sequential loop, one word at
+ * a time. */
+uint64_t oracle_checksum(const void* p, uint64_t nbytes) {
+  const unsigned char* b = (const unsigned char*)p;
+  uint64_t s = 0;
+  for (uint64_t w = 0; w * 8 < nbytes; ++w) {
+    uint64_t x = 0;
+    for (int i = 0; i < 8 && w * 8 + i < nbytes; ++i) x |= (uint64_t)b[w * 8 + i] << (8 * i);
+    s += o_splitmix64(x ^ (w * 0x9E3779B97F4A7C15ull));
+  }
+  return s;
+}

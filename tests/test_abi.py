@@ -43,6 +43,21 @@ def test_library_exports_every_declared_symbol(pkg):
     assert sorted(eng_mod.EXPORTS) == decl
 
 
+def test_service_library_exports_every_declared_symbol(pkg):
+    import ctypes
+    from importlib import import_module
+    svc = import_module(pkg.__name__ + ".service")
+    L = svc.load_service_library()
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "vsearch_service.h")).read(),
+                 flags=re.S)
+    names = sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(vsvc_\w+)\s*\(", txt, re.M)))
+    assert {"vsvc_open", "vsvc_handle", "vsvc_snapshot", "vsvc_restore", "vsvc_loadgen",
+            "vsvc_stats", "vsvc_bulk_generate"} <= set(names)
+    for name in names:
+        assert hasattr(L, name), f"{name} not exported"
+    assert isinstance(L, ctypes.CDLL)
+
+
 def test_library_links_only_the_hip_runtime(pkg):
     out = subprocess.run(["ldd", pkg.load_library()._name], capture_output=True, text=True).stdout
     assert "libamdhip64" in out

@@ -205,3 +205,25 @@ def test_check_topk_detects_errors(orc):
     bad_s = s32.copy()
     bad_s[1, 2] *= 1.001
     assert orc.check_topk(bad_s, rows, cnt, s64, rows, cnt, s64, 1e-5)
+
+
+def test_checksum_c_matches_numpy(orc):
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 7, 8, 9, 15, 16, 17, 1000, 4099, 65536 + 3):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert orc.checksum(d) == orc.np_checksum(d), n
+
+
+def test_checksum_known_answers(orc):
+    """Pinned by splitmix64's published outputs: one word w at index 0 hashes
+    to splitmix64(w); splitmix64(1) = 0x910A2DEC89025CC1 (seed-1 first output
+    of Vigna's reference splitmix64.c), splitmix64(0) = 0xE220A8397B1DCDAF."""
+    assert orc.checksum(b"") == 0
+    assert orc.checksum(b"\x01") == 0x910A2DEC89025CC1
+    assert orc.checksum(b"\x00" * 8) == 0xE220A8397B1DCDAF
+    # zero padding of the last word, position dependence, order-free sum
+    assert orc.checksum(b"\x01\x00\x00") == orc.checksum(b"\x01")
+    a, b = b"\x05" * 8, b"\x09" * 8
+    assert orc.checksum(a + b) != orc.checksum(b + a)
+    assert orc.checksum(a + b) == (orc.checksum(a) + orc.checksum(b"\0" * 8 + b)
+                                   - orc.checksum(b"\0" * 8)) % 2 ** 64
