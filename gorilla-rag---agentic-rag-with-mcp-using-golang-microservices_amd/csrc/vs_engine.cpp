@@ -101,6 +101,7 @@ struct vs_engine {
   DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
   DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
   DevBuf scratch8;                  // u64 result of the snapshot checksum
+  DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
   uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
   std::vector<uint64_t> h_keys;
   // timing
@@ -258,7 +259,7 @@ int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
 // Single-query scans (GEMV path) of preprocessed fp32 queries qp[q0 .. q0+n)
 // -> keys d_keys[i * k], one scan + merge per query.
 int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
-                uint64_t* d_keys) {
+                uint64_t* d_keys, const uint64_t* allow = nullptr) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const uint32_t n_rows = (uint32_t)c.rows;
@@ -277,7 +278,7 @@ int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
     uint32_t L = 0;
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_gemv(c.data, bf16, dim, n_rows, row_base, qp + (size_t)i * dim, k,
-                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream),
+                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream, allow),
            "gemv scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -298,7 +299,7 @@ int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
 //     host sync: both launches are no-ops unless the flag is set), the GEMV
 //     path for larger k (after a host check of the flag).
 int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
-                uint64_t* d_keys) {
+                uint64_t* d_keys, const uint64_t* allow) {
   const uint32_t dim = c.dim;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
@@ -310,7 +311,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   // the candidate pass needs the sample bound from a few tiles per workgroup;
   // small collections take the sorted-list pass (k <= 16) or the GEMV path
   const bool fast = tpw >= 8;
-  if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys);
+  if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   const size_t lbytes = (size_t)maxl * PS * std::min(k, vsk::kMfmaListMaxK) * 8;
@@ -349,7 +350,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
       VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
-                                    lists, maxl, &L, eng->stream),
+                                    lists, maxl, &L, eng->stream, allow),
              "mfma scan (lists)");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -362,7 +363,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     uint64_t* skeys = eng->sample_keys.as<uint64_t>();
     VS_HIP(vsk::launch_mfma_sample(X, dim, n_rows, row_base, qb, nv, k, st,
                                    eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), maxl,
-                                   &L, eng->stream),
+                                   &L, eng->stream, allow),
            "mfma sample scan");
     VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, 4 * st,
                               nv, k, skeys, eng->stream, ovf),
@@ -372,7 +373,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
                                  eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(), ovf,
-                                 maxl, &L, eng->stream),
+                                 maxl, &L, eng->stream, allow),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -383,7 +384,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // 3. overflow fallback
     if (k <= vsk::kMfmaListMaxK) {
       VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
-                                    maxl, &L, eng->stream),
+                                    maxl, &L, eng->stream, allow),
              "mfma scan (fallback)");
       VS_HIP(vsk::launch_merge(lists, L, (uint64_t)PS * k, k, nv, k, k, out, eng->stream, ovf,
                                eng->fallbacks.as<uint32_t>()),
@@ -393,7 +394,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, eng->stream), "flag D2H");
       VS_HIP(hipStreamSynchronize(eng->stream), "flag sync");
       if (h_ovf) {
-        int rc = search_gemv(eng, c, qp, q0, nv, k, out);
+        int rc = search_gemv(eng, c, qp, q0, nv, k, out, allow);
         if (rc != VS_OK) return rc;
         eng->host_fallbacks++;
       }
@@ -406,7 +407,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
 int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
-                uint64_t* d_keys) {
+                uint64_t* d_keys, const uint64_t* allow = nullptr) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -440,8 +441,8 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   }
   VS_HIP(vsk::launch_preprocess(d_q, nq, dim, cosine, false, qp, nullptr, 0, eng->stream, qb),
          "query preprocess");
-  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys);
-  return search_gemv(eng, c, qp, 0, nq, k, d_keys);
+  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
+  return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
 }
 
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
@@ -723,9 +724,11 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, f
   return VS_OK;
 }
 
-int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
-              uint32_t dim, uint32_t k, float* out_scores, uint64_t* out_rows,
-              uint32_t* out_count) {
+namespace {
+// vs_search / vs_search_filtered: host queries in, host results out.
+int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+                uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
+                float* out_scores, uint64_t* out_rows, uint32_t* out_count) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
   if (nq == 0) return VS_OK;
@@ -737,19 +740,29 @@ int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t n
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(c->dim) + ", got " + std::to_string(dim));
   std::shared_lock<std::shared_mutex> rl(c->mu);
+  if (allow && allow_words < (c->rows + 63) / 64)
+    return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
+                                        " words, the collection needs " +
+                                        std::to_string((c->rows + 63) / 64));
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(use_stream(eng, eng->own), "stream order");
   const size_t qbytes = (size_t)nq * c->dim * 4;
   const size_t kbytes = (size_t)nq * k * 8;
-  if (eng->q_in.bytes < qbytes || eng->keys.bytes < kbytes) {
+  const size_t abytes = allow ? (size_t)((c->rows + 63) / 64) * 8 : 0;
+  if (eng->q_in.bytes < qbytes || eng->keys.bytes < kbytes || eng->allow.bytes < abytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->q_in.ensure(qbytes), "alloc query input");
     VS_HIP(eng->keys.ensure(kbytes), "alloc keys");
+    VS_HIP(eng->allow.ensure(abytes), "alloc filter bitmap");
   }
   VS_HIP(hipMemcpyAsync(eng->q_in.p, queries, qbytes, hipMemcpyHostToDevice, eng->stream),
          "query H2D");
-  int rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>());
+  if (abytes)
+    VS_HIP(hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream),
+           "filter bitmap H2D");
+  int rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
+                       abytes ? eng->allow.as<uint64_t>() : nullptr);
   if (rc != VS_OK) return rc;
   eng->h_keys.resize((size_t)nq * k);
   VS_HIP(hipMemcpyAsync(eng->h_keys.data(), eng->keys.p, kbytes, hipMemcpyDeviceToHost,
@@ -758,6 +771,22 @@ int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t n
   VS_HIP(hipStreamSynchronize(eng->stream), "search sync");
   decode_host(eng->h_keys.data(), nq, k, out_scores, out_rows, out_count);
   return VS_OK;
+}
+}  // namespace
+
+int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+              uint32_t dim, uint32_t k, float* out_scores, uint64_t* out_rows,
+              uint32_t* out_count) {
+  return search_host(eng, coll, queries, nq, dim, k, nullptr, 0, out_scores, out_rows,
+                     out_count);
+}
+
+int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+                       uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
+                       float* out_scores, uint64_t* out_rows, uint32_t* out_count) {
+  if (!allow) return fail(VS_ERR_INVALID_ARG, "allow bitmap is NULL");
+  return search_host(eng, coll, queries, nq, dim, k, allow, allow_words, out_scores, out_rows,
+                     out_count);
 }
 
 int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uint32_t nq,

@@ -44,7 +44,7 @@ hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
 hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                        uint32_t row_base, const float* q, uint32_t k,
                        uint64_t* out, uint32_t max_lists, uint32_t* nlists,
-                       hipStream_t st);
+                       hipStream_t st, const uint64_t* allow = nullptr);
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 
@@ -65,22 +65,26 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
 //    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; a no-op
 //    unless run_if is null or *run_if != 0.
+// `allow` (nullable, all passes): filter pre-mask, bit r of allow[r / 64]
+// admits local row r; masked rows are never candidates, maxima or results.
 bool mfma_supported(uint32_t dim);
 uint32_t mfma_queries(uint32_t dim);  // queries per launch at this dim
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
-                              uint32_t max_lists, uint32_t* nlists, hipStream_t st);
+                              uint32_t max_lists, uint32_t* nlists, hipStream_t st,
+                              const uint64_t* allow = nullptr);
 hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                             const uint16_t* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
                             uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
-                            uint32_t max_lists, uint32_t* nlists, hipStream_t st);
+                            uint32_t max_lists, uint32_t* nlists, hipStream_t st,
+                            const uint64_t* allow = nullptr);
 hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
-                             uint32_t* nlists, hipStream_t st);
+                             uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
 // Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap] (4
 // quarters, counts cand_cnt[nwg][kMfmaQueries][4]) for queries 0 .. nq-1 ->
 // out[nq][k], sorted, 0-padded.

@@ -296,6 +296,13 @@ constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 constexpr int kGemvVar = 1;
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+// Payload filter pre-mask: bit r of allow[] (local row r)
+// admits the row; a null bitmap admits every row. `r` is wave-uniform, so the
+// word comes through the scalar cache (one 64-row word serves 64 rows).
+__device__ __forceinline__ bool row_allowed(const uint64_t* __restrict__ allow, uint32_t r) {
+  return !allow || ((allow[r >> 6] >> (r & 63)) & 1u);
+}
+
 // Rows of D elements are cut into 16-byte chunks; one wave covers RB whole
 // rows per step with J chunks per lane (RB*CPR == 64*J), so every load is a
 // fully coalesced 1 KiB wave-instruction and each lane's query slice is
@@ -366,8 +373,8 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 template <int D, bool BF16, int KPL, int VAR = kGemvVar>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
-    const float* __restrict__ q, uint32_t k, uint32_t rows_per_wave,
-    uint64_t* __restrict__ out) {
+    const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
+    uint32_t rows_per_wave, uint64_t* __restrict__ out) {
   using S = GemvShape<D, BF16>;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -436,7 +443,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
       for (int b = 0; b < S::RB; ++b) {
         const float s = kDpp ? wave_sum_dpp(p[b]) : wave_sum(p[b]);
         const uint32_t row = r + b;
-        if (row < hi) {
+        if (row < hi && row_allowed(allow, row)) {
           const uint64_t key = make_key(s, row_base + row);
           if (key > theta) {
             L.insert(key, k, lane);
@@ -457,8 +464,8 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
 template <bool BF16, int KPL>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
     const void* __restrict__ Xv, uint32_t dim, uint32_t n_rows, uint32_t row_base,
-    const float* __restrict__ q, uint32_t k, uint32_t rows_per_wave,
-    uint64_t* __restrict__ out) {
+    const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
+    uint32_t rows_per_wave, uint64_t* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
     }
     const float s = wave_sum(p);
     const uint64_t key = make_key(s, row_base + r);
-    if (key > theta) {
+    if (key > theta && row_allowed(allow, r)) {
       L.insert(key, k, lane);
       theta = L.kth(k);
     }
@@ -528,7 +535,8 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k) {
 
 template <int D, bool BF16>
 static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row_base,
-                                    const float* q, uint32_t k, uint64_t* out,
+                                    const float* q, const uint64_t* allow, uint32_t k,
+                                    uint64_t* out,
                                     uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
   using S = GemvShape<D, BF16>;
   GemvGrid g = gemv_grid(n_rows, S::RB);
@@ -539,19 +547,20 @@ static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row
   dim3 grid(g.nwg), block(kGemvThreads);
   if (kpl == 1)
     hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1>), grid, block, 0, st, X, n_rows,
-                       row_base, q, k, g.rows_per_wave, out);
+                       row_base, q, allow, k, g.rows_per_wave, out);
   else if (kpl == 2)
     hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 2>), grid, block, 0, st, X, n_rows,
-                       row_base, q, k, g.rows_per_wave, out);
+                       row_base, q, allow, k, g.rows_per_wave, out);
   else
     hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 16>), grid, block, 0, st, X, n_rows,
-                       row_base, q, k, g.rows_per_wave, out);
+                       row_base, q, allow, k, g.rows_per_wave, out);
   return hipGetLastError();
 }
 
 template <bool BF16>
 static hipError_t gemv_generic(const void* X, uint32_t dim, uint32_t n_rows,
-                               uint32_t row_base, const float* q, uint32_t k,
+                               uint32_t row_base, const float* q, const uint64_t* allow,
+                               uint32_t k,
                                uint64_t* out, uint32_t max_lists, uint32_t* nlists,
                                hipStream_t st) {
   GemvGrid g = gemv_grid(n_rows, 1);
@@ -562,25 +571,26 @@ static hipError_t gemv_generic(const void* X, uint32_t dim, uint32_t n_rows,
   dim3 grid(g.nwg), block(kGemvThreads);
   if (kpl == 1)
     hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 1>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, k, g.rows_per_wave, out);
+                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
   else if (kpl == 2)
     hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 2>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, k, g.rows_per_wave, out);
+                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
   else
     hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 16>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, k, g.rows_per_wave, out);
+                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
   return hipGetLastError();
 }
 
 hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                        uint32_t row_base, const float* q, uint32_t k, uint64_t* out,
-                       uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+                       uint32_t max_lists, uint32_t* nlists, hipStream_t st,
+                       const uint64_t* allow) {
   if (k == 0 || k > kMaxK || n_rows == 0) return hipErrorInvalidValue;
 #define VS_GEMV_CASE(DD)                                                              \
   case DD:                                                                            \
-    return bf16 ? gemv_dispatch_kpl<DD, true>(X, n_rows, row_base, q, k, out,         \
+    return bf16 ? gemv_dispatch_kpl<DD, true>(X, n_rows, row_base, q, allow, k, out,  \
                                               max_lists, nlists, st)                  \
-                : gemv_dispatch_kpl<DD, false>(X, n_rows, row_base, q, k, out,        \
+                : gemv_dispatch_kpl<DD, false>(X, n_rows, row_base, q, allow, k, out, \
                                                max_lists, nlists, st);
   switch (dim) {
     VS_GEMV_CASE(128)
@@ -594,10 +604,10 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
     VS_GEMV_CASE(3072)
     VS_GEMV_CASE(4096)
     default:
-      return bf16 ? gemv_generic<true>(X, dim, n_rows, row_base, q, k, out, max_lists,
-                                       nlists, st)
-                  : gemv_generic<false>(X, dim, n_rows, row_base, q, k, out, max_lists,
-                                        nlists, st);
+      return bf16 ? gemv_generic<true>(X, dim, n_rows, row_base, q, allow, k, out,
+                                       max_lists, nlists, st)
+                  : gemv_generic<false>(X, dim, n_rows, row_base, q, allow, k, out,
+                                        max_lists, nlists, st);
   }
 #undef VS_GEMV_CASE
 }
@@ -660,6 +670,7 @@ struct MfArgs {
   uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys in each quarter
   uint32_t* overflow;       // MODE 0: set to 1 when a buffer would overflow
   const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
+  const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
 };
 
@@ -1038,6 +1049,21 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
     // epilogue: acc[hr][g][i] = score(row trow0 + 16hr + 4kq + i, query ql[g])
     const uint32_t trow0 = wr0 + t * 32;
     const bool full = kPeel ? decltype(full_tag)::value : trow0 + 32 <= wr1;
+    // filter pre-mask: the tile's 32 rows are one half of a 64-row word
+    // (trow0 % 32 == 0); a lane's rows 4kq+i and 16+4kq+i are bits i and 4+i
+    // of am. Masked rows score -inf and never pass.
+    uint32_t am = 0xFFu;
+    if (a.allow) {
+      const uint32_t tw = (uint32_t)(a.allow[trow0 >> 6] >> (trow0 & 32)) >> (4 * kq);
+      am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
+#pragma unroll
+      for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            acc[hr][g][i] = ((am >> (hr * 4 + i)) & 1u) ? acc[hr][g][i] : -INFINITY;
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float mx = -INFINITY;
@@ -1072,7 +1098,8 @@ __global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_k
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const uint32_t row = trow0 + 16 * hr + 4 * kq + i;
-            const bool p = qvalid[g] && (full || row < wr1) && acc[hr][g][i] >= lvl;
+            const bool p = qvalid[g] && (full || row < wr1) && ((am >> (hr * 4 + i)) & 1u) &&
+                           acc[hr][g][i] >= lvl;
             m |= (uint32_t)p << (hr * 4 + i);
           }
         auto key_of = [&](int b) -> uint64_t {
@@ -1197,7 +1224,8 @@ static bool mfma_args_ok(uint32_t dim, uint32_t n_rows, uint32_t nq_valid, uint3
 hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
-                              uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+                              uint32_t max_lists, uint32_t* nlists, hipStream_t st,
+                              const uint64_t* allow) {
   if (!mfma_args_ok(dim, n_rows, nq_valid, k) || max_tiles == 0 || max_tiles > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
@@ -1205,7 +1233,7 @@ hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = 4 * max_tiles;
   a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
-  a.k = k;
+  a.k = k, a.allow = allow;
   return mfma_launch_mode<3>(dim, *nlists, a, st);
 }
 
@@ -1213,13 +1241,14 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
-                             uint32_t* nlists, hipStream_t st) {
+                             uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
   if (!mfma_args_ok(dim, n_rows, nq_valid, k) || k > kMfmaListMaxK) return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.lists = lists;
   a.run_if = run_if, a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
+  a.allow = allow;
   return mfma_launch_mode<8>(dim, *nlists, a, st);
 }
 
@@ -1227,7 +1256,8 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
                             const uint16_t* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
                             uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
-                            uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+                            uint32_t max_lists, uint32_t* nlists, hipStream_t st,
+                            const uint64_t* allow) {
   if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
@@ -1236,7 +1266,7 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = cand;
   a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
-  a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
+  a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
   return mfma_launch_mode<0>(dim, *nlists, a, st);
 }
 

@@ -44,7 +44,7 @@ EXPORTS = (
     "vs_generate_vectors",
     "vs_read_rows", "vs_search", "vs_search_keys", "vs_merge_keys",
     "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
-    "vs_snapshot", "vs_restore", "vs_checksum",
+    "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
 )
 
 
@@ -94,6 +94,7 @@ def load_library(path: str = LIB_PATH):
         "vs_snapshot": ([vp, cp, cp], i32),
         "vs_restore": ([vp, cp, cp], i32),
         "vs_checksum": ([vp, cp, ctypes.POINTER(u64)], i32),
+        "vs_search_filtered": ([vp, cp, vp, u32, u32, u32, vp, u64, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -111,6 +112,14 @@ def _check(rc: int):
     if rc != VS_OK:
         msg = _lib.vs_last_error().decode("utf-8", "replace")
         raise VSError(rc, msg)
+
+
+def pack_allow(mask: np.ndarray) -> np.ndarray:
+    """bool per row -> uint64 words, bit r of word r // 64 (vs_search_filtered)."""
+    m = np.asarray(mask, np.bool_).ravel()
+    pad = np.zeros((-m.size) % 64, np.bool_)
+    bits = np.packbits(np.concatenate([m, pad]), bitorder="little")
+    return bits.view("<u8").astype(np.uint64) if bits.size else np.zeros(0, np.uint64)
 
 
 def device_count() -> int:
@@ -231,6 +240,24 @@ class VectorEngine:
         count = np.zeros(nq, np.uint32)
         _check(self._L.vs_search(self._h, name.encode(), _p(q), nq, q.shape[1], k, _p(scores),
                                  _p(rows), _p(count)))
+        return scores, rows, count
+
+    def search_filtered(self, name: str, queries: np.ndarray, k: int, allow: np.ndarray):
+        """search() restricted to the rows whose bit is set in `allow` (bool per
+        local row, or packed uint64 words: bit r of word r // 64)."""
+        q = np.ascontiguousarray(queries, np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        a = np.asarray(allow)
+        if a.dtype == np.bool_:
+            a = pack_allow(a)
+        a = np.ascontiguousarray(a, np.uint64)
+        nq = q.shape[0]
+        scores = np.zeros((nq, k), np.float32)
+        rows = np.zeros((nq, k), np.uint64)
+        count = np.zeros(nq, np.uint32)
+        _check(self._L.vs_search_filtered(self._h, name.encode(), _p(q), nq, q.shape[1], k,
+                                          _p(a), a.size, _p(scores), _p(rows), _p(count)))
         return scores, rows, count
 
     def search_keys(self, name: str, d_queries: int, nq: int, dim: int, k: int, d_keys: int,

@@ -156,6 +156,17 @@ int vs_search(vs_engine* eng, const char* coll, const float* queries,
               uint32_t nq, uint32_t dim, uint32_t k, float* out_scores,
               uint64_t* out_rows, uint32_t* out_count);
 
+/* vs_search with a payload filter pre-mask: only local
+ * rows r with bit (allow[r / 64] >> (r % 64)) & 1 set can be returned;
+ * out_count[i] = min(k, allowed rows). `allow_words` >= ceil(rows / 64). The
+ * bitmap is applied inside the scan kernels (rows are read but never become
+ * candidates), so a filtered search costs what an unfiltered one does. The
+ * reference accepts `filter` and ignores it (main.go:30 vs :249-254); the
+ * service mirror applies it only when configured to. */
+int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+                       uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
+                       float* out_scores, uint64_t* out_rows, uint32_t* out_count);
+
 /* Device-pointer form for sharded callers. `d_queries` (nq x dim fp32) and
  * `d_keys` (nq x k uint64) are device pointers on this engine's device;
  * `stream` is a hipStream_t (NULL = the null stream). The work is ordered

@@ -1,0 +1,109 @@
+"""Payload filter pre-mask through vs_search_filtered.
+
+The bitmap is applied inside every scan kernel (GEMV, MFMA sample / candidate
+/ sorted-list passes and the overflow fallbacks); the result must be the
+oracle's exact top k over the allowed rows only, with the same (score desc,
+row asc) order.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SCORE_RTOL = 1e-5
+
+
+def _masked_parity(orc, X, Qp, s, r, c, k, mask):
+    idx = np.flatnonzero(mask)
+    s32, s64, rows, cnt = orc.search(np.ascontiguousarray(X[idx]), Qp, k)
+    rows = idx[rows.astype(np.int64)].astype(np.uint64)
+    rows[np.arange(k)[None, :] >= cnt[:, None]] = 0
+    assert np.all(mask[r[c[:, None] > np.arange(k)[None, :]].astype(np.int64)]), "masked row returned"
+    resc = orc.rescore(X, Qp, r, c)
+    bad = orc.check_topk(s, r, c, s64, rows, cnt, resc, SCORE_RTOL)
+    assert not bad, bad[:10]
+
+
+@pytest.fixture(scope="module")
+def fcorpus(engine, orc):
+    n, dim = 200_000, 768
+    engine.create_collection("filt", dim, 0, 1, n)
+    engine.generate("filt", n, orc.SEED_CORPUS)
+    yield "filt", orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+    engine.drop_collection("filt")
+
+
+@pytest.mark.parametrize("density", [0.5, 0.05, 0.002])
+@pytest.mark.parametrize("nq,k", [(1, 10), (256, 10), (300, 16), (64, 100)])
+def test_filtered_search_bf16(engine, orc, fcorpus, density, nq, k):
+    """nq = 1: GEMV; nq >= 2: sample + candidate MFMA passes (k > 16 and a
+    selective mask may overflow into the exact fallbacks)."""
+    name, X = fcorpus
+    rng = np.random.default_rng(int(density * 1e4) + nq + k)
+    mask = rng.random(X.shape[0]) < density
+    Q = orc.generate(orc.SEED_QUERY, 2000 + nq, nq, 768)
+    s, r, c = engine.search_filtered(name, Q, k, mask)
+    assert np.all(c == min(k, int(mask.sum())))
+    _masked_parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k, mask)
+
+
+def test_filter_blocks_and_edges(engine, orc, fcorpus, pkg):
+    name, X = fcorpus
+    n = X.shape[0]
+    Q = orc.generate(orc.SEED_QUERY, 9, 40, 768)
+    # a contiguous block (whole tiles / workgroups masked) plus single rows
+    mask = np.zeros(n, bool)
+    mask[70_000:90_000] = True
+    mask[[0, 31, 32, 63, 64, n - 1]] = True
+    s, r, c = engine.search_filtered(name, Q, 10, mask)
+    _masked_parity(orc, X, orc.preprocess(Q, True, True), s, r, c, 10, mask)
+    # all rows allowed == the unfiltered search, bit for bit
+    a = engine.search(name, Q, 10)
+    b = engine.search_filtered(name, Q, 10, np.ones(n, bool))
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    # nothing allowed: no results
+    for nq in (1, 40):
+        s, r, c = engine.search_filtered(name, Q[:nq], 10, np.zeros(n, bool))
+        assert np.all(c == 0)
+    # fewer allowed rows than k
+    few = np.zeros(n, bool)
+    few[[5, 150_000, 199_999]] = True
+    s, r, c = engine.search_filtered(name, Q, 10, few)
+    assert np.all(c == 3) and set(r[0, :3].tolist()) == {5, 150_000, 199_999}
+    with pytest.raises(pkg.VSError):
+        engine.search_filtered(name, Q, 10, pkg.pack_allow(np.ones(n - 64, bool)))  # too short
+
+
+@pytest.mark.parametrize("dtype,nq", [(0, 1), (0, 7), (1, 33)])
+def test_filtered_small_collections(engine, orc, dtype, nq):
+    """fp32 (GEMV per query) and a small bf16 collection (sorted-list MFMA pass)."""
+    n, dim = 20_000, 768
+    name = f"fsmall_{dtype}"
+    engine.create_collection(name, dim, 0, dtype)
+    engine.generate(name, n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=bool(dtype))
+    mask = np.random.default_rng(3).random(n) < 0.1
+    Q = orc.generate(orc.SEED_QUERY, 77, nq, dim)
+    s, r, c = engine.search_filtered(name, Q, 10, mask)
+    _masked_parity(orc, X, orc.preprocess(Q, True, bool(dtype)), s, r, c, 10, mask)
+    engine.drop_collection(name)
+
+
+def test_filtered_overflow_fallback(engine, orc):
+    """Ties under a mask: the allowed identical rows overflow the candidate
+    buffers; the sorted-list (k <= 16) and GEMV (k > 16) fallbacks must also
+    honour the mask."""
+    n, dim = 70_000, 768
+    base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
+    base[:40_000] = base[12_345]
+    engine.create_collection("fties", dim, 0, 1, n)
+    engine.upsert("fties", np.arange(n), base)
+    X = orc.preprocess(base, True, True)
+    mask = np.ones(n, bool)
+    mask[:20_000:2] = False  # half of the first tied rows are filtered out
+    Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 7, 20, dim)])
+    for k in (10, 50):
+        s, r, c = engine.search_filtered("fties", Q, k, mask)
+        assert r[0].tolist() == [2 * i + 1 for i in range(k)]
+        _masked_parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k, mask)
+    engine.drop_collection("fties")
