@@ -40,6 +40,13 @@ struct CollState {
   std::vector<Json> payload_of;                      // row - bulk -> payload (a decoded map)
 
   uint64_t nrows() const { return bulk + uuid_of.size(); }
+
+  // filter pre-masks (filter mode "match"), cached per canonical filter text
+  // and invalidated by any upsert (version)
+  uint64_t version = 0;
+  std::mutex fmu;
+  std::unordered_map<std::string, std::pair<uint64_t, std::shared_ptr<std::vector<uint64_t>>>>
+      fcache;
 };
 
 // Synthetic UUID of bulk row r: version 4, variant 10, the collection's
@@ -187,6 +194,7 @@ struct SearchRequest {  // main.go:26-31
   std::string collection;
   std::vector<float> query;
   int64_t top_k = 0;
+  Json filter;  // Filter map[string]interface{}: decoded; the reference never uses it
 };
 
 // Returns "" on success, else the decode error.
@@ -238,6 +246,7 @@ std::string decode_search(const char* body, size_t len, SearchRequest* req) {
   if (const Json* f = root.field("filter")) {
     if (f->kind == Json::Object) {
       if (!interface_numbers_ok(*f) && first.empty()) first = "filter: number out of range";
+      req->filter = *f;
     } else if (f->kind != Json::Null && first.empty()) {
       first = "filter: not an object";
     }
@@ -307,6 +316,7 @@ struct vsvc {
   std::unordered_map<std::string, std::shared_ptr<CollState>> colls;
   vsbatch::Options batch_opt;
   std::unique_ptr<vsbatch::Batcher> batcher;  // coalesces concurrent /search (batcher.h)
+  bool filter_match = false;  // "filter":"match": apply SearchRequest.Filter (f-4)
 
   std::shared_ptr<CollState> find(const std::string& name) {
     std::lock_guard<std::mutex> g(mu);
@@ -430,6 +440,7 @@ Response handle_upsert(vsvc* svc, const std::string& method, const char* body, s
     cs->uuid_of[rows[i] - cs->bulk] = canon[i];
     cs->payload_of[rows[i] - cs->bulk] = payloads[i];
   }
+  ++cs->version;  // cached filter masks are stale
   wl.unlock();
 
   Json o = Json::object();
@@ -443,6 +454,68 @@ Response handle_upsert(vsvc* svc, const std::string& method, const char* body, s
 }
 
 // searchHandler (main.go:227-278)
+// JSON value equality as Go's reflect.DeepEqual sees decoded interface{}
+// values: numbers as float64, objects as maps (key order free).
+bool json_equal(const Json& a, const Json& b) {
+  if (a.kind != b.kind) return false;
+  switch (a.kind) {
+    case Json::Null: return true;
+    case Json::Bool: return a.b == b.b;
+    case Json::Number: return a.num == b.num;
+    case Json::String: return a.str == b.str;
+    case Json::Array:
+      if (a.arr.size() != b.arr.size()) return false;
+      for (size_t i = 0; i < a.arr.size(); ++i)
+        if (!json_equal(a.arr[i], b.arr[i])) return false;
+      return true;
+    case Json::Object: {
+      size_t n = 0;
+      for (const auto& kv : a.obj) {
+        const Json* o = b.get(kv.first);
+        if (!o || !json_equal(*a.get(kv.first), *o)) return false;
+      }
+      for (const auto& kv : b.obj) n += a.get(kv.first) != nullptr;
+      return n == b.obj.size();
+    }
+  }
+  return false;
+}
+
+// A point matches a filter when its payload holds every filter key with an
+// equal value (a conjunction of exact matches, as retrieval-service's
+// map[string]string filters read).
+bool payload_matches(const Json& payload, const Json& filter) {
+  for (const auto& kv : filter.obj) {
+    const Json* v = payload.kind == Json::Object ? payload.get(kv.first) : nullptr;
+    if (!v || !json_equal(*v, *filter.get(kv.first))) return false;
+  }
+  return true;
+}
+
+// Allow bitmap of `filter` over cs's rows (reader lock held by the caller).
+std::shared_ptr<std::vector<uint64_t>> filter_mask(CollState& cs, const Json& filter) {
+  std::string key;
+  vsjson::encode(filter, &key);  // canonical: sorted keys
+  {
+    std::lock_guard<std::mutex> g(cs.fmu);
+    auto it = cs.fcache.find(key);
+    if (it != cs.fcache.end() && it->second.first == cs.version) return it->second.second;
+  }
+  const uint64_t n = cs.nrows();
+  auto m = std::make_shared<std::vector<uint64_t>>((n + 63) / 64, 0);
+  for (const auto& kv : cs.bulk_payload)  // other bulk rows have empty payloads
+    if (payload_matches(kv.second, filter)) (*m)[kv.first >> 6] |= 1ull << (kv.first & 63);
+  for (uint64_t i = 0; i < cs.payload_of.size(); ++i)
+    if (payload_matches(cs.payload_of[i], filter)) {
+      const uint64_t r = cs.bulk + i;
+      (*m)[r >> 6] |= 1ull << (r & 63);
+    }
+  std::lock_guard<std::mutex> g(cs.fmu);
+  if (cs.fcache.size() >= 64) cs.fcache.clear();
+  cs.fcache[key] = {cs.version, m};
+  return m;
+}
+
 Response handle_search(vsvc* svc, const std::string& method, const char* body, size_t len) {
   if (method != "POST") return error_text("Method not allowed", 405);
   SearchRequest req;
@@ -470,7 +543,14 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   // reply is encoded, so rows and UUIDs cannot change underneath.
   int rc;
   std::string err;
-  if (svc->batcher) {
+  if (svc->filter_match && req.filter.kind == Json::Object && !req.filter.obj.empty()) {
+    // filtered searches carry their own mask: one engine call each
+    auto mask = filter_mask(*cs, req.filter);
+    rc = vs_search_filtered(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
+                            (uint32_t)k, mask->data(), mask->size(), scores.data(),
+                            hit_rows.data(), &count);
+    if (rc != VS_OK) err = last_error();
+  } else if (svc->batcher) {
     rc = svc->batcher->search(req.collection, req.query.data(), cs->dim, (uint32_t)k,
                               scores.data(), hit_rows.data(), &count, &err);
   } else {
@@ -525,6 +605,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
   };
   std::vector<Spec> specs;
   vsbatch::Options bopt;
+  bool filter_match = false;
   if (!config_json) {
     for (const char* n : {"regulatory_docs", "merchant_docs", "kyc_docs"})
       specs.push_back({n, 768, VS_METRIC_COSINE, VS_DTYPE_F32});
@@ -547,6 +628,12 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
       if (dt && dt->kind == Json::String && dt->str == "bf16") s.dtype = VS_DTYPE_BF16;
       specs.push_back(s);
     }
+    // {"filter": "ignore" (the reference: main.go:30 vs :249-254) | "match"}
+    if (const Json* fm = cfg.get("filter")) {
+      if (fm->kind != Json::String || (fm->str != "ignore" && fm->str != "match"))
+        return VS_ERR_INVALID_ARG;
+      filter_match = fm->str == "match";
+    }
     // {"batching": {"enabled": bool, "max_batch": n, "max_wait_us": n}}
     if (const Json* b = cfg.get("batching")) {
       if (b->kind != Json::Object) return VS_ERR_INVALID_ARG;
@@ -567,6 +654,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
   auto svc = std::make_unique<vsvc>();
   svc->eng = eng;
   svc->batch_opt = bopt;
+  svc->filter_match = filter_match;
   for (const auto& s : specs) {
     // initializeCollections: Get, and Create when NotFound (main.go:91-112)
     uint32_t dim = 0;
@@ -605,6 +693,7 @@ int vsvc_bulk_generate(vsvc* svc, const char* coll, uint64_t n, uint64_t seed) {
   h = (h ^ (h >> 31)) * 0xBF58476D1CE4E5B9ull;
   cs->bulk_tag = ((h ^ (h >> 29)) & 0xFFFFFFFFFFFFull) | 1u;
   cs->bulk = n;
+  ++cs->version;
   return VS_OK;
 }
 
@@ -702,6 +791,7 @@ int vsvc_restore(vsvc* svc, const char* dir) {
       cs->uuid_of.push_back(e.arr[0].str);
       cs->payload_of.push_back(e.arr[1]);
     }
+    ++cs->version;
   }
   return VS_OK;
 }

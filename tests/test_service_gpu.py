@@ -320,3 +320,53 @@ def test_bulk_generate_ids_and_overwrite(batch_service, orc):
     assert got == {new, s.point_id("b16", 7)}
     with pytest.raises(Exception):
         s.bulk_generate("b16", 10, 1)  # only into an empty collection
+
+
+def test_filter_modes(pkg, svcmod, orc):
+    """Default "ignore": `filter` is decoded and dropped, as the reference does.
+    "match": only points whose payload equals every filter entry are eligible
+    (the pre-mask runs inside the scan); cached masks follow upserts."""
+    n, dim = 3000, 768
+    X = orc.generate(41, 0, n, dim)
+    ids = _ids(n, seed=41)
+    docs = ["doc-a", "doc-b", "doc-c"]
+    pts = [{"id": ids[i], "vector": X[i].tolist(),
+            "payload": {"document_id": docs[i % 3], "lang": "en" if i % 2 else "de", "n": i % 5}}
+           for i in range(n)]
+    Xp = orc.preprocess(X, True, True)
+    Q = orc.generate(orc.SEED_QUERY, 41, 6, dim)
+    for mode in ("ignore", "match"):
+        eng = pkg.VectorEngine(device=0)
+        s = svcmod.VectorService(eng, {"collections": [{"name": "c", "dim": dim, "dtype": "bf16"}],
+                                       "filter": mode})
+        try:
+            for lo in range(0, n, 1000):
+                assert _post(s, "/upsert", {"collection": "c", "points": pts[lo:lo + 1000]})[0] == 200
+            for flt, pred in (({"document_id": "doc-b"}, lambda i: i % 3 == 1),
+                              ({"document_id": "doc-a", "lang": "en"}, lambda i: i % 6 == 3),
+                              ({"n": 2}, lambda i: i % 5 == 2),          # number: float64 equality
+                              ({"n": "2"}, lambda i: False),             # string != number
+                              ({}, lambda i: True)):
+                mask = np.array([pred(i) or mode == "ignore" for i in range(n)])
+                for qi in range(len(Q)):
+                    st, body, _ = _post(s, "/search", {"collection": "c", "query": Q[qi].tolist(),
+                                                       "top_k": 8, "filter": flt})
+                    assert st == 200, body
+                    res = json.loads(body)["results"]
+                    rows = [ids.index(r["id"]) for r in res]
+                    idx = np.flatnonzero(mask)
+                    qp = orc.preprocess(Q[qi:qi + 1], True, True)
+                    s32, s64, rr, cc = orc.search(np.ascontiguousarray(Xp[idx]), qp, 8)
+                    exp = idx[rr[0, :cc[0]].astype(np.int64)].tolist()
+                    assert rows == exp, (mode, flt, qi)
+            if mode == "match":  # payload change -> the cached doc-b mask must not be reused
+                assert _post(s, "/upsert", {"collection": "c", "points": [
+                    {"id": ids[0], "vector": X[0].tolist(), "payload": {"document_id": "doc-b"}}]})[0] == 200
+                st, body, _ = _post(s, "/search", {"collection": "c", "query": X[0].tolist(),
+                                                   "top_k": 1, "filter": {"document_id": "doc-b"}})
+                assert json.loads(body)["results"][0]["id"] == ids[0]
+        finally:
+            s.close()
+            eng.close()
+    with pytest.raises(Exception):
+        svcmod.VectorService(pkg.VectorEngine(device=0), {"collections": [], "filter": "maybe"})
