@@ -1,0 +1,43 @@
+"""Builds profiles/pmc_traffic.json from rocprofv3 --pmc FETCH_SIZE runs of bench.py.
+
+    python tools/pmc_traffic.py TAG c3=gpurun_out/pmc_c3/run_counter_collection.csv \
+        c3b1=... c2=...
+
+HBM bytes per launch = FETCH_SIZE (KB) x 1024 x 2 (the gfx950 correction,
+MI355X_MICROARCH.md HBM/rocprofv3 section), averaged over the scan kernel's
+launches (the MFMA main pass for batched configs, the GEMV scan for B = 1).
+"""
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCAN = {"c3": "mfma_topk_kernel<768, 0,", "c3b1": "gemv_topk_kernel<768, true, 1",
+        "c2": "gemv_topk_kernel<768, false, 1", "c4": "mfma_topk_kernel<768, 0,",
+        "c4b1": "gemv_topk_kernel<768, true, 16"}
+
+
+def main():
+    tag, specs = sys.argv[1], sys.argv[2:]
+    out = {"_doc": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (KB, x1024, x2 gfx950 "
+                   "correction: MI355X_MICROARCH.md HBM section), averaged over the scan launches "
+                   "of `python bench.py --config <cfg> --steps 5 --warmup 1`; build " + tag}
+    for spec in specs:
+        cfg, path = spec.split("=", 1)
+        vals, name = [], None
+        for r in csv.DictReader(open(path)):
+            if SCAN[cfg] in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                vals.append(float(r["Counter_Value"]))
+                name = r["Kernel_Name"].split("(")[0].replace("void vsk::", "")
+        if not vals:
+            raise SystemExit(f"no FETCH_SIZE rows for {SCAN[cfg]} in {path}")
+        kb = sum(vals) / len(vals)
+        out[cfg] = {"kernel": name, "launches": len(vals), "fetch_size_kb_avg": round(kb, 1),
+                    "hbm_bytes_per_launch": int(kb * 1024 * 2)}
+    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
