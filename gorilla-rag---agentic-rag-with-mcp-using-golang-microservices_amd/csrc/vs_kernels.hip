@@ -826,11 +826,12 @@ struct MfShape {
 // the chunk's LDS-DMA pieces spread over its steps instead of at its head;
 // VAR 1024: non-temporal (nt) LDS-DMA loads of the corpus stream.
 template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D)>
-__global__ __launch_bounds__(64 * mf_waves(G), 8 / mf_waves(G)) void mfma_topk_kernel(
+__global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
   constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
   static_assert(WAVES * QPW <= (int)kMfmaQueries, "one launch covers <= kMfmaQueries");
-  static_assert(G * (D / 32) * 4 <= 192, "B fragments must fit the register budget");
+  static_assert(G * (D / 32) * 4 <= (mf_waves(G) == 4 ? 400 : 192),
+                "B fragments must fit the register budget");
   // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
   // VAR 2048 / 4096: 24 / 48 KiB K-chunks (384 / 768 k of 32 rows) at D = 768

@@ -103,11 +103,14 @@ int main(int argc, char** argv) {
   // gained what the sample pass lost (argv[3] overrides the sample tiles).
   // 24 / 48 KiB K-chunks (VAR 2048 / 4096, + 256 for the 144 KiB ring) were
   // slower than 16 KiB at 10M rows (3.64-3.67 vs 3.48 ms); kept as arms.
+  // G = 4 (4 waves x 64 queries, one wave per SIMD, 512 registers): no
+  // epilogue 4.23 ms, 3.74 with a 2-step fragment prefetch, 3.60 with a pinned
+  // 3-step one, vs 3.35 for G = 2 (10M rows, r01).
   std::vector<Arm> arms = {
       {"main cand", run<0, 0, 2>, true, {}},
-      {"main 24K big", run<0, 2048 + 256, 2>, true, {}},
-      {"dma-only", run<2, 0, 2>, false, {}},
       {"no-epilogue", run<1, 0, 2>, false, {}},
+      {"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}},
+      {"dma-only", run<2, 0, 2>, false, {}},
   };
   for (int r = 0; r < reps; ++r)
     for (auto& arm : arms) arm.t.push_back(arm.fn(c, arm.bound));
