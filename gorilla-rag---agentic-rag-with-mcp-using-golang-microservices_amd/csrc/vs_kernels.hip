@@ -836,20 +836,29 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
   // VAR 2048 / 4096: 24 / 48 KiB K-chunks (384 / 768 k of 32 rows) at D = 768
   constexpr int kCsx = (VAR & 4096) ? 12 : ((VAR & 2048) ? 6 : 0);
+  // candidate passes keep each lane's per-group append counters in LDS (a
+  // register each would push the kernel past 256 VGPRs, and the compiler
+  // then drops the A-fragment prefetch of the streaming loop: r01)
+  constexpr int kCntBytes = (MODE == 0 || MODE == 3) ? 64 * WAVES * G * 4 : 0;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
-                    MODE == 8 ? kMfListBytes : 16, WAVES, kCsx>;
+                    MODE == 8 ? kMfListBytes : 16 + kCntBytes, WAVES, kCsx>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 8;
   constexpr bool kCand = MODE == 0 || MODE == 3;
   constexpr int PPW = S::PPW;
   constexpr int kPD0 = (VAR & 64) ? 3 : ((VAR & 32) ? 2 : 1);
   constexpr int kPD = ((S::CPT * S::CT) % (kPD0 + 1) == 0) ? kPD0 : 1;
-  constexpr bool kPin = (VAR & 128) != 0;  // keep each step's reads + MFMAs in program order
+  // each step's fragment reads + MFMAs kept in program order, so the one-step
+  // prefetch survives scheduling (3.38 vs 3.63 ms at 10M rows); the sorted-list
+  // pass would spill with it
+  constexpr bool kPin = (VAR & 128) != 0 || MODE != 8;
   if (a.run_if && *a.run_if == 0) return;  // fallback launch with nothing to redo
   // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
   lds_vu64_t* lists = (lds_vu64_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES);
+  typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32_t;
+  lds_vu32_t* cntl = (lds_vu32_t*)(lds_ptr_t)(smem + S::NSLOT * S::CHUNK_BYTES + 16);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -871,10 +880,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   uint32_t ql[G];
   bool qvalid[G];
   float th_s[G];     // admit rows whose score reaches th_s
-  uint32_t cnt[G];   // keys this lane appended to its quarter of the query's buffer
+  // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
+  // query's buffer (candidate passes)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    cnt[g] = 0;
+    if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
     ql[g] = (uint32_t)(w * QPW + g * 16 + col);
     qvalid[g] = ql[g] < a.nq_valid;
     const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
@@ -943,6 +953,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // does not place vmcnt waits for them inside the loop, where the hardware
   // counter also holds the ring's LDS-DMA pieces (invisible to the pass).
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
+  if constexpr (MODE == 12) {  // ablation: the prologue's query-fragment loads only
+#pragma unroll
+    for (int g = 0; g < G; ++g) asm volatile("" ::"v"(qf[g][0]), "v"(qf[g][S::T - 1]));
+    return;
+  }
   __syncthreads();  // lists / counts initialised
   if constexpr (kDma)
     for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
@@ -1114,15 +1129,21 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           // lane-private quarter of the buffer: no atomics, fire-and-forget stores
           const uint32_t n = (uint32_t)__popc(m);
           const uint32_t sub = a.cand_cap >> 2;
+          const uint32_t cg = n ? cntl[g * THREADS + threadIdx.x] : 0u;
           if (n) {
-            if (cnt[g] + n > sub) {
+            if (cg + n > sub) {
               // main pass: the caller re-runs the batch exactly; sample pass:
               // dropping tile maxima only lowers the bound (still valid)
               if constexpr (MODE == 0) *a.overflow = 1u;
             } else {
-              uint64_t* dst = a.cand + ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * a.cand_cap +
-                              (uint32_t)kq * sub + cnt[g];
-              cnt[g] += n;
+              // the address is rebuilt here from an opaque thread id, so none
+              // of it is hoisted out of the tile loop (its register budget)
+              uint32_t tid = threadIdx.x;
+              asm volatile("" : "+v"(tid));
+              const uint32_t qo = (tid >> 6) * QPW + g * 16 + (tid & 15);
+              uint64_t* dst = a.cand + ((size_t)blockIdx.x * kMfmaQueries + qo) * a.cand_cap +
+                              ((tid & 63) >> 4) * sub + cg;
+              cntl[g * THREADS + threadIdx.x] = cg + n;
               while (m) {
                 const int b = __builtin_ctz(m);
                 m &= m - 1;
@@ -1148,7 +1169,8 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if constexpr (kCand) {
-      a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] = cnt[g];
+      a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
+          cntl[g * THREADS + threadIdx.x];
     } else if constexpr (kLists) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {

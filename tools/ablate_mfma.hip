@@ -109,8 +109,10 @@ int main(int argc, char** argv) {
   std::vector<Arm> arms = {
       {"main cand", run<0, 0, 2>, true, {}},
       {"no-epilogue", run<1, 0, 2>, false, {}},
-      {"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}},
+      {"max-only (6)", run<6, 0, 2>, true, {}},
       {"dma-only", run<2, 0, 2>, false, {}},
+      {"qf-only", run<12, 0, 2>, false, {}},
+      {"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}},
   };
   for (int r = 0; r < reps; ++r)
     for (auto& arm : arms) arm.t.push_back(arm.fn(c, arm.bound));
