@@ -316,7 +316,9 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   const size_t lbytes = (size_t)maxl * PS * std::min(k, vsk::kMfmaListMaxK) * 8;
   const size_t sbytes = (size_t)PS * k * 8;
-  const size_t cbytes = (size_t)maxl * PS * cap * 8;
+  // main pass slabs: 32 B of scores + a 4-B tile row per slot
+  const size_t sl_bytes = (size_t)maxl * PS * cap * 32;
+  const size_t cbytes = sl_bytes + (size_t)maxl * PS * cap * 4;
   const size_t scbytes = (size_t)maxl * PS * 4 * st * 8;
   const size_t nbytes = (size_t)maxl * PS * 4 * 4;
   if (eng->lists.bytes < lbytes || eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
@@ -371,14 +373,16 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     const uint64_t* init = skeys + (k - 1);
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-    VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k,
-                                 eng->cand.as<uint64_t>(), cap, eng->cand_cnt.as<uint32_t>(), ovf,
-                                 maxl, &L, eng->stream, allow),
+    float* slabs = eng->cand.as<float>();
+    uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + sl_bytes);
+    VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k, slabs, slab_tile,
+                                 cap, eng->cand_cnt.as<uint32_t>(), ovf, maxl, &L, eng->stream,
+                                 allow),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-    VS_HIP(vsk::launch_select(eng->cand.as<uint64_t>(), eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                              k, out, eng->stream),
+    VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
+                                    k, out, eng->stream, row_base, allow),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
     // 3. overflow fallback

@@ -57,9 +57,13 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //    with counts cand_cnt; launch_select(.., cap = 4 * max_tiles, k, ..) then
 //    gives per query the top k of those maxima, whose k-th key lower-bounds
 //    the global k-th key;
-//  * main pass: every row, survivors of the per-query lower bound
-//    init_th[q * init_stride] appended to cand[nlists][kMfmaQueries][cap]
-//    (cap % 4 == 0: quarter j is lane j's, counts cand_cnt[nlists][256][4]);
+//  * main pass: every row; a lane whose 8 scores of a tile reach the
+//    per-query lower bound init_th[q * init_stride] appends them as one slab
+//    (8 f32, the accumulator layout) and the tile's first global row to the
+//    query's buffer: slabs[nlists][kMfmaQueries][cap][8] and
+//    slab_tile[nlists][kMfmaQueries][cap] (cap % 4 == 0: quarter j of a
+//    buffer is lane j's, counts in slabs cand_cnt[nlists][256][4]);
+//    launch_select_slabs picks the top k;
 //    sets *overflow = 1 when a quarter would overflow (the caller then
 //    redoes the batch exactly: lists pass or GEMV);
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
@@ -76,10 +80,10 @@ hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                               const uint64_t* allow = nullptr);
 hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                             const uint16_t* Q, uint32_t nq_valid, uint32_t k,
-                            const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
-                            uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
-                            uint32_t max_lists, uint32_t* nlists, hipStream_t st,
-                            const uint64_t* allow = nullptr);
+                            const uint64_t* init_th, uint32_t init_stride, float* slabs,
+                            uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
+                            uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
+                            hipStream_t st, const uint64_t* allow = nullptr);
 hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
@@ -93,6 +97,13 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
                          uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
                          uint32_t* clear = nullptr);
+// The same over the main pass's slab buffers (see launch_mfma_cand); the
+// main pass leaves masked rows in its slabs, so the select applies the same
+// pre-mask `allow` (local rows = global - row_base).
+hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
+                               const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
+                               uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,
+                               const uint64_t* allow = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows);

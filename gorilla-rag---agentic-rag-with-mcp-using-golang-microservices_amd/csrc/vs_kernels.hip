@@ -665,9 +665,11 @@ struct MfArgs {
   const uint16_t* Q;        // kMfmaQueries x D bf16 (zero-padded)
   const uint64_t* init_th;  // nullable: per-query lower-bound keys at [q * init_stride]
   uint64_t* lists;          // MODE 3 / 8: [nwg][kMfmaQueries][k] sorted keys
-  uint64_t* cand;           // MODE 0 / 3: [nwg][kMfmaQueries][cand_cap] unsorted keys;
+  uint64_t* cand;           // MODE 3: [nwg][kMfmaQueries][cand_cap] unsorted keys; MODE 0:
+                            // [nwg][kMfmaQueries][cand_cap] slabs of 8 f32 scores (32 B);
                             // quarter kq of a query's buffer belongs to its lane kq
-  uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys in each quarter
+  uint32_t* cand_tile;      // MODE 0: first global row of each slab's tile
+  uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys / slabs per quarter
   uint32_t* overflow;       // MODE 0: set to 1 when a buffer would overflow
   const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
@@ -1072,18 +1074,33 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     if (a.allow) {
       const uint32_t tw = (uint32_t)(a.allow[trow0 >> 6] >> (trow0 & 32)) >> (4 * kq);
       am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
+      // the main pass leaves its accumulators as they are (the slab's masked
+      // rows are dropped by the select, which reads the same mask): a
+      // conditional rewrite here costs a copy of all 16 every tile
+      if constexpr (MODE != 0) {
 #pragma unroll
-      for (int hr = 0; hr < 2; ++hr)
+        for (int hr = 0; hr < 2; ++hr)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int g = 0; g < G; ++g)
-            acc[hr][g][i] = ((am >> (hr * 4 + i)) & 1u) ? acc[hr][g][i] : -INFINITY;
+            for (int g = 0; g < G; ++g)
+              acc[hr][g][i] = ((am >> (hr * 4 + i)) & 1u) ? acc[hr][g][i] : -INFINITY;
+      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float mx = -INFINITY;
-      if (full) {
+      if (MODE == 0 && full && a.allow) {
+        // the mask bits are taken opaque inside the branch, so their tests
+        // are not hoisted into every unfiltered tile
+        uint32_t amv = am;
+        asm volatile("" : "+v"(amv));
+        float v[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          v[b] = ((amv >> b) & 1u) ? acc[b >> 2][g][b & 3] : -INFINITY;
+        mx = fmax3(fmax3(v[0], v[1], v[2]), fmax3(v[3], v[4], v[5]), fmax3(v[6], v[7], -INFINITY));
+      } else if (full) {
         mx = fmax3(fmax3(acc[0][g][0], acc[0][g][1], acc[0][g][2]),
                    fmax3(acc[0][g][3], acc[1][g][0], acc[1][g][1]),
                    fmax3(acc[1][g][2], acc[1][g][3], -INFINITY));
@@ -1093,8 +1110,43 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const uint32_t row = trow0 + 16 * hr + 4 * kq + i;
+            if constexpr (MODE == 0) {  // padding / masked rows leave the slab as -inf
+              if (row >= wr1 || !((am >> (hr * 4 + i)) & 1u)) acc[hr][g][i] = -INFINITY;
+            }
             if (row < wr1 && acc[hr][g][i] > mx) mx = acc[hr][g][i];
           }
+      }
+      if constexpr (MODE == 0) {
+        // Main pass: a lane whose max reaches the bound appends its whole
+        // 8-score slab (the two accumulators as they are) and the tile's first
+        // row to its quarter of the query's buffer; select_cand_kernel expands
+        // slabs into keys. No per-row mask, key packing or loop here: the rare
+        // path is a few instructions, and any wave in it holds up the other
+        // seven at the next chunk barrier (r01: -0.12 ms at 1.25M rows).
+        if (qvalid[g] && mx >= th_s[g] && mx != -INFINITY) {
+          const uint32_t sub = a.cand_cap >> 2;
+          const uint32_t cg = cntl[g * THREADS + threadIdx.x];
+          if (cg >= sub) {
+            *a.overflow = 1u;  // the caller re-runs the batch exactly
+          } else {
+            // the address is rebuilt here from an opaque thread id, so none
+            // of it is hoisted out of the tile loop (its register budget)
+            uint32_t tid = threadIdx.x;
+            asm volatile("" : "+v"(tid));
+            // layout [wg][query][cap], a quarter = sub slots: a workgroup's
+            // stores stay in its own region (a query-major layout spread each
+            // wave's stores over 16 regions 0.5 MiB apart: +4% main pass, r01)
+            const uint32_t qo = (tid >> 6) * QPW + g * 16 + (tid & 15);
+            const size_t slot = ((size_t)blockIdx.x * kMfmaQueries + qo) * a.cand_cap +
+                                ((tid & 63) >> 4) * sub + cg;
+            f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
+            sp[0] = acc[0][g];
+            sp[1] = acc[1][g];
+            a.cand_tile[slot] = a.row_base + trow0;
+            cntl[g * THREADS + threadIdx.x] = cg + 1;
+          }
+        }
+        continue;
       }
       // sample pass: one candidate per (tile, query), the tile maximum
       float lvl = th_s[g];
@@ -1277,18 +1329,18 @@ hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
 
 hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                             const uint16_t* Q, uint32_t nq_valid, uint32_t k,
-                            const uint64_t* init_th, uint32_t init_stride, uint64_t* cand,
-                            uint32_t cand_cap, uint32_t* cand_cnt, uint32_t* overflow,
-                            uint32_t max_lists, uint32_t* nlists, hipStream_t st,
-                            const uint64_t* allow) {
+                            const uint64_t* init_th, uint32_t init_stride, float* slabs,
+                            uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
+                            uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
+                            hipStream_t st, const uint64_t* allow) {
   if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = cand;
-  a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
+  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = (uint64_t*)slabs;
+  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
   return mfma_launch_mode<0>(dim, *nlists, a, st);
 }
@@ -1307,11 +1359,13 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
 }
 
 uint32_t mfma_sample_tiles(uint32_t n_rows) {
-  // 1/64 of every workgroup's tiles. (A floor of 8 tiles for small shards cut
-  // the survivors 4x at 1.25M rows but cost more in the sample pass than it
-  // saved in the main pass's epilogue: measured, r01.)
+  // 1/64 of every workgroup's tiles, at least 4 when it has 64 or more: with
+  // the slab select, whose cost grows with the survivors, 4 instead of 2
+  // tiles at 1.25M rows (the N = 8 share) saved 2-3 us per batch (r01; the
+  // key-based select of earlier builds gained nothing from it).
   const uint32_t tpw = mfma_tiles_per_wg(n_rows);
   uint32_t st = tpw / 64;
+  if (tpw >= 64 && st < 4) st = 4;
   if (st < 1) st = 1;
   if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;
   return st;
@@ -1350,6 +1404,41 @@ __device__ __forceinline__ void bitonic_sort_desc_n(uint64_t* buf, int n_pow2, i
   }
 }
 
+// Bitonic sort of one u64 per lane across a wave, descending (lane 0 gets
+// the largest): 21 shuffle stages, no LDS, no barrier.
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t x, int lane) {
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint32_t lo = __shfl_xor((unsigned)(uint32_t)x, stride, 64);
+      const uint32_t hi = __shfl_xor((unsigned)(uint32_t)(x >> 32), stride, 64);
+      const uint64_t y = ((uint64_t)hi << 32) | lo;
+      const bool keep_max = ((lane & stride) == 0) == ((lane & size) == 0);
+      x = keep_max ? (x > y ? x : y) : (x < y ? x : y);
+    }
+  return x;
+}
+
+// First bound of a select, for k <= 64: the k-th largest of the 64 maxima of
+// 4 consecutive per-buffer maxima lmax[0, 256) (k keys of k distinct rows
+// reach it, so it is <= the k-th largest of all 256 and of the result).
+// Wave 0 computes it; the caller publishes it with a barrier.
+__device__ __forceinline__ uint64_t sel_bound_wave(const uint64_t* lmax, uint32_t k, int lane) {
+  const uint64_t* g4 = lmax + 4 * lane;
+  const uint64_t a = g4[0] > g4[1] ? g4[0] : g4[1], b = g4[2] > g4[3] ? g4[2] : g4[3];
+  const uint64_t g = wave_sort_desc(a > b ? a : b, lane);
+  return shfl64(g, (int)k - 1);
+}
+
+// Final top k of c <= 64 keys in buf by wave 0 alone: sorted in registers and
+// written out (0-padded to k <= kMfmaMaxK).
+__device__ __forceinline__ void sel_finish_wave(const uint64_t* buf, uint32_t c, uint32_t k,
+                                                int lane, uint64_t* out) {
+  const uint64_t x = wave_sort_desc((uint32_t)lane < c ? buf[lane] : 0ull, lane);
+  for (uint32_t j = (uint32_t)lane; j < k; j += 64) out[j] = j < 64 ? x : 0ull;
+}
+
 // max (or filtered append) over one quarter list, 4 loads in flight
 template <bool APPEND>
 __device__ __forceinline__ uint64_t sel_scan_quarter(const uint64_t* __restrict__ p, uint32_t c,
@@ -1375,6 +1464,28 @@ __device__ __forceinline__ uint64_t sel_scan_quarter(const uint64_t* __restrict_
   return m;
 }
 
+// Main-pass slabs: slab j of quarter list l holds the scores of rows
+// tile + 16 (b / 4) + 4 kq + b % 4, b = 0..7 (the MFMA accumulator layout; kq
+// = l & 3). A score of -inf is a padding row; with a filter pre-mask `allow`
+// (bit r = local row r = global - row_base; nullable) the main pass leaves
+// masked rows in the slab and the select drops them here.
+struct SlabMask {
+  const uint64_t* allow;
+  uint32_t row_base;
+};
+// the 8 mask bits of a slab (tile % 32 == 0 locally: one half of a word)
+__device__ __forceinline__ uint32_t slab_bits(SlabMask fm, uint32_t tile, uint32_t kq) {
+  if (!fm.allow) return 0xFFu;
+  const uint32_t r = tile - fm.row_base;
+  const uint32_t tw = (uint32_t)(fm.allow[r >> 6] >> (r & 32)) >> (4 * kq);
+  return (tw & 0xFu) | ((tw >> 12) & 0xF0u);
+}
+
+// The sample pass's key buffers (select_slab_kernel below takes the main
+// pass's slabs).
+// SV (ablation builds only, tools/ablate_mfma.hip): 1 = stop after the
+// first pass, 2 = after the bound, 3 = after the append pass.
+template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
     uint32_t cap, uint32_t k, uint32_t* __restrict__ clear, uint64_t* __restrict__ out) {
@@ -1383,24 +1494,35 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint32_t fill, spill;
+  __shared__ uint64_t thr_sh;
   static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two quarters per thread");
   const uint32_t q = blockIdx.x;
   const uint32_t sub = cap >> 2, nl = 4 * nwg;  // a buffer = 4 lane quarters
-  auto qptr = [&](uint32_t l) {
-    return cand + ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub;
+  // first key of quarter list l: [wg][query][cap], a quarter = sub keys
+  auto qoff = [&](uint32_t l) -> size_t {
+    return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub;
   };
   uint32_t qc[2];
+  {
+    uint32_t craw[2];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const uint32_t l = threadIdx.x + r * kSelThreads;
-    uint32_t c = 0;
-    if (l < nl) c = cnt[((size_t)(l >> 2) * kMfmaQueries + q) * 4 + (l & 3)];
-    qc[r] = c < sub ? c : sub;
+    for (int r = 0; r < 2; ++r) {  // both counts in flight (index clamped, masked)
+      const uint32_t l = threadIdx.x + r * kSelThreads;
+      const uint32_t lc = l < nl ? l : 0u;
+      craw[r] = cnt[((size_t)(lc >> 2) * kMfmaQueries + q) * 4 + (lc & 3)];
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t l = threadIdx.x + r * kSelThreads;
+      const uint32_t c = l < nl ? craw[r] : 0u;
+      qc[r] = c < sub ? c : sub;
+    }
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const uint32_t l = threadIdx.x + r * kSelThreads;
-    uint64_t m = sel_scan_quarter<false>(qptr(l), qc[r], 0, nullptr, nullptr, nullptr);
+    uint64_t m = sel_scan_quarter<false>(cand + qoff(l < nl ? l : 0u), qc[r], 0, buf, &fill,
+                                         &spill);
 #pragma unroll
     for (int s = 1; s <= 2; s <<= 1) {  // the 4 quarters of a buffer are 4 adjacent lanes
       const uint64_t o = __shfl_xor(m, s, 64);
@@ -1410,14 +1532,33 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
   }
   if (threadIdx.x == 0) fill = 0, spill = 0;
   __syncthreads();
-  bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+  if constexpr (SV == 1) return;
   // admit keys > thr (0 marks an empty slot)
-  uint64_t thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+  uint64_t thr;
+  if (k <= 64) {
+    if (threadIdx.x < 64) {
+      const uint64_t b = sel_bound_wave(lmax, k, (int)threadIdx.x);
+      if (threadIdx.x == 0) thr_sh = b ? b - 1 : 0;
+    }
+    __syncthreads();
+    thr = thr_sh;
+  } else {
+    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+    thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+  }
+  if constexpr (SV == 2) return;
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
-    sel_scan_quarter<true>(qptr(threadIdx.x + r * kSelThreads), qc[r], thr, buf, &fill, &spill);
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t l = threadIdx.x + r * kSelThreads;
+    sel_scan_quarter<true>(cand + qoff(l < nl ? l : 0u), qc[r], thr, buf, &fill, &spill);
+  }
   __syncthreads();
+  if constexpr (SV == 3) return;
   uint32_t nR = 0;  // running top-k in buf[0, nR)
+  if (!spill && fill <= 64) {
+    if (threadIdx.x < 64) sel_finish_wave(buf, fill, k, (int)threadIdx.x, out + (size_t)q * k);
+    return;
+  }
   if (!spill) {
     const uint32_t c = fill;
     if (c) {
@@ -1447,7 +1588,7 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
           const uint32_t mid = (lo + hi) >> 1;
           if (pre[mid] <= i) lo = mid; else hi = mid;
         }
-        const uint64_t x = qptr(lo)[i - pre[lo]];
+        const uint64_t x = cand[qoff(lo) + (i - pre[lo])];
         if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
       }
       __syncthreads();
@@ -1467,14 +1608,237 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
   for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
 }
 
+// Slab select, compacted (the main pass's buffers; one workgroup per query).
+// A query's slabs are few (~600-800 at k = 10) but spread over 4 * nwg lists
+// of 0-8 each, so per-list rounds of loads would cost as many dependent
+// memory round trips as the longest list in a wave. Instead: one round for
+// the 1024 counts, a block prefix sum, an LDS owner table (flat slab index ->
+// list), then every thread loads up to kSelHeld slabs of the flat range in
+// ONE round and keeps them in registers for both passes. Pass 1: per
+// buffer (workgroup) the maximum admitted score, LDS atomicMax; the k-th
+// largest is a score bound (k distinct rows reach it). Pass 2: keys of the
+// held scores that reach it -> buf, sorted once. More slabs than the
+// workgroup holds (large k, adversarial ties) go through the same passes in
+// chunks, re-loading; more than kMfmaSelBuf keys past the bound take the
+// streaming path of select_cand_kernel.
+constexpr int kSelHeld = 4;                      // slabs per thread per chunk
+constexpr uint32_t kSelChunk = kSelHeld * kSelThreads;  // 2048 slabs
+
+template <int SV = 0>
+__global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
+    const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
+    const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
+    uint64_t* __restrict__ out, SlabMask fm) {
+  __shared__ uint64_t buf[kMfmaSelBuf];
+  __shared__ uint64_t lmax[kMfmaMaxLists];
+  __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
+  __shared__ uint16_t owner[kSelChunk];
+  __shared__ uint32_t wtot[kSelThreads / 64];
+  __shared__ uint32_t fill, spill;
+  __shared__ uint64_t thr_sh;
+  static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two lists per thread");
+  const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t sub = cap >> 2, nl = 4 * nwg;
+  // lists 2 tid, 2 tid + 1: counts (both loads in flight; past nl: 0)
+  const uint32_t l0 = 2 * tid;
+  uint32_t c0 = 0, c1 = 0;
+  {
+    const uint32_t a0 = l0 < nl ? l0 : 0u, a1 = l0 + 1 < nl ? l0 + 1 : 0u;
+    const uint32_t r0 = cnt[((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3)];
+    const uint32_t r1 = cnt[((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3)];
+    c0 = l0 < nl ? (r0 < sub ? r0 : sub) : 0u;
+    c1 = l0 + 1 < nl ? (r1 < sub ? r1 : sub) : 0u;
+  }
+  if (tid < kMfmaMaxLists) lmax[tid] = 0;
+  // block exclusive prefix sum of the counts
+  uint32_t incl = c0 + c1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if ((int)lane >= d) incl += y;
+  }
+  if (lane == 63) wtot[w] = incl;
+  if (tid == 0) fill = 0, spill = 0;
+  __syncthreads();
+  uint32_t woff = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kSelThreads / 64; ++i) {
+    const uint32_t x = wtot[i];
+    woff += (uint32_t)i < w ? x : 0u;
+    total += x;
+  }
+  const uint32_t ex = woff + incl - (c0 + c1);
+  pre[l0] = ex;
+  pre[l0 + 1] = ex + c0;
+  if (tid == 0) pre[2 * kSelThreads] = total;
+  for (uint32_t j = 0; j < c0; ++j)
+    if (ex + j < kSelChunk) owner[ex + j] = (uint16_t)l0;
+  for (uint32_t j = 0; j < c1; ++j)
+    if (ex + c0 + j < kSelChunk) owner[ex + c0 + j] = (uint16_t)(l0 + 1);
+  __syncthreads();
+  const uint32_t T = total;
+  // slot j of quarter list l (layout [wg][query][cap], a quarter = sub slots)
+  auto slab_at = [&](uint32_t l, uint32_t j) -> size_t {
+    return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub + j;
+  };
+  // flat slab i -> its list (owner table inside the first chunk, else a
+  // binary search of pre), its entry and kq
+  auto list_of = [&](uint32_t i) -> uint32_t {
+    if (i < kSelChunk) return owner[i];
+    uint32_t lo = 0, hi = 2 * kSelThreads;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  f32x4_t v[kSelHeld][2];
+  uint32_t tl[kSelHeld], ls[kSelHeld], bits[kSelHeld];
+  auto load_chunk = [&](uint32_t base) {
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      const uint32_t i = base + tid + (uint32_t)u * kSelThreads;
+      const bool ok = i < T;
+      const uint32_t l = ok ? list_of(i) : 0u;
+      const size_t e = slab_at(l, ok ? i - pre[l] : 0u);
+      ls[u] = l;
+      v[u][0] = slabs[2 * e];
+      v[u][1] = slabs[2 * e + 1];
+      tl[u] = tiles[e];
+      bits[u] = ok ? 0xFFu : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u)
+      if (bits[u]) bits[u] = slab_bits(fm, tl[u], ls[u] & 3);
+  };
+  // pass 1: per buffer (workgroup) maximum admitted score
+  for (uint32_t base = 0; base < T; base += kSelChunk) {
+    load_chunk(base);
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      float sv[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) sv[b] = ((bits[u] >> b) & 1u) ? v[u][b >> 2][b & 3] : -INFINITY;
+      const float m = fmax3(fmax3(sv[0], sv[1], sv[2]), fmax3(sv[3], sv[4], sv[5]),
+                            fmax3(sv[6], sv[7], -INFINITY));
+      if (m != -INFINITY)
+        atomicMax((unsigned long long*)&lmax[ls[u] >> 2], (unsigned long long)make_key(m, 0xFFFFFFFFu));
+    }
+  }
+  __syncthreads();
+  if constexpr (SV == 1) return;
+  // admit keys > thr: every such key's score reaches thr_s
+  uint64_t thr;
+  if (k <= 64) {
+    if (w == 0) {
+      const uint64_t b = sel_bound_wave(lmax, k, (int)lane);
+      if (lane == 0) thr_sh = b ? b - 1 : 0;
+    }
+    __syncthreads();
+    thr = thr_sh;
+  } else {
+    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+    thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+  }
+  // the bound is a score with the smallest row key, so thr + 1 is its key
+  const float thr_s = thr ? key_score(thr + 1) : -INFINITY;
+  if constexpr (SV == 2) return;
+  // pass 2: keys reaching the bound -> buf (held slabs when one chunk did it)
+  for (uint32_t base = 0; base < T; base += kSelChunk) {
+    if (T > kSelChunk) load_chunk(base);
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float sc = v[u][b >> 2][b & 3];
+        if (((bits[u] >> b) & 1u) && sc >= thr_s) {
+          const uint64_t x = make_key(
+              sc, tl[u] + 16u * (uint32_t)(b >> 2) + 4u * (ls[u] & 3) + (uint32_t)(b & 3));
+          if (x > thr) {
+            const uint32_t pos = atomicAdd(&fill, 1u);
+            if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = x; else spill = 1u;
+          }
+        }
+      }
+  }
+  __syncthreads();
+  if constexpr (SV == 3) return;
+  uint32_t nR = 0;  // running top-k in buf[0, nR)
+  if (!spill && fill <= 64) {
+    if (w == 0) sel_finish_wave(buf, fill, k, (int)lane, out + (size_t)q * k);
+    return;
+  }
+  if (!spill) {
+    const uint32_t c = fill;
+    if (c) {
+      int p2 = 1;
+      while ((uint32_t)p2 < c) p2 <<= 1;
+      for (uint32_t i = c + tid; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+      __syncthreads();
+      bitonic_sort_desc_n(buf, p2, kSelThreads);
+      nR = c < k ? c : k;
+    }
+  } else {
+    // more than kMfmaSelBuf keys reach the bound: stream the slabs in chunks
+    // of (kMfmaSelBuf - k) / 8 through buf, keeping a running top k
+    const uint32_t chunk = (kMfmaSelBuf - k) / 8;
+    for (uint32_t base = 0; base < T; base += chunk) {
+      if (tid == 0) fill = nR;
+      __syncthreads();
+      const uint32_t end = base + chunk < T ? base + chunk : T;
+      for (uint32_t i = base + tid; i < end; i += kSelThreads) {
+        const uint32_t l = list_of(i);
+        const size_t e = slab_at(l, i - pre[l]);
+        const f32x4_t v0 = slabs[2 * e], v1 = slabs[2 * e + 1];
+        const uint32_t t = tiles[e];
+        const uint32_t bb8 = slab_bits(fm, t, l & 3);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const float sc = b < 4 ? v0[b] : v1[b - 4];
+          const uint32_t row = t + 16u * (uint32_t)(b >> 2) + 4u * (l & 3) + (uint32_t)(b & 3);
+          const uint64_t x = (((bb8 >> b) & 1u) && sc != -INFINITY) ? make_key(sc, row) : 0ull;
+          if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
+        }
+      }
+      __syncthreads();
+      const uint32_t c = fill;
+      if (c > nR) {
+        int p2 = 1;
+        while ((uint32_t)p2 < c) p2 <<= 1;
+        for (uint32_t i = c + tid; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+        __syncthreads();
+        bitonic_sort_desc_n(buf, p2, kSelThreads);
+        nR = c < k ? c : k;
+        if (nR == k && buf[k - 1] > thr) thr = buf[k - 1];
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
+}
+
+static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) {
+  return nwg != 0 && nwg <= kMfmaMaxLists && cap >= 4 && cap % 4 == 0 && k != 0 &&
+         k <= kMfmaMaxK && nq != 0 && nq <= kMfmaQueries;
+}
+
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
                          uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
                          uint32_t* clear) {
-  if (nwg == 0 || nwg > kMfmaMaxLists || cap < 4 || cap % 4 || k == 0 || k > kMfmaMaxK ||
-      nq == 0 || nq > kMfmaQueries)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_cand_kernel, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt, nwg,
-                     cap, k, clear, out);
+  if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_cand_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt,
+                     nwg, cap, k, clear, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
+                               const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
+                               uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
+                               const uint64_t* allow) {
+  if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
+                     (const f32x4_t*)slabs, slab_tile, cand_cnt, nwg, cap, k, out,
+                     SlabMask{allow, row_base});
   return hipGetLastError();
 }
 

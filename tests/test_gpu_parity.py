@@ -145,14 +145,16 @@ def test_mfma_candidate_path_dims(engine, orc, dim, nq, k):
 
 
 def test_mfma_overflow_fallback(engine, orc):
-    """Adversarial ties: 70k rows, the first 40k identical. Every identical row
-    reaches the sample bound of the queries that match it, the candidate
-    buffers overflow, and the sorted-list pass must give the exact answer
-    (ties -> lowest rows) for those queries and for the others alike."""
+    """Adversarial ties: 300k rows, the first 200k identical. Every identical
+    row reaches the sample bound of the queries that match it, so every lane
+    of those queries appends a slab per tile (~24 per workgroup), the
+    16-slab quarters overflow, and the sorted-list pass (k <= 16) or the GEMV
+    re-run (k > 16) must give the exact answer (ties -> lowest rows) for
+    those queries and for the others alike."""
     import json
-    n, dim = 70_000, 768
+    n, dim = 300_000, 768
     base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
-    base[:40_000] = base[12_345]
+    base[:200_000] = base[12_345]
     engine.create_collection("ties", dim, 0, 1, n)
     engine.upsert("ties", np.arange(n), base)
     X = orc.preprocess(base, True, True)
@@ -165,6 +167,25 @@ def test_mfma_overflow_fallback(engine, orc):
         _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
     assert json.loads(engine.health())["mfma_fallbacks"] >= before + 3
     engine.drop_collection("ties")
+
+
+def test_mfma_select_spill_ties(engine, orc):
+    """70k rows, the first 40k identical: each workgroup's ~9 tiles fit its
+    16-slab quarters (no overflow), but ~40k keys tie at the top for the
+    matching queries, so the select streams the slabs in chunks (its spill
+    path) and must still return the lowest rows."""
+    n, dim = 70_000, 768
+    base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
+    base[:40_000] = base[12_345]
+    engine.create_collection("ties70", dim, 0, 1, n)
+    engine.upsert("ties70", np.arange(n), base)
+    X = orc.preprocess(base, True, True)
+    Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 9, 40, dim)])
+    for k in (10, 50, 128):
+        s, r, c = engine.search("ties70", Q, k)
+        assert r[0].tolist() == list(range(k))
+        _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    engine.drop_collection("ties70")
 
 
 def test_fp32_batched(engine, orc, corpora):

@@ -67,7 +67,9 @@ int main(int argc, char** argv) {
   mfma_grid(n, &c.nwg, &rpw);
   CK(hipMalloc(&out, (size_t)c.nwg * 256 * k * 8));
   const uint32_t st = st_over ? st_over : mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
-  CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 8));
+  CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 32));  // main-pass slabs
+  uint32_t* ctile;
+  CK(hipMalloc(&ctile, (size_t)c.nwg * 256 * cap * 4));
   CK(hipMalloc(&scand, (size_t)c.nwg * 256 * 4 * st * 8));
   CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4 * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
@@ -94,7 +96,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   MfArgs& g = c.args;
   g.X = X, g.Q = Q, g.init_th = skeys + (k - 1), g.init_stride = k, g.lists = out;
-  g.cand = cand, g.cand_cnt = cnt, g.overflow = ovf, g.cand_cap = cap;
+  g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.overflow = ovf, g.cand_cap = cap;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
@@ -126,13 +128,86 @@ int main(int argc, char** argv) {
     printf("%-16s median %.3f ms  min %.3f ms  HBM %.0f GB/s  MFMA %.0f TF/s\n", arm.name, med,
            arm.t[0], bytes / med / 1e6, flops / med / 1e9);
   }
+  // the main pass once more, then its select (timed) and, on the host, how
+  // many slab keys pass the select's first bound per query
+  {
+    MfArgs m = c.args;
+    hipLaunchKernelGGL((mfma_topk_kernel<768, 0, 0, 2>), dim3(c.nwg), dim3(512), 0, 0, m);
+    CK(hipDeviceSynchronize());
+    std::vector<float> tsel;
+    for (int r = 0; r < 3 * reps; ++r) {
+      hipEventRecord(a, 0);
+      CK(launch_select_slabs((const float*)cand, ctile, cnt, c.nwg, cap, 256, k, out, 0));
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      float ms = 0;
+      hipEventElapsedTime(&ms, a, b);
+      tsel.push_back(ms);
+    }
+    std::sort(tsel.begin(), tsel.end());
+    printf("%-16s median %.1f us  min %.1f us\n", "slab select", 1e3 * tsel[tsel.size() / 2],
+           1e3 * tsel[0]);
+    auto sv = [&](auto kern, const char* name) {
+      std::vector<float> tv;
+      for (int r = 0; r < 3 * reps; ++r) {
+        hipEventRecord(a, 0);
+        hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const f32x4_t*)cand,
+                           (const uint32_t*)ctile, (const uint32_t*)cnt, c.nwg, cap, k, out,
+                           SlabMask{nullptr, 0});
+        hipEventRecord(b, 0);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        tv.push_back(ms);
+      }
+      std::sort(tv.begin(), tv.end());
+      printf("%-16s median %.1f us\n", name, 1e3 * tv[tv.size() / 2]);
+    };
+    sv(select_slab_kernel<1>, "sel: pass 1");
+    sv(select_slab_kernel<2>, "sel: + sort");
+    sv(select_slab_kernel<3>, "sel: + append");
+    sv(select_slab_kernel<0>, "sel: full");
+    const uint32_t nl = 4 * c.nwg, sub = cap / 4;
+    std::vector<uint32_t> hcnt((size_t)256 * nl), htile((size_t)c.nwg * 256 * cap);
+    std::vector<float> hsl((size_t)c.nwg * 256 * cap * 8);
+    CK(hipMemcpy(hcnt.data(), cnt, hcnt.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(htile.data(), ctile, htile.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hsl.data(), cand, hsl.size() * 4, hipMemcpyDeviceToHost));
+    double pass_sum = 0, slab_sum = 0;
+    uint32_t pass_max = 0;
+    for (uint32_t q = 0; q < 256; ++q) {
+      std::vector<uint64_t> bmax(c.nwg, 0), keys;
+      for (uint32_t l = 0; l < nl; ++l) {
+        const uint32_t n = std::min(hcnt[((size_t)(l >> 2) * 256 + q) * 4 + (l & 3)], sub);
+        slab_sum += n;
+        for (uint32_t j = 0; j < n; ++j) {
+          const size_t e = ((size_t)(l >> 2) * 256 + q) * cap + (l & 3) * sub + j;
+          for (int bb = 0; bb < 8; ++bb) {
+            const float sc = hsl[8 * e + bb];
+            if (sc == -INFINITY) continue;
+            const uint64_t key = vs::make_key(sc, htile[e] + 16 * (bb >> 2) + 4 * (l & 3) + (bb & 3));
+            keys.push_back(key);
+            bmax[l >> 2] = std::max(bmax[l >> 2], key);
+          }
+        }
+      }
+      std::sort(bmax.rbegin(), bmax.rend());
+      const uint64_t thr = bmax[k - 1] ? bmax[k - 1] - 1 : 0;
+      uint32_t np = 0;
+      for (uint64_t x : keys) np += x > thr;
+      pass_sum += np;
+      pass_max = std::max(pass_max, np);
+    }
+    printf("slabs/query %.1f; keys past the select's first bound: mean %.1f, max %u\n",
+           slab_sum / 256, pass_sum / 256, pass_max);
+  }
   uint32_t of = 0;
   CK(hipMemcpy(&of, ovf, 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
   uint64_t tot = 0, mx = 0;
   for (uint32_t v : hc) tot += v, mx = v > mx ? v : mx;
-  printf("cap %u; grid %u WGs x %u rows, sample tiles/wg %u, overflow %u, candidates/query %.1f, max per buffer %lu\n",
+  printf("cap %u; grid %u WGs x %u rows, sample tiles/wg %u, overflow %u, slabs/query %.1f, max per buffer %lu\n",
          cap, c.nwg, rpw, st, of, (double)tot / 256, (unsigned long)mx);
   return 0;
 }
