@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
     ap.add_argument("--cpu-sample-queries", type=int, default=320)
+    ap.add_argument("--dump-keys", default="",
+                    help="rank 0 writes the last step's merged keys here (.npy; parity tests)")
     return ap.parse_args()
 
 
@@ -123,7 +125,8 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         dist.barrier()
     el = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        gloo = dist.get_backend() == "gloo"
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     tm = eng.timing(reset=True)
@@ -158,11 +161,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VS_DIST_BACKEND=gloo (tests only): several ranks may then share one GPU
+    # (RCCL refuses duplicate devices); the driver's runs use nccl = RCCL
+    backend = os.environ.get("VS_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist_on = world > 1
     if dist_on:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import __graft_entry__ as ge
     pkg = ge.load_package()
@@ -238,6 +249,8 @@ def main():
         s, r, c = pkg.keys_decode(out.cpu().numpy().view(np.uint64))
         assert int(c.min()) == min(k, n_full), "incomplete result lists"
         assert np.all(np.diff(s, axis=1) <= 0), "unsorted results"
+        if args.dump_keys:
+            np.save(args.dump_keys, out.cpu().numpy().view(np.uint64))
 
     if rank == 0:
         print(json.dumps(result), flush=True)

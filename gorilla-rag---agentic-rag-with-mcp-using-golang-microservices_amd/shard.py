@@ -59,7 +59,14 @@ class ShardedSearch:
         if flat is None:
             flat = self._gather_bufs[key] = torch.empty(shape, dtype=local.dtype,
                                                         device=local.device)
-        dist.all_gather_into_tensor(flat, local, group=self.group)
+        if local.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo moves host memory only: stage through the host (tests that
+            # put several ranks on one GPU, where RCCL refuses duplicate devices)
+            host = torch.empty(shape, dtype=local.dtype)
+            dist.all_gather_into_tensor(host, local.cpu(), group=self.group)
+            flat.copy_(host)
+        else:
+            dist.all_gather_into_tensor(flat, local, group=self.group)
         return self.merge(flat.view((P,) + tuple(local.shape)), k)
 
 

@@ -1,0 +1,51 @@
+"""bench.py's multi-rank path on the one GPU of a test box: two ranks (gloo for
+the exchange, since RCCL refuses two ranks on one device), each holding half
+of the rows, must return exactly the keys one rank holding all rows returns.
+This runs the product's shard / all-gather / on-device merge code end to end
+in separate processes (the driver's 8-GPU runs use the same code over RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(tmp_path, tag, nproc, extra):
+    out = str(tmp_path / f"{tag}.npy")
+    args = ["bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+            "--no-secondary", "--dump-keys", out] + extra
+    env = dict(os.environ, VS_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line), np.load(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,rows", [("c3", 300_000), ("c3b1", 200_000)])
+def test_two_ranks_equal_one_rank(tmp_path, config, rows):
+    r1, k1 = _bench(tmp_path, f"{config}_one", 1, ["--config", config, "--rows", str(rows)])
+    r2, k2 = _bench(tmp_path, f"{config}_two", 2, ["--config", config, "--rows", str(rows)])
+    assert r2["n_gpus"] == 2 and r2["config"]["rows_per_gpu"] == rows // 2
+    assert r1["config"]["rows_per_gpu"] == rows
+    assert k1.shape == k2.shape and k1.shape[1] == 10
+    np.testing.assert_array_equal(k1, k2)

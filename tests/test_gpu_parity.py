@@ -367,6 +367,65 @@ def test_large_properties(engine, orc):
     engine.drop_collection("big")
 
 
+def test_mfma_large_shard_parity_128(engine, orc):
+    """Large shard with a partial last tile: full oracle parity at dim 128,
+    4.4M + 17 rows (537 tiles per workgroup), 64 queries, repeated; probes
+    that are corpus rows from the start, the middle and the partial last
+    tile must each be their own top hit."""
+    dim, n = 128, 4_400_017
+    engine.create_collection("big128", dim, 0, 1, n)
+    engine.generate("big128", n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 7, 64, dim)
+    for _ in range(2):
+        s, r, c = engine.search("big128", Q, 10)
+        _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, 10)
+    probe = [0, 1_000_003, n * 7 // 8 + 11, n - 40, n - 17, n - 1]
+    P = np.stack([X[i] for i in probe] + [X[5]] * 58)
+    s, r, c = engine.search("big128", P, 1)
+    assert r[:len(probe), 0].tolist() == probe
+    engine.drop_collection("big128")
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_mfma_parity_1m_768(engine, orc, k):
+    """Full oracle parity at dim 768 on 1M + 3 rows (122 tiles per
+    workgroup, a partial last tile), 64 queries, k = 10 and 100."""
+    dim, n = 768, 1_000_003
+    try:
+        engine.collection_info("c1m768")
+    except Exception:
+        engine.create_collection("c1m768", dim, 0, 1, n)
+        engine.generate("c1m768", n, orc.SEED_CORPUS)
+    X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 300, 64, dim)
+    s, r, c = engine.search("c1m768", Q, k)
+    _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
+    if k == 100:
+        engine.drop_collection("c1m768")
+
+
+def test_mfma_probes_4_5m_768(engine, orc):
+    """4.5M + 5 rows at dim 768: probes across the corpus and in the last
+    tile find themselves, and each probe's batched top-10 equals the GEMV
+    path's (where no near-tie makes the order ambiguous)."""
+    dim, n = 768, 4_500_005
+    engine.create_collection("big768", dim, 0, 1, n)
+    engine.generate("big768", n, orc.SEED_CORPUS)
+    probe = [17, 2_250_001, n * 7 // 8 + 3, n * 15 // 16, n - 5, n - 1]
+    Q = np.concatenate([orc.generate(orc.SEED_CORPUS, i, 1, dim, True) for i in probe])
+    Qb = np.concatenate([Q] + [orc.generate(orc.SEED_QUERY, 0, 250, dim)])
+    s, r, c = engine.search("big768", Qb, 10)  # MFMA path
+    assert r[:len(probe), 0].tolist() == probe
+    for i, p in enumerate(probe):
+        s1, r1, c1 = engine.search("big768", Q[i], 10)  # GEMV path
+        assert r1[0, 0] == p
+        np.testing.assert_allclose(s[i], s1[0], rtol=1e-5, atol=1e-6)
+        if np.abs(np.diff(s1[0])).min() > 1e-5:
+            assert r[i].tolist() == r1[0].tolist()
+    engine.drop_collection("big768")
+
+
 def test_health(engine):
     import json
     h = json.loads(engine.health())

@@ -31,14 +31,20 @@ template <int MODE, int VAR, int G = 2>
 static float run(const Ctx& c, bool bound) {
   MfArgs a = c.args;
   if (!bound) a.init_th = nullptr;
+  // VS_ABL_BURST=B: B launches back to back per timing (sustained clocks, as
+  // in a serving loop; the time per launch is returned). Default 1
+  // (isolated launches). Isolated launches favoured a dynamic tile pool by
+  // 8%; back to back it was 3-5% slower than the static split (r01).
+  static const int burst = getenv("VS_ABL_BURST") ? atoi(getenv("VS_ABL_BURST")) : 1;
   hipEventRecord(c.a, 0);
-  hipLaunchKernelGGL((mfma_topk_kernel<768, MODE, VAR, G>), dim3(c.nwg), dim3(64 * mf_waves(G)), 0,
-                     0, a);
+  for (int i = 0; i < burst; ++i)
+    hipLaunchKernelGGL((mfma_topk_kernel<768, MODE, VAR, G>), dim3(c.nwg), dim3(64 * mf_waves(G)),
+                       0, 0, a);
   hipEventRecord(c.b, 0);
   hipEventSynchronize(c.b);
   float ms = 0;
   hipEventElapsedTime(&ms, c.a, c.b);
-  return ms;
+  return ms / burst;
 }
 
 struct Arm {
@@ -116,8 +122,13 @@ int main(int argc, char** argv) {
       {"qf-only", run<12, 0, 2>, false, {}},
       {"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}},
   };
+  // arms rotate their position every rep: a fixed order measured position
+  // effects of up to 8% (the arm after the tiny ones ran fastest, r01)
   for (int r = 0; r < reps; ++r)
-    for (auto& arm : arms) arm.t.push_back(arm.fn(c, arm.bound));
+    for (size_t j = 0; j < arms.size(); ++j) {
+      auto& arm = arms[(j + (size_t)r) % arms.size()];
+      arm.t.push_back(arm.fn(c, arm.bound));
+    }
   CK(hipDeviceSynchronize());
   const double bytes = (double)n * 768 * 2, flops = 2.0 * 256 * n * 768;
   std::sort(ts.begin(), ts.end());
