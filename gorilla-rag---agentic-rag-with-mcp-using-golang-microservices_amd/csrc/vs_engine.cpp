@@ -257,17 +257,14 @@ int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
 }
 
 // Single-query scans (GEMV path) of preprocessed fp32 queries qp[q0 .. q0+n)
-// -> keys d_keys[i * k], one scan + merge per query.
+// -> keys d_keys[i * k], one scan + merge per query. For bf16 collections qp
+// already holds bf16-rounded values (search_core's query prep).
 int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
-  if (bf16)
-    VS_HIP(vsk::launch_round_bf16(qp + (size_t)q0 * dim, (uint64_t)n * dim,
-                                  qp + (size_t)q0 * dim, eng->stream),
-           "round query");
   const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
   const size_t lbytes = (size_t)maxl * k * 8;
   if (eng->lists.bytes < lbytes) {
@@ -443,7 +440,11 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     }
     qb = eng->q_bf16.as<uint16_t>();
   }
-  VS_HIP(vsk::launch_preprocess(d_q, nq, dim, cosine, false, qp, nullptr, 0, eng->stream, qb),
+  // the fp32 copy feeds the GEMV path only: the MFMA path needs it just for
+  // its k > 16 fallback
+  const bool need_qp = !use_mfma || k > vsk::kMfmaListMaxK;
+  VS_HIP(vsk::launch_query_prep(d_q, nq, dim, cosine, bf16, need_qp ? qp : nullptr, qb,
+                                eng->stream),
          "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
   return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);

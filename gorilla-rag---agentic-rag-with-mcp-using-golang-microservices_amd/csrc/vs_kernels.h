@@ -32,6 +32,12 @@ hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
                              const uint64_t* dst_rows, uint64_t dst0,
                              hipStream_t st, uint16_t* also_bf16 = nullptr);
 
+// Search-side query preprocess (Qdrant cosine normalise when `cosine`):
+// qp (nullable) = fp32 queries, rounded to bf16 values when round_qp;
+// qb (nullable) = bf16 copy. Bit-identical to launch_preprocess's values.
+hipError_t launch_query_prep(const float* in, uint32_t n, uint32_t dim, bool cosine,
+                             bool round_qp, float* qp, uint16_t* qb, hipStream_t st);
+
 // Generate n synthetic unit rows with global numbers grow0 .. grow0+n-1 and
 // store them into dst rows dst0 .. (bf16 or fp32), or as fp32 when f32_out.
 hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,

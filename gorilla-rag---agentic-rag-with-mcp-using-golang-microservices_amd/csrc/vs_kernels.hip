@@ -155,6 +155,65 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
   }
 }
 
+// Query side (search): one wave per query, dim <= 64 * kQPrepMax. All of a
+// lane's elements are loaded at once (one memory latency instead of dim/64
+// dependent ones: 9 -> ~4 us per batch), the squared norm is summed in the
+// store side's order (lane l: elements l, l+64, ... in sequence, then the
+// same butterfly) and only for cosine, and each output is optional: qp =
+// fp32 (rounded to bf16 values when round_qp: what a bf16 scan multiplies),
+// qb = bf16 copy.
+constexpr int kQPrepMax = 24;  // dim <= 1536
+__global__ __launch_bounds__(256) void query_prep_kernel(const float* __restrict__ in, uint32_t n,
+                                                         uint32_t dim, int cosine, int round_qp,
+                                                         float* __restrict__ qp,
+                                                         uint16_t* __restrict__ qb) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const float* x = in + (size_t)i * dim;
+  float v[kQPrepMax];
+#pragma unroll
+  for (int j = 0; j < kQPrepMax; ++j) {
+    const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
+    v[j] = d < dim ? x[d] : 0.f;
+  }
+  bool keep = true;
+  double nrm = 1.0;
+  if (cosine) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQPrepMax; ++j) {
+      const double t = (double)v[j];
+      s = s + t * t;  // zero padding adds exact zeros: same sum as the store side
+    }
+    s = wave_sum_f64(s);
+    keep = vs::cosine_keep(s);
+    nrm = sqrt(s);
+  }
+#pragma unroll
+  for (int j = 0; j < kQPrepMax; ++j) {
+    const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
+    if (d >= dim) break;
+    const float y = keep ? v[j] : (float)((double)v[j] / nrm);
+    const uint16_t h = vs::f32_to_bf16(y);
+    if (qp) qp[(size_t)i * dim + d] = round_qp ? vs::bf16_to_f32(h) : y;
+    if (qb) qb[(size_t)i * dim + d] = h;
+  }
+}
+
+hipError_t launch_query_prep(const float* in, uint32_t n, uint32_t dim, bool cosine,
+                             bool round_qp, float* qp, uint16_t* qb, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (dim > 64u * kQPrepMax) {  // wide vectors: the store side's loop kernel
+    hipError_t e = launch_preprocess(in, n, dim, cosine, false, qp, nullptr, 0, st, qb);
+    if (e != hipSuccess || !round_qp || !qp) return e;
+    return launch_round_bf16(qp, (uint64_t)n * dim, qp, st);
+  }
+  hipLaunchKernelGGL(query_prep_kernel, dim3((n + 3) / 4), dim3(256), 0, st, in, n, dim,
+                     (int)cosine, (int)round_qp, qp, qb);
+  return hipGetLastError();
+}
+
 hipError_t launch_preprocess(const float* in, uint32_t n, uint32_t dim,
                              bool cosine, bool bf16, void* dst,
                              const uint64_t* dst_rows, uint64_t dst0,
