@@ -1911,6 +1911,7 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // chunk added something. Correct for any input; fast when the bound is good.
 constexpr int kMergeThreads = 512;
 constexpr int kMergeCap = 4096;
+constexpr int kMergeHeld = 16;  // fast path: keys per thread held in registers
 
 __device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
   for (int size = 2; size <= n_pow2; size <<= 1) {
@@ -1941,6 +1942,80 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
   __shared__ uint32_t cnt;
   const uint32_t q = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+
+  // Fast path (single-query GEMV merges and shard merges at k <= 32): all
+  // L * kin keys fit kMergeHeld per thread, so they are read in ONE memory
+  // round trip, and the top k is taken by tournament: each wave extracts its
+  // k largest (wave max by xor-shuffles, k rounds; keys are unique, 0 =
+  // empty), then wave 0 extracts the k largest of the 8 waves' winners. The
+  // general path below filters against max_l list_l[k-1], which admitted
+  // hundreds of keys here (a weak bound over many short lists) and paid a
+  // block-wide bitonic sort for them.
+  const uint64_t total0 = (uint64_t)L * kin;
+  if (total0 <= (uint64_t)kMergeThreads * kMergeHeld && k <= 32) {
+    uint64_t x[kMergeHeld];
+    // every load issued unconditionally (clamped index), all in flight at
+    // once; a conditional load per key compiled to one round trip each
+#pragma unroll
+    for (int u = 0; u < kMergeHeld; ++u) {
+      const uint32_t i0 = threadIdx.x + (uint32_t)u * kMergeThreads;
+      const uint32_t i = i0 < total0 ? i0 : 0u;
+      const uint32_t l = i / kin, j = i - l * kin;
+      x[u] = lists[l * lstride + q * qstride + j];
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeHeld; ++u)
+      if (threadIdx.x + (uint32_t)u * kMergeThreads >= total0) x[u] = 0;
+    auto lane_max = [&]() {
+      uint64_t m = 0;
+#pragma unroll
+      for (int u = 0; u < kMergeHeld; ++u) m = x[u] > m ? x[u] : m;
+      return m;
+    };
+    auto wave_max = [&](uint64_t v) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+      }
+      return v;
+    };
+    uint64_t lm = lane_max();
+    for (uint32_t r = 0; r < k; ++r) {
+      const uint64_t wm = wave_max(lm);
+      if (lane == 0) buf[w * 32 + r] = wm;
+      if (wm != 0 && lm == wm) {  // the one lane holding it (keys are unique)
+#pragma unroll
+        for (int u = 0; u < kMergeHeld; ++u) x[u] = x[u] == wm ? 0ull : x[u];
+        lm = lane_max();
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      // 8 waves x k winners: lane l holds winners l, l + 64, l + 128, l + 192
+      uint64_t y[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t e = (uint32_t)lane + 64u * (uint32_t)u, ww = e / 32, rr = e % 32;
+        y[u] = rr < k ? buf[ww * 32 + rr] : 0ull;
+      }
+      uint64_t m2 = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) m2 = y[u] > m2 ? y[u] : m2;
+      for (uint32_t r = 0; r < k; ++r) {
+        const uint64_t wm = wave_max(m2);
+        if (lane == 0) out[(size_t)q * k + r] = wm;
+        if (wm != 0 && m2 == wm) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) y[u] = y[u] == wm ? 0ull : y[u];
+          m2 = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) m2 = y[u] > m2 ? y[u] : m2;
+        }
+      }
+    }
+    return;
+  }
 
   // initial bound (strict filter "key > thr")
   uint64_t b = 0;
