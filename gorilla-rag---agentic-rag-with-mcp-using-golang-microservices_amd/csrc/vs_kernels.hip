@@ -914,6 +914,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // pass would spill with it
   constexpr bool kPin = (VAR & 128) != 0 || MODE != 8;
   if (a.run_if && *a.run_if == 0) return;  // fallback launch with nothing to redo
+  // VAR 8192 (ablation): per-workgroup start / end wall clock into a.lists
+  constexpr bool kClock = (VAR & 8192) != 0;
+  uint64_t tclk0 = 0;
+  if constexpr (kClock) tclk0 = wall_clock64();
   // ONE shared array: a second __shared__ object makes hipcc drain vmcnt
   // before LDS reads (cdna_hip_programming.md §5, trap 4(a)).
   __shared__ __attribute__((aligned(16))) unsigned char smem[S::LDS_BYTES];
@@ -1276,6 +1280,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   } else {
     for (uint32_t t = 0; t < ntiles; ++t) tile(t, MfFull<false>{});
   }
+  if constexpr (kClock)
+    if (threadIdx.x == 0) {
+      a.lists[2 * blockIdx.x] = tclk0;
+      a.lists[2 * blockIdx.x + 1] = wall_clock64();
+    }
   // each wave owns its queries' lists / counters: no barrier before the write-out
 #pragma unroll
   for (int g = 0; g < G; ++g) {

@@ -212,6 +212,33 @@ int main(int argc, char** argv) {
     printf("slabs/query %.1f; keys past the select's first bound: mean %.1f, max %u\n",
            slab_sum / 256, pass_sum / 256, pass_max);
   }
+  // per-workgroup start / end clocks of the main pass (VAR 8192; wall_clock64
+  // ticks at 100 MHz) in the last of `burst` back-to-back launches: how far
+  // the static row split leaves XCDs apart (blockIdx % 8 = XCD)
+  for (int burst : {1, 8}) {
+    for (int r = 0; r < 2; ++r) {
+      MfArgs m = c.args;
+      m.lists = out;
+      for (int i = 0; i < burst; ++i)
+        hipLaunchKernelGGL((mfma_topk_kernel<768, 0, 8192, 2>), dim3(c.nwg), dim3(512), 0, 0, m);
+      CK(hipDeviceSynchronize());
+      std::vector<uint64_t> clk((size_t)2 * c.nwg);
+      CK(hipMemcpy(clk.data(), out, clk.size() * 8, hipMemcpyDeviceToHost));
+      uint64_t s0 = ~0ull, e0 = ~0ull, e1 = 0;
+      double dsum = 0;
+      std::vector<double> xe(8, 0);
+      for (uint32_t i = 0; i < c.nwg; ++i) s0 = std::min(s0, clk[2 * i]);
+      for (uint32_t i = 0; i + 1 < c.nwg; ++i) {  // the last workgroup may hold fewer rows
+        e0 = std::min(e0, clk[2 * i + 1]), e1 = std::max(e1, clk[2 * i + 1]);
+        dsum += (double)(clk[2 * i + 1] - clk[2 * i]);
+        xe[i % 8] += (double)(clk[2 * i + 1] - s0);
+      }
+      printf("burst %d clocks: end spread %.1f us, mean dur %.1f us, last end %.1f; mean end by xcd:",
+             burst, (e1 - e0) / 100.0, dsum / (c.nwg - 1) / 100.0, (e1 - s0) / 100.0);
+      for (int x = 0; x < 8; ++x) printf(" %.0f", xe[x] / ((c.nwg - 1) / 8.0) / 100.0);
+      printf("\n");
+    }
+  }
   uint32_t of = 0;
   CK(hipMemcpy(&of, ovf, 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
