@@ -377,20 +377,23 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                  allow),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    // 3. overflow fallback, k <= 16: the sorted-list pass (a no-op launch
+    // unless the main pass set the flag), whose lists the select then merges
+    // in place of the slabs
+    const bool dev_fb = k <= vsk::kMfmaListMaxK;
+    uint32_t Lf = 0;
+    if (dev_fb)
+      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
+                                    maxl, &Lf, eng->stream, allow),
+             "mfma scan (fallback)");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
     VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                                    k, out, eng->stream, row_base, allow),
+                                    k, out, eng->stream, row_base, allow,
+                                    dev_fb ? ovf : nullptr, lists, Lf, (uint64_t)PS * k,
+                                    eng->fallbacks.as<uint32_t>()),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
-    // 3. overflow fallback
-    if (k <= vsk::kMfmaListMaxK) {
-      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
-                                    maxl, &L, eng->stream, allow),
-             "mfma scan (fallback)");
-      VS_HIP(vsk::launch_merge(lists, L, (uint64_t)PS * k, k, nv, k, k, out, eng->stream, ovf,
-                               eng->fallbacks.as<uint32_t>()),
-             "merge (fallback)");
-    } else {
+    if (!dev_fb) {
       uint32_t h_ovf = 0;
       VS_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, eng->stream), "flag D2H");
       VS_HIP(hipStreamSynchronize(eng->stream), "flag sync");

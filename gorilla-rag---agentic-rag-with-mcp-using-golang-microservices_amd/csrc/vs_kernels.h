@@ -109,7 +109,13 @@ hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,
-                               const uint64_t* allow = nullptr);
+                               const uint64_t* allow = nullptr,
+                               // overflow fallback (k <= kMfmaListMaxK): when *fb_flag is
+                               // set, merge the lists pass's [fb_L][kMfmaQueries][k] lists
+                               // (list stride fb_lstride keys) instead; fb_ran counts it
+                               const uint32_t* fb_flag = nullptr,
+                               const uint64_t* fb_lists = nullptr, uint32_t fb_L = 0,
+                               uint64_t fb_lstride = 0, uint32_t* fb_ran = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows);

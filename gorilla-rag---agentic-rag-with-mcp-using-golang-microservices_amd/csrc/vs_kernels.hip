@@ -733,6 +733,7 @@ struct MfArgs {
   const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
+  const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
 };
 
 // XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
@@ -930,9 +931,13 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   const int col = lane & 15;  // MFMA column (query in group) / A-fragment row
   const int kq = lane >> 4;   // 8-element k slice; C rows 4kq .. 4kq+3
   const uint32_t k = a.k;
-  const uint32_t wr0 = blockIdx.x * a.rows_per_wg;
-  const uint32_t wr1 =
-      (uint64_t)wr0 + a.rows_per_wg < a.n_rows ? wr0 + a.rows_per_wg : a.n_rows;
+  uint32_t wr0 = blockIdx.x * a.rows_per_wg;
+  uint32_t wr1 = (uint64_t)wr0 + a.rows_per_wg < a.n_rows ? wr0 + a.rows_per_wg : a.n_rows;
+  if (a.wg_tile) {  // a weighted split (per-XCD speeds)
+    wr0 = a.wg_tile[blockIdx.x] * 32u;
+    const uint64_t e = (uint64_t)a.wg_tile[blockIdx.x + 1] * 32u;
+    wr1 = e < a.n_rows ? (uint32_t)e : a.n_rows;
+  }
   uint32_t ntiles = (wr1 - wr0 + 31) / 32;
   if (a.max_tiles && ntiles > a.max_tiles) ntiles = a.max_tiles;
   const uint32_t nchunks = ntiles * S::CPT;
@@ -1692,11 +1697,28 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
 constexpr int kSelHeld = 4;                      // slabs per thread per chunk
 constexpr uint32_t kSelChunk = kSelHeld * kSelThreads;  // 2048 slabs
 
+// The main pass's overflow fallback, folded into the select: when *flag is
+// set, the sorted-list pass (MODE 8, enqueued before the select) has re-run
+// the batch, and the select merges its lists [L][kMfmaQueries][k] instead of
+// reading slabs (one launch less per batch than a separate no-op merge).
+struct SlabFallback {
+  const uint32_t* flag;  // nullable
+  const uint64_t* lists;
+  uint32_t L;
+  uint64_t lstride;
+  uint32_t* ran;  // nullable: counts fallback batches
+};
+
+__device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, uint32_t L,
+                                            uint64_t lstride, uint64_t qstride, uint32_t kin,
+                                            uint32_t k, uint32_t q, uint64_t* __restrict__ out,
+                                            uint64_t* buf, uint64_t* red, uint32_t& cnt);
+
 template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
-    uint64_t* __restrict__ out, SlabMask fm) {
+    uint64_t* __restrict__ out, SlabMask fm, SlabFallback fb) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -1705,6 +1727,11 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
   __shared__ uint32_t fill, spill;
   __shared__ uint64_t thr_sh;
   static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two lists per thread");
+  if (fb.flag && *fb.flag) {
+    if (fb.ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(fb.ran, 1u);
+    merge_query(fb.lists, fb.L, fb.lstride, k, k, k, blockIdx.x, out, buf, lmax, fill);
+    return;
+  }
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
   // lists 2 tid, 2 tid + 1: counts (both loads in flight; past nl: 0)
@@ -1902,11 +1929,15 @@ hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
-                               const uint64_t* allow) {
+                               const uint64_t* allow, const uint32_t* fb_flag,
+                               const uint64_t* fb_lists, uint32_t fb_L, uint64_t fb_lstride,
+                               uint32_t* fb_ran) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
+  if (fb_flag && (!fb_lists || fb_L == 0 || k > kMfmaListMaxK)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
                      (const f32x4_t*)slabs, slab_tile, cand_cnt, nwg, cap, k, out,
-                     SlabMask{allow, row_base});
+                     SlabMask{allow, row_base},
+                     SlabFallback{fb_flag, fb_lists, fb_L, fb_lstride, fb_ran});
   return hipGetLastError();
 }
 
@@ -1940,16 +1971,13 @@ __device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
   }
 }
 
-__global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
-    const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
-    uint32_t kin, uint32_t k, const uint32_t* __restrict__ run_if, uint32_t* __restrict__ ran,
-    uint64_t* __restrict__ out) {
-  if (run_if && *run_if == 0) return;  // fallback launch with nothing to redo
-  if (ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ran, 1u);
-  __shared__ uint64_t buf[kMergeCap];
-  __shared__ uint64_t red[kMergeThreads / 64];
-  __shared__ uint32_t cnt;
-  const uint32_t q = blockIdx.x;
+// Top-k of query q over L lists (merge_keys_kernel; also select_slab_kernel's
+// overflow fallback). buf holds >= kMergeCap keys; red / cnt are the
+// caller's shared scratch. One workgroup of kMergeThreads threads.
+__device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, uint32_t L,
+                                            uint64_t lstride, uint64_t qstride, uint32_t kin,
+                                            uint32_t k, uint32_t q, uint64_t* __restrict__ out,
+                                            uint64_t* buf, uint64_t* red, uint32_t& cnt) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 
   // Fast path (single-query GEMV merges and shard merges at k <= 32): all
@@ -2085,6 +2113,18 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
   }
   for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads)
     out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
+    const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
+    uint32_t kin, uint32_t k, const uint32_t* __restrict__ run_if, uint32_t* __restrict__ ran,
+    uint64_t* __restrict__ out) {
+  if (run_if && *run_if == 0) return;  // fallback launch with nothing to redo
+  if (ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ran, 1u);
+  __shared__ uint64_t buf[kMergeCap];
+  __shared__ uint64_t red[kMergeThreads / 64];
+  __shared__ uint32_t cnt;
+  merge_query(lists, L, lstride, qstride, kin, k, blockIdx.x, out, buf, red, cnt);
 }
 
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,

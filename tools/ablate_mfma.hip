@@ -23,6 +23,7 @@ using namespace vsk;
 
 struct Ctx {
   MfArgs args;
+  uint32_t* wgt;
   uint32_t nwg;
   hipEvent_t a, b;
 };
@@ -31,6 +32,7 @@ template <int MODE, int VAR, int G = 2>
 static float run(const Ctx& c, bool bound) {
   MfArgs a = c.args;
   if (!bound) a.init_th = nullptr;
+  if (VAR & 65536) a.wg_tile = c.wgt;  // ablation: the weighted split
   // VS_ABL_BURST=B: B launches back to back per timing (sustained clocks, as
   // in a serving loop; the time per launch is returned). Default 1
   // (isolated launches). Isolated launches favoured a dynamic tile pool by
@@ -114,8 +116,36 @@ int main(int argc, char** argv) {
   // G = 4 (4 waves x 64 queries, one wave per SIMD, 512 registers): no
   // epilogue 4.23 ms, 3.74 with a 2-step fragment prefetch, 3.60 with a pinned
   // 3-step one, vs 3.35 for G = 2 (10M rows, r01).
+  // weighted split: VS_XCD_W = 8 comma-separated weights for blockIdx % 8
+  uint32_t* wgt = nullptr;
+  {
+    std::vector<double> xw(8, 1.0);
+    if (const char* e = getenv("VS_XCD_W")) {
+      int x = 0;
+      for (const char* p = e; *p && x < 8; ++x) {
+        xw[x] = atof(p);
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    }
+    const uint32_t T = (n + 31) / 32;
+    double tot = 0;
+    for (uint32_t b = 0; b < c.nwg; ++b) tot += xw[b % 8];
+    std::vector<uint32_t> h(c.nwg + 1);
+    double acc = 0;
+    for (uint32_t b = 0; b < c.nwg; ++b) {
+      h[b] = (uint32_t)(acc / tot * T + 0.5);
+      acc += xw[b % 8];
+    }
+    h[c.nwg] = T;
+    CK(hipMalloc(&wgt, h.size() * 4));
+    CK(hipMemcpy(wgt, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    printf("weighted split: %u..%u tiles per workgroup\n", h[1] - h[0], h[2] - h[1]);
+  }
+  c.wgt = wgt;
   std::vector<Arm> arms = {
       {"main cand", run<0, 0, 2>, true, {}},
+      {"main weighted", run<0, 65536, 2>, true, {}},
       {"no-epilogue", run<1, 0, 2>, false, {}},
       {"max-only (6)", run<6, 0, 2>, true, {}},
       {"dma-only", run<2, 0, 2>, false, {}},
@@ -164,7 +194,7 @@ int main(int argc, char** argv) {
         hipEventRecord(a, 0);
         hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const f32x4_t*)cand,
                            (const uint32_t*)ctile, (const uint32_t*)cnt, c.nwg, cap, k, out,
-                           SlabMask{nullptr, 0});
+                           SlabMask{nullptr, 0}, SlabFallback{});
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms = 0;
