@@ -951,10 +951,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   bool qvalid[G];
   float th_s[G];     // admit rows whose score reaches th_s
   // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
-  // query's buffer (candidate passes)
+  // query's buffer (candidate passes). VAR 131072 (main pass): the counts and
+  // each lane's first slot live in registers instead (no LDS round trip and
+  // no address rebuild in the append path).
+  constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) != 0;
+  uint32_t cnt_r[G], slot0[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
+    if constexpr (kRegCnt) {
+      cnt_r[g] = 0u;
+      slot0[g] = (uint32_t)(((size_t)blockIdx.x * kMfmaQueries +
+                             (uint32_t)(w * QPW + g * 16 + col)) * a.cand_cap +
+                            (uint32_t)kq * (a.cand_cap >> 2));
+    }
     ql[g] = (uint32_t)(w * QPW + g * 16 + col);
     qvalid[g] = ql[g] < a.nq_valid;
     const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
@@ -1193,9 +1203,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         // seven at the next chunk barrier (r01: -0.12 ms at 1.25M rows).
         if (qvalid[g] && mx >= th_s[g] && mx != -INFINITY) {
           const uint32_t sub = a.cand_cap >> 2;
-          const uint32_t cg = cntl[g * THREADS + threadIdx.x];
+          const uint32_t cg = kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
           if (cg >= sub) {
             *a.overflow = 1u;  // the caller re-runs the batch exactly
+          } else if constexpr (kRegCnt) {
+            const size_t slot = (size_t)slot0[g] + cg;
+            f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
+            sp[0] = acc[0][g];
+            sp[1] = acc[1][g];
+            a.cand_tile[slot] = a.row_base + trow0;
+            cnt_r[g] = cg + 1;
           } else {
             // the address is rebuilt here from an opaque thread id, so none
             // of it is hoisted out of the tile loop (its register budget)
@@ -1295,7 +1312,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   for (int g = 0; g < G; ++g) {
     if constexpr (kCand) {
       a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
-          cntl[g * THREADS + threadIdx.x];
+          kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
     } else if constexpr (kLists) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {

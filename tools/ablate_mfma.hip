@@ -146,6 +146,9 @@ int main(int argc, char** argv) {
   std::vector<Arm> arms = {
       {"main cand", run<0, 0, 2>, true, {}},
       {"main weighted", run<0, 65536, 2>, true, {}},
+      {"main nt-dma", run<0, 1024, 2>, true, {}},
+      {"main regcnt", run<0, 131072, 2>, true, {}},
+      {"main regcnt nt", run<0, 131072 + 1024, 2>, true, {}},
       {"no-epilogue", run<1, 0, 2>, false, {}},
       {"max-only (6)", run<6, 0, 2>, true, {}},
       {"dma-only", run<2, 0, 2>, false, {}},
