@@ -886,7 +886,9 @@ struct MfShape {
 // 4-B LDS-DMA (a quarter of the bytes, same instructions). VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1;
 // VAR 128: each step's reads and MFMAs pinned in program order; VAR 512:
 // the chunk's LDS-DMA pieces spread over its steps instead of at its head;
-// VAR 1024: non-temporal (nt) LDS-DMA loads of the corpus stream.
+// VAR 1024: flips the corpus stream's load policy (MODE 0 default: non-temporal
+// LDS-DMA; other modes: default policy). VAR 131072 (MODE 0): append counters
+// in LDS instead of registers (the r01-v13 form).
 template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D)>
 __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
@@ -951,10 +953,13 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   bool qvalid[G];
   float th_s[G];     // admit rows whose score reaches th_s
   // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
-  // query's buffer (candidate passes). VAR 131072 (main pass): the counts and
-  // each lane's first slot live in registers instead (no LDS round trip and
-  // no address rebuild in the append path).
-  constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) != 0;
+  // query's buffer (candidate passes). The main pass keeps the counts and
+  // each lane's first slot in registers instead (no LDS round trip and no
+  // address rebuild in the append path; 256 VGPRs, no spill), and streams the
+  // corpus non-temporally: back to back, -2.0% at 1.25M rows and -1.2% at 10M
+  // against LDS counters and default-policy DMA (r01, 2 x 40 / 16 reps).
+  constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) == 0;
+  constexpr bool kNtDma = (MODE == 0) != ((VAR & 1024) != 0);
   uint32_t cnt_r[G], slot0[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -1000,7 +1005,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     if constexpr (MODE == 11)
       glds4(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
     else
-      glds16<(VAR & 1024) != 0>(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
+      glds16<kNtDma>(xnext, loff[i], lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024));
   };
   auto advance = [&]() {
     const bool last = unext == S::CPT - 1;

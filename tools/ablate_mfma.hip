@@ -144,17 +144,20 @@ int main(int argc, char** argv) {
   }
   c.wgt = wgt;
   std::vector<Arm> arms = {
-      {"main cand", run<0, 0, 2>, true, {}},
-      {"main weighted", run<0, 65536, 2>, true, {}},
-      {"main nt-dma", run<0, 1024, 2>, true, {}},
-      {"main regcnt", run<0, 131072, 2>, true, {}},
-      {"main regcnt nt", run<0, 131072 + 1024, 2>, true, {}},
-      {"no-epilogue", run<1, 0, 2>, false, {}},
-      {"max-only (6)", run<6, 0, 2>, true, {}},
-      {"dma-only", run<2, 0, 2>, false, {}},
-      {"qf-only", run<12, 0, 2>, false, {}},
-      {"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}},
+      {"main cand", run<0, 0, 2>, true, {}},                // regs + nt (default)
+      {"main cached-dma", run<0, 1024, 2>, true, {}},       // regs, default policy
+      {"main lds-cnt", run<0, 131072, 2>, true, {}},        // LDS counters + nt
+      {"main v13", run<0, 131072 + 1024, 2>, true, {}},     // LDS counters, default policy
   };
+  if (!getenv("VS_ABL_SHORT")) {
+    arms.push_back({"main weighted", run<0, 65536, 2>, true, {}});
+    arms.push_back({"no-epilogue", run<1, 0, 2>, false, {}});
+    arms.push_back({"max-only (6)", run<6, 0, 2>, true, {}});
+    arms.push_back({"dma-only", run<2, 0, 2>, false, {}});
+    arms.push_back({"qf-only", run<12, 0, 2>, false, {}});
+    arms.push_back({"G4 no-epi pd3pin", run<1, 64 + 128, 4>, false, {}});
+  }
+
   // arms rotate their position every rep: a fixed order measured position
   // effects of up to 8% (the arm after the tiny ones ran fastest, r01)
   for (int r = 0; r < reps; ++r)
