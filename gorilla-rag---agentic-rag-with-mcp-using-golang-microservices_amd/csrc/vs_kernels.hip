@@ -1212,12 +1212,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           if (cg >= sub) {
             *a.overflow = 1u;  // the caller re-runs the batch exactly
           } else if constexpr (kRegCnt) {
+            // VAR 262144 (ablation): the appending wave runs at raised
+            // priority, so it reaches the next chunk barrier sooner
+            if constexpr ((VAR & 262144) != 0) __builtin_amdgcn_s_setprio(3);
             const size_t slot = (size_t)slot0[g] + cg;
             f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
             sp[0] = acc[0][g];
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
             cnt_r[g] = cg + 1;
+            if constexpr ((VAR & 262144) != 0) __builtin_amdgcn_s_setprio(0);
           } else {
             // the address is rebuilt here from an opaque thread id, so none
             // of it is hoisted out of the tile loop (its register budget)

@@ -148,6 +148,7 @@ int main(int argc, char** argv) {
       {"main cached-dma", run<0, 1024, 2>, true, {}},       // regs, default policy
       {"main lds-cnt", run<0, 131072, 2>, true, {}},        // LDS counters + nt
       {"main v13", run<0, 131072 + 1024, 2>, true, {}},     // LDS counters, default policy
+      {"main prio", run<0, 262144, 2>, true, {}},           // default + raised priority appends
   };
   if (!getenv("VS_ABL_SHORT")) {
     arms.push_back({"main weighted", run<0, 65536, 2>, true, {}});
