@@ -102,6 +102,7 @@ struct vs_engine {
   DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
+  DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters)
   uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
   std::vector<uint64_t> h_keys;
   // timing
@@ -170,6 +171,11 @@ hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
 // Rows allocated past the capacity: the MFMA scan streams whole 32-row tiles
 // and reads (then masks) up to 31 rows beyond the last one.
 constexpr uint64_t kPadRows = 32;
+// Filtered single-query searches gather the allowed rows when at most
+// 1 / kGatherDensityDen of the collection is allowed: below
+// that density the scattered 1.5-3 KB row reads stay near the streaming rate,
+// and the compaction launch is paid back many times over.
+constexpr uint64_t kGatherDensityDen = 8;
 
 // Grows a collection to hold `need` rows (writer lock held by the caller).
 int grow(vs_engine* eng, Collection& c, uint64_t need) {
@@ -258,12 +264,14 @@ int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
 
 // Single-query scans (GEMV path) of preprocessed fp32 queries qp[q0 .. q0+n)
 // -> keys d_keys[i * k], one scan + merge per query. For bf16 collections qp
-// already holds bf16-rounded values (search_core's query prep).
+// already holds bf16-rounded values (search_core's query prep). With `gather`
+// (n_gather device row indices) only those rows are scanned.
 int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow = nullptr) {
+                uint64_t* d_keys, const uint64_t* allow = nullptr,
+                const uint32_t* gather = nullptr, uint32_t n_gather = 0) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
-  const uint32_t n_rows = (uint32_t)c.rows;
+  const uint32_t n_rows = gather ? n_gather : (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
   const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
   const size_t lbytes = (size_t)maxl * k * 8;
@@ -275,7 +283,7 @@ int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
     uint32_t L = 0;
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_gemv(c.data, bf16, dim, n_rows, row_base, qp + (size_t)i * dim, k,
-                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream, allow),
+                            eng->lists.as<uint64_t>(), maxl, &L, eng->stream, allow, gather),
            "gemv scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -411,7 +419,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
 int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow = nullptr) {
+                uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -450,6 +458,24 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                                 eng->stream),
          "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
+  // selective filter on the GEMV path: scan only the allowed rows, gathered
+  // through a compacted row list (cost ~ allowed rows instead of all rows)
+  if (allow && allowed * kGatherDensityDen <= c.rows) {
+    if (allowed == 0) {
+      VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
+      return VS_OK;
+    }
+    if (eng->gather_rows.bytes < allowed * 4 || eng->gather_cnt.bytes < 4) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->gather_rows.ensure(allowed * 4), "alloc gather list");
+      VS_HIP(eng->gather_cnt.ensure(4), "alloc gather count");
+    }
+    VS_HIP(vsk::launch_compact_rows(allow, (uint32_t)c.rows, eng->gather_rows.as<uint32_t>(),
+                                    eng->gather_cnt.as<uint32_t>(), eng->stream),
+           "compact filter rows");
+    return search_gemv(eng, c, qp, 0, nq, k, d_keys, nullptr, eng->gather_rows.as<uint32_t>(),
+                       (uint32_t)allowed);
+  }
   return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
 }
 
@@ -769,8 +795,17 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
   if (abytes)
     VS_HIP(hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream),
            "filter bitmap H2D");
+  uint64_t allowed = 0;  // popcount of the bitmap over the collection's rows
+  if (abytes) {
+    const uint64_t nw = (c->rows + 63) / 64;
+    for (uint64_t i = 0; i < nw; ++i) {
+      uint64_t w = allow[i];
+      if (i == nw - 1 && (c->rows & 63)) w &= (1ull << (c->rows & 63)) - 1;
+      allowed += (uint64_t)__builtin_popcountll(w);
+    }
+  }
   int rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
-                       abytes ? eng->allow.as<uint64_t>() : nullptr);
+                       abytes ? eng->allow.as<uint64_t>() : nullptr, allowed);
   if (rc != VS_OK) return rc;
   eng->h_keys.resize((size_t)nq * k);
   VS_HIP(hipMemcpyAsync(eng->h_keys.data(), eng->keys.p, kbytes, hipMemcpyDeviceToHost,

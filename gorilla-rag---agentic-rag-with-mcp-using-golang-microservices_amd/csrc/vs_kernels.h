@@ -50,7 +50,14 @@ hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
 hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                        uint32_t row_base, const float* q, uint32_t k,
                        uint64_t* out, uint32_t max_lists, uint32_t* nlists,
-                       hipStream_t st, const uint64_t* allow = nullptr);
+                       hipStream_t st, const uint64_t* allow = nullptr,
+                       const uint32_t* rows = nullptr);
+// With `rows` (device, n_rows entries of local row indices) the scan gathers
+// those rows only (a selective filter) and `allow` is ignored.
+// Filter bitmap -> the allowed local rows (< n_rows), in arbitrary order, and
+// their count in *d_count (device). `rows` holds popcount(allow) entries.
+hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t* rows,
+                               uint32_t* d_count, hipStream_t st);
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 

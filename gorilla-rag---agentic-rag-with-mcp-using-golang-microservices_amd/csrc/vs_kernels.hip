@@ -429,11 +429,16 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 
 // VAR (ablation knobs, tools/ablate_gemv.hip): 1 = non-temporal loads,
 // 2 = DPP/permlane wave sum, 4 = loads two steps ahead instead of one.
-template <int D, bool BF16, int KPL, int VAR = kGemvVar>
+// GATHER: the scan walks positions [0, n_rows) of the compacted row list
+// rows[] (a selective filter, compact_rows_kernel) instead of the rows
+// themselves; each gathered row is still one contiguous, coalesced read, and
+// the list entries are fetched one step ahead of the row data.
+template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
-    uint32_t rows_per_wave, uint64_t* __restrict__ out) {
+    uint32_t rows_per_wave, uint64_t* __restrict__ out,
+    const uint32_t* __restrict__ rows = nullptr) {
   using S = GemvShape<D, BF16>;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -463,11 +468,24 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     constexpr bool kNT = (VAR & 1) != 0, kDpp = (VAR & 2) != 0;
     constexpr int DEPTH = (VAR & 4) ? 2 : 1;
     uint4 buf[DEPTH + 1][S::J];
+    uint32_t ixn[S::J];  // GATHER: rows of the next position to load
+    auto fetch_ix = [&](uint32_t r0) {
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        const uint32_t pos = r0 + rowsel[j];
+        ixn[j] = rows[pos < hi ? pos : hi - 1];
+      }
+    };
     auto load = [&](uint4* dst, uint32_t r0) {
 #pragma unroll
       for (int j = 0; j < S::J; ++j) {
-        uint32_t row = r0 + rowsel[j];
-        row = row < hi ? row : hi - 1;
+        uint32_t row;
+        if constexpr (GATHER) {
+          row = ixn[j];
+        } else {
+          row = r0 + rowsel[j];
+          row = row < hi ? row : hi - 1;
+        }
         const char* p = X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16;
         if constexpr (kNT) {
           const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
@@ -480,11 +498,14 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       const uint32_t r0 = lo + d * S::RB;
+      if constexpr (GATHER) fetch_ix(r0 < hi ? r0 : lo);
       load(buf[d], r0 < hi ? r0 : lo);
     }
+    if constexpr (GATHER) fetch_ix(lo + DEPTH * S::RB);
     for (uint32_t r = lo; r < hi; r += S::RB) {
       const uint32_t rn = r + DEPTH * S::RB;
       load(buf[DEPTH], rn < hi ? rn : r);
+      if constexpr (GATHER) fetch_ix(rn + S::RB);
       float p[S::RB];
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) p[b] = 0.f;
@@ -502,8 +523,8 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
       for (int b = 0; b < S::RB; ++b) {
         const float s = kDpp ? wave_sum_dpp(p[b]) : wave_sum(p[b]);
         const uint32_t row = r + b;
-        if (row < hi && row_allowed(allow, row)) {
-          const uint64_t key = make_key(s, row_base + row);
+        if (row < hi && (GATHER || row_allowed(allow, row))) {
+          const uint64_t key = make_key(s, row_base + (GATHER ? rows[row] : row));
           if (key > theta) {
             L.insert(key, k, lane);
             theta = L.kth(k);
@@ -520,11 +541,12 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
 }
 
 // Any dimension: one row per wave step, lane-strided scalar loads.
-template <bool BF16, int KPL>
+template <bool BF16, int KPL, bool GATHER = false>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
     const void* __restrict__ Xv, uint32_t dim, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
-    uint32_t rows_per_wave, uint64_t* __restrict__ out) {
+    uint32_t rows_per_wave, uint64_t* __restrict__ out,
+    const uint32_t* __restrict__ rows = nullptr) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
@@ -534,7 +556,8 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
   WaveList<KPL> L;
   L.init();
   uint64_t theta = 0;
-  for (uint32_t r = lo; r < hi; ++r) {
+  for (uint32_t pos = lo; pos < hi; ++pos) {
+    const uint32_t r = GATHER ? rows[pos] : pos;
     float p = 0.f;
     for (uint32_t d = lane; d < dim; d += 64) {
       const float x =
@@ -544,7 +567,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
     }
     const float s = wave_sum(p);
     const uint64_t key = make_key(s, row_base + r);
-    if (key > theta && row_allowed(allow, r)) {
+    if (key > theta && (GATHER || row_allowed(allow, r))) {
       L.insert(key, k, lane);
       theta = L.kth(k);
     }
@@ -592,11 +615,27 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k) {
   return g.nwg * per;
 }
 
+template <int D, bool BF16, bool GATHER>
+static void gemv_launch_kpl(int kpl, dim3 grid, dim3 block, hipStream_t st, const void* X,
+                            uint32_t n_rows, uint32_t row_base, const float* q,
+                            const uint64_t* allow, uint32_t k, uint32_t rpw, uint64_t* out,
+                            const uint32_t* rows) {
+  if (kpl == 1)
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1, GATHER>), grid, block, 0, st, X, n_rows,
+                       row_base, q, allow, k, rpw, out, rows);
+  else if (kpl == 2)
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 2, GATHER>), grid, block, 0, st, X, n_rows,
+                       row_base, q, allow, k, rpw, out, rows);
+  else
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 16, GATHER>), grid, block, 0, st, X, n_rows,
+                       row_base, q, allow, k, rpw, out, rows);
+}
+
 template <int D, bool BF16>
 static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row_base,
                                     const float* q, const uint64_t* allow, uint32_t k,
-                                    uint64_t* out,
-                                    uint32_t max_lists, uint32_t* nlists, hipStream_t st) {
+                                    uint64_t* out, uint32_t max_lists, uint32_t* nlists,
+                                    hipStream_t st, const uint32_t* rows) {
   using S = GemvShape<D, BF16>;
   GemvGrid g = gemv_grid(n_rows, S::RB);
   const int kpl = gemv_kpl(k);
@@ -604,53 +643,62 @@ static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row
   if (lists > max_lists) return hipErrorInvalidValue;
   *nlists = lists;
   dim3 grid(g.nwg), block(kGemvThreads);
-  if (kpl == 1)
-    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1>), grid, block, 0, st, X, n_rows,
-                       row_base, q, allow, k, g.rows_per_wave, out);
-  else if (kpl == 2)
-    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 2>), grid, block, 0, st, X, n_rows,
-                       row_base, q, allow, k, g.rows_per_wave, out);
+  if (rows)
+    gemv_launch_kpl<D, BF16, true>(kpl, grid, block, st, X, n_rows, row_base, q, nullptr, k,
+                                   g.rows_per_wave, out, rows);
   else
-    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 16>), grid, block, 0, st, X, n_rows,
-                       row_base, q, allow, k, g.rows_per_wave, out);
+    gemv_launch_kpl<D, BF16, false>(kpl, grid, block, st, X, n_rows, row_base, q, allow, k,
+                                    g.rows_per_wave, out, nullptr);
   return hipGetLastError();
+}
+
+template <bool BF16, bool GATHER>
+static void gemv_generic_kpl(int kpl, dim3 grid, dim3 block, hipStream_t st, const void* X,
+                             uint32_t dim, uint32_t n_rows, uint32_t row_base, const float* q,
+                             const uint64_t* allow, uint32_t k, uint32_t rpw, uint64_t* out,
+                             const uint32_t* rows) {
+  if (kpl == 1)
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 1, GATHER>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, allow, k, rpw, out, rows);
+  else if (kpl == 2)
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 2, GATHER>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, allow, k, rpw, out, rows);
+  else
+    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 16, GATHER>), grid, block, 0, st, X, dim,
+                       n_rows, row_base, q, allow, k, rpw, out, rows);
 }
 
 template <bool BF16>
 static hipError_t gemv_generic(const void* X, uint32_t dim, uint32_t n_rows,
                                uint32_t row_base, const float* q, const uint64_t* allow,
-                               uint32_t k,
-                               uint64_t* out, uint32_t max_lists, uint32_t* nlists,
-                               hipStream_t st) {
+                               uint32_t k, uint64_t* out, uint32_t max_lists, uint32_t* nlists,
+                               hipStream_t st, const uint32_t* rows) {
   GemvGrid g = gemv_grid(n_rows, 1);
   const int kpl = gemv_kpl(k);
   const uint32_t lists = g.nwg * (kpl == 1 ? 1 : kGemvWaves);
   if (lists > max_lists) return hipErrorInvalidValue;
   *nlists = lists;
   dim3 grid(g.nwg), block(kGemvThreads);
-  if (kpl == 1)
-    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 1>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
-  else if (kpl == 2)
-    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 2>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
+  if (rows)
+    gemv_generic_kpl<BF16, true>(kpl, grid, block, st, X, dim, n_rows, row_base, q, nullptr, k,
+                                 g.rows_per_wave, out, rows);
   else
-    hipLaunchKernelGGL((gemv_topk_generic_kernel<BF16, 16>), grid, block, 0, st, X, dim,
-                       n_rows, row_base, q, allow, k, g.rows_per_wave, out);
+    gemv_generic_kpl<BF16, false>(kpl, grid, block, st, X, dim, n_rows, row_base, q, allow, k,
+                                  g.rows_per_wave, out, nullptr);
   return hipGetLastError();
 }
 
 hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                        uint32_t row_base, const float* q, uint32_t k, uint64_t* out,
                        uint32_t max_lists, uint32_t* nlists, hipStream_t st,
-                       const uint64_t* allow) {
+                       const uint64_t* allow, const uint32_t* rows) {
   if (k == 0 || k > kMaxK || n_rows == 0) return hipErrorInvalidValue;
 #define VS_GEMV_CASE(DD)                                                              \
   case DD:                                                                            \
     return bf16 ? gemv_dispatch_kpl<DD, true>(X, n_rows, row_base, q, allow, k, out,  \
-                                              max_lists, nlists, st)                  \
+                                              max_lists, nlists, st, rows)            \
                 : gemv_dispatch_kpl<DD, false>(X, n_rows, row_base, q, allow, k, out, \
-                                               max_lists, nlists, st);
+                                               max_lists, nlists, st, rows);
   switch (dim) {
     VS_GEMV_CASE(128)
     VS_GEMV_CASE(256)
@@ -664,11 +712,54 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
     VS_GEMV_CASE(4096)
     default:
       return bf16 ? gemv_generic<true>(X, dim, n_rows, row_base, q, allow, k, out,
-                                       max_lists, nlists, st)
+                                       max_lists, nlists, st, rows)
                   : gemv_generic<false>(X, dim, n_rows, row_base, q, allow, k, out,
-                                        max_lists, nlists, st);
+                                        max_lists, nlists, st, rows);
   }
 #undef VS_GEMV_CASE
+}
+
+// Filter bitmap -> compacted list of the allowed local rows (< n_rows), for
+// the GATHER scans. One 64-row word per lane; a wave prefix sum of the
+// popcounts places each lane's rows and one atomic per wave reserves the
+// wave's range. The list order across waves is arbitrary: keys are totally
+// ordered by (score, row), so the scan result does not depend on it.
+__global__ __launch_bounds__(256) void compact_rows_kernel(const uint64_t* __restrict__ allow,
+                                                            uint32_t n_rows,
+                                                            uint32_t* __restrict__ rows,
+                                                            uint32_t* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwords = (n_rows + 63) / 64;
+  const uint32_t wi = blockIdx.x * 256u + threadIdx.x;
+  uint64_t w = wi < nwords ? allow[wi] : 0;
+  if (wi == nwords - 1 && (n_rows & 63)) w &= (1ull << (n_rows & 63)) - 1;
+  const uint32_t c = (uint32_t)__popcll(w);
+  uint32_t inc = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off);
+    if (lane >= off) inc += t;
+  }
+  const uint32_t total = __shfl(inc, 63);
+  uint32_t base = 0;
+  if (lane == 63 && total) base = atomicAdd(count, total);
+  base = __shfl(base, 63);
+  uint32_t o = base + inc - c;
+  while (w) {
+    rows[o++] = wi * 64u + (uint32_t)(__ffsll((unsigned long long)w) - 1);
+    w &= w - 1;
+  }
+}
+
+hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t* rows,
+                               uint32_t* d_count, hipStream_t st) {
+  if (n_rows == 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(d_count, 0, 4, st);
+  if (e != hipSuccess) return e;
+  const uint32_t nwords = (n_rows + 63) / 64;
+  hipLaunchKernelGGL(compact_rows_kernel, dim3((nwords + 255) / 256), dim3(256), 0, st, allow,
+                     n_rows, rows, d_count);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

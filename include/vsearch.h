@@ -158,10 +158,13 @@ int vs_search(vs_engine* eng, const char* coll, const float* queries,
 
 /* vs_search with a payload filter pre-mask: only local
  * rows r with bit (allow[r / 64] >> (r % 64)) & 1 set can be returned;
- * out_count[i] = min(k, allowed rows). `allow_words` >= ceil(rows / 64). The
- * bitmap is applied inside the scan kernels (rows are read but never become
- * candidates), so a filtered search costs what an unfiltered one does. The
- * reference accepts `filter` and ignores it (main.go:30 vs :249-254); the
+ * out_count[i] = min(k, allowed rows). `allow_words` >= ceil(rows / 64); bits
+ * past the last row are ignored. Batched (MFMA) searches apply the bitmap
+ * inside the scan kernels (rows are read but never become candidates), so
+ * they cost what an unfiltered search does. GEMV-path searches (one query,
+ * fp32, or k > 128) with at most 1/8 of the rows allowed scan only the
+ * allowed rows, gathered through a compacted row list built on the device.
+ * The reference accepts `filter` and ignores it (main.go:30 vs :249-254); the
  * service mirror applies it only when configured to. */
 int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
                        uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,

@@ -107,3 +107,44 @@ def test_filtered_overflow_fallback(engine, orc):
         assert r[0].tolist() == [2 * i + 1 for i in range(k)]
         _masked_parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k, mask)
     engine.drop_collection("fties")
+
+
+@pytest.mark.parametrize("dtype,dim", [(0, 768), (1, 768), (0, 100), (1, 1024)])
+def test_filtered_gather_path(engine, orc, pkg, dtype, dim):
+    """Selective filters (<= 1/8 of the rows allowed) on the GEMV path scan a
+    compacted row list instead of the whole collection (compact_rows_kernel +
+    the GATHER scans): results must equal the oracle over the allowed rows,
+    including exact ties (duplicated rows), every list width (k = 1, 100,
+    1000 > allowed), the generic-dimension kernel (dim 100) and a mask whose
+    last word is partial."""
+    n = 48_037
+    name = f"fgather_{dtype}_{dim}"
+    base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
+    base[100:400] = base[7]  # 301 identical rows
+    engine.create_collection(name, dim, 0, dtype, n)
+    engine.upsert(name, np.arange(n), base)
+    X = orc.preprocess(base, True, bool(dtype))
+    rng = np.random.default_rng(dim + dtype)
+    mask = rng.random(n) < 0.02
+    mask[100:400:3] = True  # a third of the tied rows
+    mask[[7, n - 1]] = True
+    assert mask.sum() * 8 <= n
+    Q = np.concatenate([base[7:8], orc.generate(orc.SEED_QUERY, 31, 2, dim)])
+    Qp = orc.preprocess(Q, True, bool(dtype))
+    for k in (1, 100, 1000):
+        for nq in (1, 3):
+            s, r, c = engine.search_filtered(name, Q[:nq], k, mask)
+            assert np.all(c == min(k, int(mask.sum())))
+            _masked_parity(orc, X, Qp[:nq], s, r, c, k, mask)
+    # the tied rows come back in row order for the query equal to them
+    s, r, c = engine.search_filtered(name, Q[:1], 50, mask)
+    tied = [7] + [i for i in range(100, 400) if mask[i]]
+    assert r[0, :50].tolist() == sorted(tied)[:50]
+    # bits set past the last row (in the partial last word) must not leak rows
+    words = pkg.pack_allow(mask)
+    words[-1] |= ~np.uint64(0) << np.uint64(n % 64)
+    s2, r2, c2 = engine.search_filtered(name, Q, 100, words)
+    s1, r1, c1 = engine.search_filtered(name, Q, 100, mask)
+    assert np.array_equal(r1, r2) and np.array_equal(c1, c2)
+    engine.drop_collection(name)
+

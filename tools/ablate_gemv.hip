@@ -25,7 +25,7 @@ static float run(const void* X, uint32_t n, const float* q, uint64_t* out, hipEv
   using S = GemvShape<768, BF16>;
   GemvGrid g = gemv_grid(n, S::RB);
   hipEventRecord(a, 0);
-  hipLaunchKernelGGL((gemv_topk_kernel<768, BF16, 1, VAR>), dim3(g.nwg), dim3(kGemvThreads), 0,
+  hipLaunchKernelGGL((gemv_topk_kernel<768, BF16, 1, false, VAR>), dim3(g.nwg), dim3(kGemvThreads), 0,
                      0, X, n, 0u, q, 10u, g.rows_per_wave, out);
   hipEventRecord(b, 0);
   hipEventSynchronize(b);

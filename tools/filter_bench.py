@@ -1,0 +1,65 @@
+"""Filtered single-query search cost vs filter density.
+
+    python tools/filter_bench.py [--rows 10000000] [--dim 768] [--reps 50]
+
+For each density the same random bitmap is used for --reps single-query
+vs_search_filtered calls (host bitmap in, host results out). Reported: wall
+ms per call, the scan kernel's HIP-event ms, and for the gather path (density
+<= 1/8) the gathered row bytes / kernel time. One JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--k", type=int, default=10)
+    args = ap.parse_args()
+    import torch  # noqa: F401
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from oracle import oracle as orc  # query generator only (same seeds as bench.py)
+    eng = pkg.VectorEngine(device=0, timing=True)
+    eng.create_collection("big", args.dim, 1, 1, args.rows)
+    eng.generate("big", args.rows, orc.SEED_CORPUS)
+    Q = orc.generate(orc.SEED_QUERY, 0, args.reps, args.dim)
+    rng = np.random.default_rng(1)
+    out = {"workload": f"{args.rows} x {args.dim} bf16, single query, top-{args.k}",
+           "densities": []}
+    for dens in (1.0, 0.5, 0.125, 0.05, 0.01, 0.001):
+        mask = pkg.pack_allow(rng.random(args.rows) < dens)
+        for i in range(3):
+            eng.search_filtered("big", Q[i], args.k, mask)
+        eng.timing(reset=True)
+        t0 = time.perf_counter()
+        for i in range(args.reps):
+            eng.search_filtered("big", Q[i], args.k, mask)
+        wall = (time.perf_counter() - t0) / args.reps
+        tm = eng.timing(reset=True)
+        scan = tm["scan_ms"]  # vs_timing reports the average per scan
+        allowed = int(np.unpackbits(mask.view(np.uint8)).sum())
+        row = {"density": dens, "allowed": allowed, "wall_ms": round(wall * 1e3, 4),
+               "scan_ms": round(scan, 4), "qps": round(1.0 / wall, 1)}
+        if allowed * 8 <= args.rows:
+            row["gather_gbs"] = round(allowed * args.dim * 2 / (scan * 1e-3) / 1e9, 1)
+        else:
+            row["stream_gbs"] = round(args.rows * args.dim * 2 / (scan * 1e-3) / 1e9, 1)
+        out["densities"].append(row)
+        print(json.dumps(row), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
