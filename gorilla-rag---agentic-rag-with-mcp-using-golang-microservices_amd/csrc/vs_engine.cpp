@@ -176,6 +176,9 @@ constexpr uint64_t kPadRows = 32;
 // that density the scattered 1.5-3 KB row reads stay near the streaming rate,
 // and the compaction launch is paid back many times over.
 constexpr uint64_t kGatherDensityDen = 8;
+// Per-query launch overhead of a gathered scan (scan + merge launches,
+// ~10 us) in bytes of HBM streaming, for the batch decision in search_core.
+constexpr uint64_t kGatherCallBytes = 64ull << 20;
 
 // Grows a collection to hold `need` rows (writer lock held by the caller).
 int grow(vs_engine* eng, Collection& c, uint64_t need) {
@@ -437,7 +440,17 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     VS_HIP(eng->q_pre.ensure(qbytes), "alloc query scratch");
   }
   float* qp = eng->q_pre.as<float>();
-  const bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
+  bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
+  // selective filter: scan only the allowed rows, gathered through a
+  // compacted row list (cost ~ allowed rows instead of all rows), one GEMV
+  // per query. A batch leaves the MFMA pass for it only while nq gathers
+  // (each charged kGatherCallBytes of launch overhead) read less than the
+  // one streamed pass.
+  const uint64_t rbytes = (uint64_t)dim * (bf16 ? 2 : 4);
+  const bool gather = allow && allowed * kGatherDensityDen <= c.rows &&
+                      (!use_mfma || (double)nq * (double)(allowed * rbytes + kGatherCallBytes) <=
+                                        (double)c.rows * (double)rbytes);
+  if (gather) use_mfma = false;
   // the MFMA path reads a bf16 copy, 256 queries per pass (rows past nq are
   // padding: finite, and masked by the kernels)
   uint16_t* qb = nullptr;
@@ -458,9 +471,7 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                                 eng->stream),
          "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
-  // selective filter on the GEMV path: scan only the allowed rows, gathered
-  // through a compacted row list (cost ~ allowed rows instead of all rows)
-  if (allow && allowed * kGatherDensityDen <= c.rows) {
+  if (gather) {
     if (allowed == 0) {
       VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
       return VS_OK;

@@ -148,3 +148,36 @@ def test_filtered_gather_path(engine, orc, pkg, dtype, dim):
     assert np.array_equal(r1, r2) and np.array_equal(c1, c2)
     engine.drop_collection(name)
 
+
+
+def test_filtered_gather_batches(engine, orc):
+    """A batch with a very selective filter on a large collection leaves the
+    MFMA pass for per-query gathered scans (search_core: nq gathers cost less
+    than one streamed pass). Only the allowed rows are generated on the host:
+    a block, scattered single rows and the collection's last row."""
+    n, dim = 2_000_000, 768
+    engine.create_collection("fgbig", dim, 0, 1, n)
+    engine.generate("fgbig", n, orc.SEED_CORPUS)
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([np.arange(700_000, 703_000),
+                                    rng.choice(n, 1500, replace=False), [n - 1]]))
+    mask = np.zeros(n, bool)
+    mask[idx] = True
+    Xa = np.concatenate([orc.generate(orc.SEED_CORPUS, 700_000, 3000, dim, bf16=True)] +
+                        [orc.generate(orc.SEED_CORPUS, int(r), 1, dim, bf16=True)
+                         for r in idx if not 700_000 <= r < 703_000])
+    order = np.argsort(np.concatenate([np.arange(700_000, 703_000),
+                                       [r for r in idx if not 700_000 <= r < 703_000]]))
+    Xa = Xa[order]  # rows of idx, ascending
+    for nq, k in ((8, 10), (4, 128), (2, 1)):
+        Q = orc.generate(orc.SEED_QUERY, 600 + nq, nq, dim)
+        Qp = orc.preprocess(Q, True, True)
+        s, r, c = engine.search_filtered("fgbig", Q, k, mask)
+        assert np.all(c == k)
+        assert np.all(mask[r.astype(np.int64)]), "masked row returned"
+        pos = np.searchsorted(idx, r.astype(np.int64)).astype(np.uint64)
+        s32, s64, rows, cnt = orc.search(Xa, Qp, k)
+        resc = orc.rescore(Xa, Qp, pos, c)
+        bad = orc.check_topk(s, pos, c, s64, rows, cnt, resc, SCORE_RTOL)
+        assert not bad, bad[:10]
+    engine.drop_collection("fgbig")

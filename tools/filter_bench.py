@@ -57,6 +57,21 @@ def main():
             row["stream_gbs"] = round(args.rows * args.dim * 2 / (scan * 1e-3) / 1e9, 1)
         out["densities"].append(row)
         print(json.dumps(row), file=sys.stderr, flush=True)
+    # batches of 8 queries: the MFMA pass with the bitmap fused (dense
+    # filters) or 8 gathered scans (selective filters, search_core's rule)
+    out["batch8"] = []
+    for dens in (0.5, 0.05, 0.01, 0.001):
+        mask = pkg.pack_allow(rng.random(args.rows) < dens)
+        for i in range(3):
+            eng.search_filtered("big", Q[:8], args.k, mask)
+        t0 = time.perf_counter()
+        for i in range(args.reps // 5):
+            eng.search_filtered("big", Q[:8], args.k, mask)
+        wall = (time.perf_counter() - t0) / (args.reps // 5)
+        row = {"density": dens, "nq": 8, "wall_ms": round(wall * 1e3, 4),
+               "qps": round(8 / wall, 1)}
+        out["batch8"].append(row)
+        print(json.dumps(row), file=sys.stderr, flush=True)
     print(json.dumps(out))
     eng.close()
 
