@@ -42,11 +42,16 @@ struct CollState {
   uint64_t nrows() const { return bulk + uuid_of.size(); }
 
   // filter pre-masks (filter mode "match"), cached per canonical filter text
-  // and invalidated by any upsert (version)
+  // and invalidated by any upsert (version); each also lives on the device
+  // (vs_filter_create) so a repeated filter ships no bitmap per search
   uint64_t version = 0;
   std::mutex fmu;
-  std::unordered_map<std::string, std::pair<uint64_t, std::shared_ptr<std::vector<uint64_t>>>>
-      fcache;
+  struct FilterEntry {
+    uint64_t version = 0;
+    std::shared_ptr<std::vector<uint64_t>> mask;
+    uint64_t device_id = 0;  // 0: not resident (the mask is sent per call)
+  };
+  std::unordered_map<std::string, FilterEntry> fcache;
 };
 
 // Synthetic UUID of bulk row r: version 4, variant 10, the collection's
@@ -492,14 +497,20 @@ bool payload_matches(const Json& payload, const Json& filter) {
   return true;
 }
 
-// Allow bitmap of `filter` over cs's rows (reader lock held by the caller).
-std::shared_ptr<std::vector<uint64_t>> filter_mask(CollState& cs, const Json& filter) {
+// Allow bitmap of `filter` over cs's rows and its device-resident copy
+// (reader lock held by the caller).
+CollState::FilterEntry filter_mask(vs_engine* eng, const std::string& coll, CollState& cs,
+                                   const Json& filter) {
   std::string key;
   vsjson::encode(filter, &key);  // canonical: sorted keys
   {
     std::lock_guard<std::mutex> g(cs.fmu);
     auto it = cs.fcache.find(key);
-    if (it != cs.fcache.end() && it->second.first == cs.version) return it->second.second;
+    if (it != cs.fcache.end()) {
+      if (it->second.version == cs.version) return it->second;
+      if (it->second.device_id) (void)vs_filter_drop(eng, it->second.device_id);
+      cs.fcache.erase(it);
+    }
   }
   const uint64_t n = cs.nrows();
   auto m = std::make_shared<std::vector<uint64_t>>((n + 63) / 64, 0);
@@ -510,10 +521,21 @@ std::shared_ptr<std::vector<uint64_t>> filter_mask(CollState& cs, const Json& fi
       const uint64_t r = cs.bulk + i;
       (*m)[r >> 6] |= 1ull << (r & 63);
     }
+  CollState::FilterEntry e;
+  e.version = cs.version;
+  e.mask = m;
+  if (vs_filter_create(eng, coll.c_str(), m->data(), m->size(), &e.device_id) != VS_OK)
+    e.device_id = 0;  // e.g. out of memory: send the mask per call instead
   std::lock_guard<std::mutex> g(cs.fmu);
-  if (cs.fcache.size() >= 64) cs.fcache.clear();
-  cs.fcache[key] = {cs.version, m};
-  return m;
+  if (cs.fcache.size() >= 64) {
+    for (auto& kv : cs.fcache)
+      if (kv.second.device_id) (void)vs_filter_drop(eng, kv.second.device_id);
+    cs.fcache.clear();
+  }
+  auto& slot = cs.fcache[key];
+  if (slot.device_id) (void)vs_filter_drop(eng, slot.device_id);  // a concurrent build
+  slot = e;
+  return e;
 }
 
 Response handle_search(vsvc* svc, const std::string& method, const char* body, size_t len) {
@@ -545,10 +567,15 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   std::string err;
   if (svc->filter_match && req.filter.kind == Json::Object && !req.filter.obj.empty()) {
     // filtered searches carry their own mask: one engine call each
-    auto mask = filter_mask(*cs, req.filter);
-    rc = vs_search_filtered(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
-                            (uint32_t)k, mask->data(), mask->size(), scores.data(),
-                            hit_rows.data(), &count);
+    auto f = filter_mask(svc->eng, req.collection, *cs, req.filter);
+    rc = f.device_id ? vs_search_filter_id(svc->eng, req.collection.c_str(), req.query.data(),
+                                           1, cs->dim, (uint32_t)k, f.device_id, scores.data(),
+                                           hit_rows.data(), &count)
+                     : VS_ERR_NOT_FOUND;
+    if (rc != VS_OK)  // not resident, or evicted by a concurrent request
+      rc = vs_search_filtered(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
+                              (uint32_t)k, f.mask->data(), f.mask->size(), scores.data(),
+                              hit_rows.data(), &count);
     if (rc != VS_OK) err = last_error();
   } else if (svc->batcher) {
     rc = svc->batcher->search(req.collection, req.query.data(), cs->dim, (uint32_t)k,

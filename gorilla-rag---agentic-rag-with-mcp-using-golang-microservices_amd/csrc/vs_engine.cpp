@@ -102,7 +102,15 @@ struct vs_engine {
   DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
-  DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters)
+  DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch
+  // device-resident filters (vs_filter_create), guarded by work_mu
+  struct DevFilter {
+    std::string coll;
+    uint64_t rows = 0, allowed = 0;  // collection rows it was built over
+    DevBuf bits, list;               // bitmap; compacted rows when selective
+  };
+  std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
+  uint64_t next_filter = 1;
   uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
   std::vector<uint64_t> h_keys;
   // timing
@@ -422,7 +430,8 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
 int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0) {
+                uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
+                const uint32_t* allow_list = nullptr) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -476,16 +485,19 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
       VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
       return VS_OK;
     }
-    if (eng->gather_rows.bytes < allowed * 4 || eng->gather_cnt.bytes < 4) {
-      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-      VS_HIP(eng->gather_rows.ensure(allowed * 4), "alloc gather list");
-      VS_HIP(eng->gather_cnt.ensure(4), "alloc gather count");
+    if (!allow_list) {  // not precompacted (vs_filter_create): compact now
+      const size_t sc = (size_t)vsk::compact_scratch_words((uint32_t)c.rows) * 4;
+      if (eng->gather_rows.bytes < allowed * 4 || eng->gather_cnt.bytes < sc) {
+        VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+        VS_HIP(eng->gather_rows.ensure(allowed * 4), "alloc gather list");
+        VS_HIP(eng->gather_cnt.ensure(sc), "alloc compaction scratch");
+      }
+      VS_HIP(vsk::launch_compact_rows(allow, (uint32_t)c.rows, eng->gather_rows.as<uint32_t>(),
+                                      eng->gather_cnt.as<uint32_t>(), eng->stream),
+             "compact filter rows");
+      allow_list = eng->gather_rows.as<uint32_t>();
     }
-    VS_HIP(vsk::launch_compact_rows(allow, (uint32_t)c.rows, eng->gather_rows.as<uint32_t>(),
-                                    eng->gather_cnt.as<uint32_t>(), eng->stream),
-           "compact filter rows");
-    return search_gemv(eng, c, qp, 0, nq, k, d_keys, nullptr, eng->gather_rows.as<uint32_t>(),
-                       (uint32_t)allowed);
+    return search_gemv(eng, c, qp, 0, nq, k, d_keys, nullptr, allow_list, (uint32_t)allowed);
   }
   return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
 }
@@ -771,9 +783,21 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, f
 
 namespace {
 // vs_search / vs_search_filtered: host queries in, host results out.
+uint64_t popcount_rows(const uint64_t* allow, uint64_t rows) {
+  uint64_t allowed = 0;  // popcount of the bitmap over the collection's rows
+  const uint64_t nw = (rows + 63) / 64;
+  for (uint64_t i = 0; i < nw; ++i) {
+    uint64_t w = allow[i];
+    if (i == nw - 1 && (rows & 63)) w &= (1ull << (rows & 63)) - 1;
+    allowed += (uint64_t)__builtin_popcountll(w);
+  }
+  return allowed;
+}
+
 int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
                 uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
-                float* out_scores, uint64_t* out_rows, uint32_t* out_count) {
+                float* out_scores, uint64_t* out_rows, uint32_t* out_count,
+                uint64_t filter_id = 0) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
   if (nq == 0) return VS_OK;
@@ -790,6 +814,16 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
                                         " words, the collection needs " +
                                         std::to_string((c->rows + 63) / 64));
   std::lock_guard<std::mutex> g(eng->work_mu);
+  const vs_engine::DevFilter* df = nullptr;
+  if (filter_id) {
+    auto it = eng->filters.find(filter_id);
+    if (it == eng->filters.end())
+      return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
+    df = it->second.get();
+    if (df->coll != coll || df->rows != c->rows)
+      return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
+                                          " was built for another collection state");
+  }
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(use_stream(eng, eng->own), "stream order");
   const size_t qbytes = (size_t)nq * c->dim * 4;
@@ -806,17 +840,15 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
   if (abytes)
     VS_HIP(hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream),
            "filter bitmap H2D");
-  uint64_t allowed = 0;  // popcount of the bitmap over the collection's rows
-  if (abytes) {
-    const uint64_t nw = (c->rows + 63) / 64;
-    for (uint64_t i = 0; i < nw; ++i) {
-      uint64_t w = allow[i];
-      if (i == nw - 1 && (c->rows & 63)) w &= (1ull << (c->rows & 63)) - 1;
-      allowed += (uint64_t)__builtin_popcountll(w);
-    }
-  }
-  int rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
-                       abytes ? eng->allow.as<uint64_t>() : nullptr, allowed);
+  int rc;
+  if (df)
+    rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
+                     df->bits.as<uint64_t>(), df->allowed,
+                     df->list.p ? df->list.as<uint32_t>() : nullptr);
+  else
+    rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
+                     abytes ? eng->allow.as<uint64_t>() : nullptr,
+                     abytes ? popcount_rows(allow, c->rows) : 0);
   if (rc != VS_OK) return rc;
   eng->h_keys.resize((size_t)nq * k);
   VS_HIP(hipMemcpyAsync(eng->h_keys.data(), eng->keys.p, kbytes, hipMemcpyDeviceToHost,
@@ -841,6 +873,68 @@ int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, u
   if (!allow) return fail(VS_ERR_INVALID_ARG, "allow bitmap is NULL");
   return search_host(eng, coll, queries, nq, dim, k, allow, allow_words, out_scores, out_rows,
                      out_count);
+}
+
+int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
+                     uint64_t allow_words, uint64_t* filter_id) {
+  if (!eng || !allow || !filter_id) return fail(VS_ERR_INVALID_ARG, "NULL argument");
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  const uint64_t nw = (c->rows + 63) / 64;
+  if (allow_words < nw)
+    return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
+                                        " words, the collection needs " + std::to_string(nw));
+  if (c->rows >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  auto f = std::make_unique<vs_engine::DevFilter>();
+  f->coll = coll;
+  f->rows = c->rows;
+  f->allowed = popcount_rows(allow, c->rows);
+  VS_HIP(f->bits.ensure(std::max<uint64_t>(nw, 1) * 8), "alloc filter bitmap");
+  if (nw)
+    VS_HIP(hipMemcpyAsync(f->bits.p, allow, nw * 8, hipMemcpyHostToDevice, eng->stream),
+           "filter bitmap H2D");
+  // selective: keep the compacted row list too (search_core's gather path)
+  if (f->allowed && f->allowed * kGatherDensityDen <= c->rows) {
+    VS_HIP(f->list.ensure(f->allowed * 4), "alloc filter row list");
+    const size_t sc = (size_t)vsk::compact_scratch_words((uint32_t)c->rows) * 4;
+    if (eng->gather_cnt.bytes < sc) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->gather_cnt.ensure(sc), "alloc compaction scratch");
+    }
+    VS_HIP(vsk::launch_compact_rows(f->bits.as<uint64_t>(), (uint32_t)c->rows,
+                                    f->list.as<uint32_t>(), eng->gather_cnt.as<uint32_t>(),
+                                    eng->stream),
+           "compact filter rows");
+  }
+  VS_HIP(hipStreamSynchronize(eng->stream), "filter sync");
+  *filter_id = eng->next_filter++;
+  eng->filters.emplace(*filter_id, std::move(f));
+  return VS_OK;
+}
+
+int vs_filter_drop(vs_engine* eng, uint64_t filter_id) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  auto it = eng->filters.find(filter_id);
+  if (it == eng->filters.end())
+    return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(hipStreamSynchronize(eng->stream), "sync");  // no search still reads it
+  eng->filters.erase(it);
+  return VS_OK;
+}
+
+int vs_search_filter_id(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+                        uint32_t dim, uint32_t k, uint64_t filter_id, float* out_scores,
+                        uint64_t* out_rows, uint32_t* out_count) {
+  if (!filter_id) return fail(VS_ERR_INVALID_ARG, "filter id 0");
+  return search_host(eng, coll, queries, nq, dim, k, nullptr, 0, out_scores, out_rows,
+                     out_count, filter_id);
 }
 
 int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uint32_t nq,

@@ -54,10 +54,11 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                        const uint32_t* rows = nullptr);
 // With `rows` (device, n_rows entries of local row indices) the scan gathers
 // those rows only (a selective filter) and `allow` is ignored.
-// Filter bitmap -> the allowed local rows (< n_rows), in arbitrary order, and
-// their count in *d_count (device). `rows` holds popcount(allow) entries.
+// Filter bitmap -> the allowed local rows (< n_rows), ascending. `rows`
+// holds popcount(allow) entries; `scratch` compact_scratch_words(n_rows) u32.
 hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t* rows,
-                               uint32_t* d_count, hipStream_t st);
+                               uint32_t* scratch, hipStream_t st);
+uint32_t compact_scratch_words(uint32_t n_rows);
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 

@@ -719,46 +719,101 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 #undef VS_GEMV_CASE
 }
 
-// Filter bitmap -> compacted list of the allowed local rows (< n_rows), for
-// the GATHER scans. One 64-row word per lane; a wave prefix sum of the
-// popcounts places each lane's rows and one atomic per wave reserves the
-// wave's range. The list order across waves is arbitrary: keys are totally
-// ordered by (score, row), so the scan result does not depend on it.
-__global__ __launch_bounds__(256) void compact_rows_kernel(const uint64_t* __restrict__ allow,
-                                                            uint32_t n_rows,
-                                                            uint32_t* __restrict__ rows,
-                                                            uint32_t* __restrict__ count) {
-  const int lane = threadIdx.x & 63;
+// Filter bitmap -> compacted list of the allowed local rows, ascending, for
+// the GATHER scans. Ascending order makes the list (and so every gathered
+// score: a row's position in its wave step decides its summation order) a
+// function of the bitmap alone, whichever way it was built. Three launches:
+// per-block popcounts of 256 words (16384 rows), an in-place exclusive scan
+// of those counts in one workgroup, then each block places its rows.
+constexpr int kCompactThreads = 256;
+
+__device__ __forceinline__ uint64_t compact_word(const uint64_t* __restrict__ allow,
+                                                 uint32_t n_rows, uint32_t wi) {
   const uint32_t nwords = (n_rows + 63) / 64;
-  const uint32_t wi = blockIdx.x * 256u + threadIdx.x;
   uint64_t w = wi < nwords ? allow[wi] : 0;
   if (wi == nwords - 1 && (n_rows & 63)) w &= (1ull << (n_rows & 63)) - 1;
-  const uint32_t c = (uint32_t)__popcll(w);
-  uint32_t inc = c;
+  return w;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(inc, off);
-    if (lane >= off) inc += t;
+    const uint32_t t = __shfl_up(v, off);
+    if (lane >= off) v += t;
   }
-  const uint32_t total = __shfl(inc, 63);
-  uint32_t base = 0;
-  if (lane == 63 && total) base = atomicAdd(count, total);
-  base = __shfl(base, 63);
-  uint32_t o = base + inc - c;
-  while (w) {
-    rows[o++] = wi * 64u + (uint32_t)(__ffsll((unsigned long long)w) - 1);
-    w &= w - 1;
+  return v;
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(
+    const uint64_t* __restrict__ allow, uint32_t n_rows, uint32_t* __restrict__ block_cnt) {
+  __shared__ uint32_t part[kCompactThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t c = (uint32_t)__popcll(compact_word(allow, n_rows, blockIdx.x * kCompactThreads + threadIdx.x));
+  const uint32_t t = wave_incl_scan(c, lane);
+  if (lane == 63) part[w] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sum = 0;
+    for (int v = 0; v < kCompactThreads / 64; ++v) sum += part[v];
+    block_cnt[blockIdx.x] = sum;
   }
 }
 
+// One workgroup: exclusive scan of block_cnt[0, n) in place, 256 at a time.
+__global__ __launch_bounds__(kCompactThreads) void compact_scan_kernel(uint32_t* __restrict__ block_cnt,
+                                                                       uint32_t n) {
+  __shared__ uint32_t part[kCompactThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < n; b0 += kCompactThreads) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t c = i < n ? block_cnt[i] : 0;
+    const uint32_t inc = wave_incl_scan(c, lane);
+    if (lane == 63) part[w] = inc;
+    __syncthreads();
+    uint32_t base = carry, tot = 0;
+    for (int v = 0; v < kCompactThreads / 64; ++v) {
+      if (v < w) base += part[v];
+      tot += part[v];
+    }
+    if (i < n) block_cnt[i] = base + inc - c;
+    carry += tot;
+    __syncthreads();  // part[] is rewritten by the next chunk
+  }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_rows_kernel(
+    const uint64_t* __restrict__ allow, uint32_t n_rows, const uint32_t* __restrict__ block_base,
+    uint32_t* __restrict__ rows) {
+  __shared__ uint32_t part[kCompactThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t wi = blockIdx.x * kCompactThreads + threadIdx.x;
+  uint64_t word = compact_word(allow, n_rows, wi);
+  const uint32_t c = (uint32_t)__popcll(word);
+  const uint32_t inc = wave_incl_scan(c, lane);
+  if (lane == 63) part[w] = inc;
+  __syncthreads();
+  uint32_t o = block_base[blockIdx.x] + inc - c;
+  for (int v = 0; v < w; ++v) o += part[v];
+  while (word) {
+    rows[o++] = wi * 64u + (uint32_t)(__ffsll((unsigned long long)word) - 1);
+    word &= word - 1;
+  }
+}
+
+uint32_t compact_scratch_words(uint32_t n_rows) {
+  return ((n_rows + 63) / 64 + kCompactThreads - 1) / kCompactThreads;
+}
+
 hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t* rows,
-                               uint32_t* d_count, hipStream_t st) {
+                               uint32_t* scratch, hipStream_t st) {
   if (n_rows == 0) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(d_count, 0, 4, st);
-  if (e != hipSuccess) return e;
-  const uint32_t nwords = (n_rows + 63) / 64;
-  hipLaunchKernelGGL(compact_rows_kernel, dim3((nwords + 255) / 256), dim3(256), 0, st, allow,
-                     n_rows, rows, d_count);
+  const uint32_t nb = compact_scratch_words(n_rows);
+  hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(kCompactThreads), 0, st, allow,
+                     n_rows, scratch);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kCompactThreads), 0, st, scratch, nb);
+  hipLaunchKernelGGL(compact_rows_kernel, dim3(nb), dim3(kCompactThreads), 0, st, allow, n_rows,
+                     scratch, rows);
   return hipGetLastError();
 }
 

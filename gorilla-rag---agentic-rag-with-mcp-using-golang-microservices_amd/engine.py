@@ -45,6 +45,7 @@ EXPORTS = (
     "vs_read_rows", "vs_search", "vs_search_keys", "vs_merge_keys",
     "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
+    "vs_filter_create", "vs_filter_drop", "vs_search_filter_id",
 )
 
 
@@ -95,6 +96,9 @@ def load_library(path: str = LIB_PATH):
         "vs_restore": ([vp, cp, cp], i32),
         "vs_checksum": ([vp, cp, ctypes.POINTER(u64)], i32),
         "vs_search_filtered": ([vp, cp, vp, u32, u32, u32, vp, u64, vp, vp, vp], i32),
+        "vs_filter_create": ([vp, cp, vp, u64, vp], i32),
+        "vs_filter_drop": ([vp, u64], i32),
+        "vs_search_filter_id": ([vp, cp, vp, u32, u32, u32, u64, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -258,6 +262,33 @@ class VectorEngine:
         count = np.zeros(nq, np.uint32)
         _check(self._L.vs_search_filtered(self._h, name.encode(), _p(q), nq, q.shape[1], k,
                                           _p(a), a.size, _p(scores), _p(rows), _p(count)))
+        return scores, rows, count
+
+    def filter_create(self, name: str, allow: np.ndarray) -> int:
+        """Uploads a filter bitmap (bool per row or packed words) once; returns
+        its id for search_filter_id (vs_filter_create)."""
+        a = np.asarray(allow)
+        if a.dtype == np.bool_:
+            a = pack_allow(a)
+        a = np.ascontiguousarray(a, np.uint64)
+        fid = ctypes.c_uint64()
+        _check(self._L.vs_filter_create(self._h, name.encode(), _p(a), a.size,
+                                        ctypes.byref(fid)))
+        return fid.value
+
+    def filter_drop(self, filter_id: int):
+        _check(self._L.vs_filter_drop(self._h, filter_id))
+
+    def search_filter_id(self, name: str, queries: np.ndarray, k: int, filter_id: int):
+        q = np.ascontiguousarray(queries, np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        scores = np.zeros((nq, k), np.float32)
+        rows = np.zeros((nq, k), np.uint64)
+        count = np.zeros(nq, np.uint32)
+        _check(self._L.vs_search_filter_id(self._h, name.encode(), _p(q), nq, q.shape[1], k,
+                                           filter_id, _p(scores), _p(rows), _p(count)))
         return scores, rows, count
 
     def search_keys(self, name: str, d_queries: int, nq: int, dim: int, k: int, d_keys: int,

@@ -170,6 +170,22 @@ int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, u
                        uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                        float* out_scores, uint64_t* out_rows, uint32_t* out_count);
 
+/* Device-resident filters: a filter the caller will reuse (the service caches
+ * one per canonical `filter` object) is uploaded once: the bitmap, its
+ * popcount and, when at most 1/8 of the rows are allowed, the compacted row
+ * list stay in HBM, so vs_search_filter_id ships no bitmap and builds no list
+ * per call. A filter is bound to the collection and its row count at
+ * creation: a search after rows were added fails with VS_ERR_INVALID_ARG
+ * (rebuild it). Bits are rows, not payloads: a caller whose payloads changed
+ * must rebuild it too. Ids are never reused within an engine. */
+int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
+                     uint64_t allow_words, uint64_t* filter_id);
+int vs_filter_drop(vs_engine* eng, uint64_t filter_id);
+/* vs_search_filtered with a filter made by vs_filter_create. */
+int vs_search_filter_id(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+                        uint32_t dim, uint32_t k, uint64_t filter_id, float* out_scores,
+                        uint64_t* out_rows, uint32_t* out_count);
+
 /* Device-pointer form for sharded callers. `d_queries` (nq x dim fp32) and
  * `d_keys` (nq x k uint64) are device pointers on this engine's device;
  * `stream` is a hipStream_t (NULL = the null stream). The work is ordered

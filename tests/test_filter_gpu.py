@@ -181,3 +181,47 @@ def test_filtered_gather_batches(engine, orc):
         bad = orc.check_topk(s, pos, c, s64, rows, cnt, resc, SCORE_RTOL)
         assert not bad, bad[:10]
     engine.drop_collection("fgbig")
+
+
+def test_device_resident_filters(engine, orc, pkg, fcorpus):
+    """vs_filter_create / vs_search_filter_id / vs_filter_drop: a filter kept
+    in HBM (bitmap, and the compacted row list when selective) gives exactly
+    what vs_search_filtered gives with the same bitmap, on the GEMV gather,
+    GEMV streamed and MFMA paths; it is bound to the collection's row count
+    and dies with vs_filter_drop."""
+    name, X = fcorpus
+    n = X.shape[0]
+    rng = np.random.default_rng(21)
+    Q = orc.generate(orc.SEED_QUERY, 808, 40, 768)
+    ids = []
+    for dens in (0.003, 0.1, 0.6, 0.0):
+        mask = rng.random(n) < dens
+        fid = engine.filter_create(name, mask)
+        assert fid not in ids
+        ids.append(fid)
+        for nq, k in ((1, 10), (1, 200), (40, 10), (3, 100)):
+            a = engine.search_filtered(name, Q[:nq], k, mask)
+            b = engine.search_filter_id(name, Q[:nq], k, fid)
+            assert all(np.array_equal(x, y) for x, y in zip(a, b)), (dens, nq, k)
+    for fid in ids:
+        engine.filter_drop(fid)
+    with pytest.raises(pkg.VSError):
+        engine.search_filter_id(name, Q[:1], 10, ids[0])  # dropped
+    with pytest.raises(pkg.VSError):
+        engine.filter_drop(ids[0])
+    with pytest.raises(pkg.VSError):
+        engine.filter_create(name, pkg.pack_allow(np.ones(n - 64, bool)))  # too short
+    # bound to the row count at creation
+    engine.create_collection("fres", 128, 0, 0)
+    base = orc.generate(orc.SEED_CORPUS, 0, 5000, 128)
+    engine.upsert("fres", np.arange(4000), base[:4000])
+    fid = engine.filter_create("fres", np.arange(4000) % 7 == 0)
+    s, r, c = engine.search_filter_id("fres", base[:2], 5, fid)
+    assert np.all(r % 7 == 0) and r[0, 0] == 0
+    with pytest.raises(pkg.VSError):
+        engine.search_filter_id(name, Q[:1], 10, fid)  # another collection
+    engine.upsert("fres", np.arange(4000, 5000), base[4000:])
+    with pytest.raises(pkg.VSError):
+        engine.search_filter_id("fres", base[:2], 5, fid)  # rows were added: stale
+    engine.filter_drop(fid)
+    engine.drop_collection("fres")

@@ -57,6 +57,24 @@ def main():
             row["stream_gbs"] = round(args.rows * args.dim * 2 / (scan * 1e-3) / 1e9, 1)
         out["densities"].append(row)
         print(json.dumps(row), file=sys.stderr, flush=True)
+    # the same single-query searches through a device-resident filter
+    # (vs_filter_create once, then vs_search_filter_id: no bitmap per call)
+    out["resident"] = []
+    for dens in (0.125, 0.01, 0.001):
+        fid = eng.filter_create("big", rng.random(args.rows) < dens)
+        for i in range(3):
+            eng.search_filter_id("big", Q[i], args.k, fid)
+        eng.timing(reset=True)
+        t0 = time.perf_counter()
+        for i in range(args.reps):
+            eng.search_filter_id("big", Q[i], args.k, fid)
+        wall = (time.perf_counter() - t0) / args.reps
+        tm = eng.timing(reset=True)
+        eng.filter_drop(fid)
+        row = {"density": dens, "wall_ms": round(wall * 1e3, 4),
+               "scan_ms": round(tm["scan_ms"], 4), "qps": round(1.0 / wall, 1)}
+        out["resident"].append(row)
+        print(json.dumps(row), file=sys.stderr, flush=True)
     # batches of 8 queries: the MFMA pass with the bitmap fused (dense
     # filters) or 8 gathered scans (selective filters, search_core's rule)
     out["batch8"] = []
