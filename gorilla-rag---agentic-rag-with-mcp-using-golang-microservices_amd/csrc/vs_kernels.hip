@@ -589,13 +589,18 @@ int device_cu_count() {
 
 static int gemv_kpl(uint32_t k) { return k <= 64 ? 1 : (k <= 128 ? 2 : 16); }
 
+constexpr uint32_t kGemvMinRowsPerWave = 16;
+
 struct GemvGrid {
   uint32_t nwg, rows_per_wave;
 };
 static GemvGrid gemv_grid(uint32_t n_rows, int rb) {
   const int cus = g_cu_count ? g_cu_count : device_cu_count();
   uint64_t want = (uint64_t)cus * 3;  // 3 x 8 waves per CU
-  const uint64_t by_rows = ((uint64_t)n_rows + kGemvWaves * 64 - 1) / (kGemvWaves * 64);
+  // small scans (small collections, gathered selective filters) are latency
+  // bound: spread them down to kGemvMinRowsPerWave rows per wave
+  const uint64_t by_rows =
+      ((uint64_t)n_rows + kGemvWaves * kGemvMinRowsPerWave - 1) / (kGemvWaves * kGemvMinRowsPerWave);
   if (want > by_rows) want = by_rows;
   if (want < 1) want = 1;
   const uint64_t waves = want * kGemvWaves;

@@ -75,6 +75,16 @@ def main():
                "scan_ms": round(tm["scan_ms"], 4), "qps": round(1.0 / wall, 1)}
         out["resident"].append(row)
         print(json.dumps(row), file=sys.stderr, flush=True)
+    # fixed cost of one host-API search (tiny collection, no filter)
+    eng.create_collection("tiny", args.dim, 1, 1, 1000)
+    eng.generate("tiny", 1000, orc.SEED_CORPUS)
+    for i in range(3):
+        eng.search("tiny", Q[i], args.k)
+    t0 = time.perf_counter()
+    for i in range(args.reps):
+        eng.search("tiny", Q[i], args.k)
+    out["tiny_unfiltered_wall_ms"] = round((time.perf_counter() - t0) / args.reps * 1e3, 4)
+    print(json.dumps({"tiny_unfiltered_wall_ms": out["tiny_unfiltered_wall_ms"]}), file=sys.stderr)
     # batches of 8 queries: the MFMA pass with the bitmap fused (dense
     # filters) or 8 gathered scans (selective filters, search_core's rule)
     out["batch8"] = []
