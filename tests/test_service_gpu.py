@@ -370,3 +370,50 @@ def test_filter_modes(pkg, svcmod, orc):
             eng.close()
     with pytest.raises(Exception):
         svcmod.VectorService(pkg.VectorEngine(device=0), {"collections": [], "filter": "maybe"})
+
+
+def test_filter_cache_eviction_and_resident_filters(pkg, svcmod, orc):
+    """"match" mode keeps one device-resident filter per cached filter; more
+    distinct filters than the cache holds (64) evict and drop them, repeated
+    filters reuse them, and an upsert that adds rows makes them stale. Every
+    reply must hold only points whose payload matches, best first, and equal
+    the oracle's top k over the matching points."""
+    n, dim, groups = 2600, 128, 70
+    X = orc.generate(43, 0, n, dim)
+    ids = _ids(n, seed=43)
+    pts = [{"id": ids[i], "vector": X[i].tolist(), "payload": {"g": i % groups}}
+           for i in range(n)]
+    Xp = orc.preprocess(X, True, False)
+    Q = orc.generate(orc.SEED_QUERY, 43, 3, dim)
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng, {"collections": [{"name": "c", "dim": dim}], "filter": "match"})
+    try:
+        assert _post(s, "/upsert", {"collection": "c", "points": pts})[0] == 200
+
+        grp = [i % groups for i in range(n)]
+
+        def check(g, qi, nrows):
+            st, body, _ = _post(s, "/search", {"collection": "c", "query": Q[qi].tolist(),
+                                               "top_k": 5, "filter": {"g": g}})
+            assert st == 200, body
+            got = [ids.index(r["id"]) for r in json.loads(body)["results"]]
+            idx = np.array([i for i in range(nrows) if grp[i] == g])
+            s32, s64, rr, cc = orc.search(np.ascontiguousarray(Xp[idx]), orc.preprocess(
+                Q[qi:qi + 1], True, False), 5)
+            assert got == idx[rr[0, :cc[0]].astype(np.int64)].tolist(), (g, qi)
+
+        for rnd in range(2):  # 70 distinct filters twice: evictions, then reuse
+            for g in range(groups):
+                check(g, (g + rnd) % 3, n)
+        extra = [{"id": str(uuid.UUID(int=(1 << 100) + i, version=4)), "vector": X[i].tolist(),
+                  "payload": {"g": i % groups}} for i in range(100)]
+        assert _post(s, "/upsert", {"collection": "c", "points": extra})[0] == 200
+        ids.extend(p["id"] for p in extra)
+        grp.extend(i % groups for i in range(100))
+        X2 = np.concatenate([X, X[:100]])
+        Xp = orc.preprocess(X2, True, False)
+        for g in (0, 5, 69):
+            check(g, 1, n + 100)
+    finally:
+        s.close()
+        eng.close()
