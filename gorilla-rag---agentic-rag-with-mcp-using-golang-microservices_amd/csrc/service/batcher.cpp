@@ -19,6 +19,7 @@ struct Batcher::Req {
   const std::string* coll;
   const float* q;
   uint32_t dim, k;
+  uint64_t filter_id;
   float* scores;
   uint64_t* rows;
   uint32_t* count;
@@ -43,9 +44,10 @@ Batcher::~Batcher() {
 }
 
 int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint32_t k,
-                    float* scores, uint64_t* rows, uint32_t* count, std::string* err) {
+                    float* scores, uint64_t* rows, uint32_t* count, std::string* err,
+                    uint64_t filter_id) {
   std::condition_variable done_cv;
-  Req r{&coll, q, dim, k, scores, rows, count};
+  Req r{&coll, q, dim, k, filter_id, scores, rows, count};
   r.cv = &done_cv;
   std::unique_lock<std::mutex> lk(mu_);
   if (stop_) {
@@ -81,7 +83,7 @@ void Batcher::run() {
     std::vector<Req*> batch;
     for (auto it = queue_.begin(); it != queue_.end() && batch.size() < opt_.max_batch;) {
       Req* r = *it;
-      if (*r->coll == *first->coll && r->dim == first->dim &&
+      if (*r->coll == *first->coll && r->dim == first->dim && r->filter_id == first->filter_id &&
           (r->k > kMfmaMaxK) == (first->k > kMfmaMaxK)) {
         batch.push_back(r);
         it = queue_.erase(it);
@@ -100,15 +102,17 @@ void Batcher::run() {
 }
 
 void Batcher::execute(std::vector<Req*>& batch) {
-  // group: collection, dim, k class (MFMA-eligible or not); arrival order kept
-  std::map<std::tuple<std::string, uint32_t, bool>, std::vector<Req*>> groups;
-  for (Req* r : batch) groups[{*r->coll, r->dim, r->k > kMfmaMaxK}].push_back(r);
+  // group: collection, dim, filter, k class (MFMA-eligible or not); arrival
+  // order kept
+  std::map<std::tuple<std::string, uint32_t, uint64_t, bool>, std::vector<Req*>> groups;
+  for (Req* r : batch) groups[{*r->coll, r->dim, r->filter_id, r->k > kMfmaMaxK}].push_back(r);
   std::vector<float> q, sc;
   std::vector<uint64_t> rw;
   std::vector<uint32_t> cn;
   for (auto& kv : groups) {
     const std::string& coll = std::get<0>(kv.first);
     const uint32_t dim = std::get<1>(kv.first);
+    const uint64_t fid = std::get<2>(kv.first);
     auto& reqs = kv.second;
     for (size_t b0 = 0; b0 < reqs.size(); b0 += opt_.max_batch) {
       const size_t nq = std::min<size_t>(opt_.max_batch, reqs.size() - b0);
@@ -120,8 +124,11 @@ void Batcher::execute(std::vector<Req*>& batch) {
       sc.resize(nq * kmax);
       rw.resize(nq * kmax);
       cn.resize(nq);
-      const int rc = vs_search(eng_, coll.c_str(), q.data(), (uint32_t)nq, dim, kmax, sc.data(),
-                               rw.data(), cn.data());
+      const int rc =
+          fid ? vs_search_filter_id(eng_, coll.c_str(), q.data(), (uint32_t)nq, dim, kmax, fid,
+                                    sc.data(), rw.data(), cn.data())
+              : vs_search(eng_, coll.c_str(), q.data(), (uint32_t)nq, dim, kmax, sc.data(),
+                          rw.data(), cn.data());
       const std::string err = rc == VS_OK ? std::string() : std::string(vs_last_error());
       for (size_t i = 0; i < nq; ++i) {
         Req* r = reqs[b0 + i];

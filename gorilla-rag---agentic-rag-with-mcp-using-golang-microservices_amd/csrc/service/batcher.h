@@ -22,6 +22,11 @@
 // idle, up to max_batch under load), a lone request waits for nothing, and
 // with several collections each call finds its collection's whole backlog.
 // max_wait_us > 0 adds a linger before a non-full batch.
+//
+// Filtered requests ("filter":"match") carry the id of their device-resident
+// filter (vs_filter_create) and are grouped by it too: requests sharing a
+// filter become one vs_search_filter_id call (the MFMA pass with the bitmap
+// fused for dense filters, per-query gathers for selective ones).
 #pragma once
 #include <condition_variable>
 #include <cstdint>
@@ -58,8 +63,9 @@ class Batcher {
   // Blocks until the request's batch ran. Same contract as vs_search for one
   // query of `dim` floats: scores / rows hold k entries, *count the valid ones.
   // On failure returns the engine's status with its message in *err.
+  // `filter_id` != 0: vs_search_filter_id semantics with that filter.
   int search(const std::string& coll, const float* q, uint32_t dim, uint32_t k, float* scores,
-             uint64_t* rows, uint32_t* count, std::string* err);
+             uint64_t* rows, uint32_t* count, std::string* err, uint64_t filter_id = 0);
 
   Stats stats();
   const Options& options() const { return opt_; }

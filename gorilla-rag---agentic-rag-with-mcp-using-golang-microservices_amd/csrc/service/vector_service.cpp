@@ -566,12 +566,16 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   int rc;
   std::string err;
   if (svc->filter_match && req.filter.kind == Json::Object && !req.filter.obj.empty()) {
-    // filtered searches carry their own mask: one engine call each
+    // filtered searches: through the batcher with the other requests of the
+    // same resident filter, or directly
     auto f = filter_mask(svc->eng, req.collection, *cs, req.filter);
-    rc = f.device_id ? vs_search_filter_id(svc->eng, req.collection.c_str(), req.query.data(),
-                                           1, cs->dim, (uint32_t)k, f.device_id, scores.data(),
-                                           hit_rows.data(), &count)
-                     : VS_ERR_NOT_FOUND;
+    rc = VS_ERR_NOT_FOUND;
+    if (f.device_id && svc->batcher)
+      rc = svc->batcher->search(req.collection, req.query.data(), cs->dim, (uint32_t)k,
+                                scores.data(), hit_rows.data(), &count, &err, f.device_id);
+    else if (f.device_id)
+      rc = vs_search_filter_id(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
+                               (uint32_t)k, f.device_id, scores.data(), hit_rows.data(), &count);
     if (rc != VS_OK)  // not resident, or evicted by a concurrent request
       rc = vs_search_filtered(svc->eng, req.collection.c_str(), req.query.data(), 1, cs->dim,
                               (uint32_t)k, f.mask->data(), f.mask->size(), scores.data(),

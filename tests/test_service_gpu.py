@@ -417,3 +417,63 @@ def test_filter_cache_eviction_and_resident_filters(pkg, svcmod, orc):
     finally:
         s.close()
         eng.close()
+
+
+def test_batcher_groups_filtered_requests(pkg, svcmod, orc):
+    """"match" mode with batching: concurrent requests that share a filter go
+    to the engine together (one vs_search_filter_id call per filter group:
+    the MFMA pass with the bitmap fused for a dense filter, gathers for a
+    selective one), and each reply is still its own exact top k over the
+    matching points."""
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng, dict(_BATCH_CFG, filter="match",
+                                       batching={"max_wait_us": 50_000}))
+    try:
+        n = 4000
+        X = orc.generate(47, 0, n, 768)
+        ids = _ids(n, seed=47)
+        for lo in range(0, n, 500):
+            st, body, _ = _post(s, "/upsert", {"collection": "b16", "points": [
+                {"id": ids[i], "vector": X[i].tolist(), "payload": {"g": i % 2, "h": i % 40}}
+                for i in range(lo, min(n, lo + 500))]})
+            assert st == 200, body
+        Xp = orc.preprocess(X, True, True)
+        flts = [{"g": 1}, {"h": 7}, {"g": 0, "h": 4}]
+        preds = [lambda i: i % 2 == 1, lambda i: i % 40 == 7, lambda i: i % 2 == 0 and i % 40 == 4]
+        nreq = 48
+        Q = orc.generate(orc.SEED_QUERY, 700, nreq, 768)
+        ks = [1 + (5 * i) % 30 for i in range(nreq)]
+        replies = [None] * nreq
+        for f in flts:  # build (and make resident) every filter before the burst
+            assert _post(s, "/search", {"collection": "b16", "query": Q[0].tolist(),
+                                        "top_k": 1, "filter": f})[0] == 200
+        before = s.stats()
+        gate = threading.Barrier(nreq)
+
+        def client(i):
+            gate.wait()
+            replies[i] = _post(s, "/search", {"collection": "b16", "query": Q[i].tolist(),
+                                              "top_k": ks[i], "filter": flts[i % 3]})
+
+        th = [threading.Thread(target=client, args=(i,)) for i in range(nreq)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for i in range(nreq):
+            st, body, _ = replies[i]
+            assert st == 200, body
+            res = json.loads(body)["results"]
+            rows = [ids.index(r["id"]) for r in res]
+            idx = np.array([j for j in range(n) if preds[i % 3](j)])
+            s32, s64, rr, cc = orc.search(np.ascontiguousarray(Xp[idx]), orc.preprocess(
+                Q[i:i + 1], True, True), ks[i])
+            exp = idx[rr[0, :cc[0]].astype(np.int64)].tolist()
+            assert rows == exp, i
+        after = s.stats()
+        calls = after["engine_calls"] - before["engine_calls"]
+        reqs = after["requests"] - before["requests"]
+        assert reqs == nreq and calls < reqs, (before, after)
+    finally:
+        s.close()
+        eng.close()
