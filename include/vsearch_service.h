@@ -40,10 +40,12 @@ typedef struct vsvc vsvc;
  *  "filter":"ignore"|"match"}.
  * "filter":"ignore" (default) keeps the reference's behaviour: the request's
  * `filter` is decoded and dropped (main.go:30 vs :249-254). "match" applies
- * it as a pre-mask fused into the scan (vs_search_filtered): a point is
- * eligible when its payload holds every filter key with an equal JSON value.
- * Existing collections are reused. Batching (on by default) coalesces
- * concurrent /search requests into one engine call per collection
+ * it as a pre-mask (a point is eligible when its payload holds every filter
+ * key with an equal JSON value); each distinct filter is cached as a
+ * device-resident filter (vs_filter_create) until the next upsert, and
+ * searched with vs_search_filter_id. Existing collections are reused.
+ * Batching (on by default) coalesces concurrent /search requests into one
+ * engine call per collection (and per filter, for filtered requests)
  * (csrc/service/batcher.h); each request still gets exactly its own top k. */
 int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out);
 void vsvc_close(vsvc* svc);
