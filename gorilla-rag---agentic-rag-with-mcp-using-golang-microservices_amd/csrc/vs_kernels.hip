@@ -2166,6 +2166,28 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   // hundreds of keys here (a weak bound over many short lists) and paid a
   // block-wide bitonic sort for them.
   const uint64_t total0 = (uint64_t)L * kin;
+  // Few keys (cross-shard merges: P x k; small collections): one key per
+  // thread, and each key's output slot is its rank, the number of keys above
+  // it (a loop of LDS broadcast reads; keys are unique, 0 = empty). No
+  // shuffle rounds: P = 8, k = 10 was 10 + 10 dependent wave-max rounds.
+  if (total0 <= (uint64_t)kMergeThreads) {
+    const uint32_t t = threadIdx.x, tot = (uint32_t)total0;
+    uint64_t x = 0;
+    if (t < tot) {
+      const uint32_t l = t / kin, j = t - l * kin;
+      x = lists[l * lstride + q * qstride + j];
+    }
+    buf[t] = x;
+    __syncthreads();
+    if (x != 0) {
+      uint32_t rank = 0;
+      for (uint32_t i = 0; i < tot; ++i) rank += buf[i] > x ? 1u : 0u;
+      if (rank < k) out[(size_t)q * k + rank] = x;
+    }
+    const uint32_t nz = (uint32_t)__syncthreads_count(x != 0);  // also: buf reads done
+    for (uint32_t r = nz + t; r < k; r += kMergeThreads) out[(size_t)q * k + r] = 0;
+    return;
+  }
   if (total0 <= (uint64_t)kMergeThreads * kMergeHeld && k <= 32) {
     uint64_t x[kMergeHeld];
     // every load issued unconditionally (clamped index), all in flight at
