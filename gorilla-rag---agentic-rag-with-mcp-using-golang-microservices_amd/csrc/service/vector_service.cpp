@@ -543,6 +543,10 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   SearchRequest req;
   if (!decode_search(body, len, &req).empty()) return error_json("Invalid request body", 400);
   if (req.top_k == 0) req.top_k = 5;
+  // The reference sends Limit: uint64(req.TopK), so a negative top_k wraps to
+  // a limit near 2^64 whose Qdrant reply is unpinned; here it is refused as a
+  // bad request instead of returning every row.
+  if (req.top_k < 0) return error_json("top_k must not be negative", 400);
   const uint64_t limit = (uint64_t)req.top_k;  // Limit: uint64(req.TopK)
 
   auto cs = svc->find(req.collection);
@@ -770,6 +774,64 @@ int vsvc_snapshot(vsvc* svc, const char* dir) {
   return VS_OK;
 }
 
+namespace {
+// A parsed, fully checked sidecar (vsvc_snapshot's <coll>.points.json).
+struct Sidecar {
+  uint64_t bulk = 0, bulk_tag = 0;
+  std::vector<std::pair<uint64_t, Json>> bulk_payload;
+  std::vector<std::string> uuids;  // canonical; row bulk + i
+  std::vector<Json> payloads;
+};
+
+bool json_uint(const Json* v, uint64_t max, uint64_t* out) {
+  if (!v || v->kind != Json::Number || !(v->num >= 0) || v->num > (double)max ||
+      v->num != (double)(uint64_t)v->num)
+    return false;
+  *out = (uint64_t)v->num;
+  return true;
+}
+
+// Every field is checked before anything is changed: integral, in-range
+// counters; payload rows inside the bulk range; every point a [uuid, object]
+// pair with a canonical, unique UUID that is not one of the bulk ids.
+bool parse_sidecar(const std::string& text, Sidecar* sc) {
+  Json side;
+  std::string err;
+  if (!vsjson::parse(text.data(), text.size(), &side, &err) || side.kind != Json::Object)
+    return false;
+  const Json* jbp = side.get("bulk_payload");
+  const Json* jp = side.get("points");
+  if (!json_uint(side.get("bulk"), (1ull << 40) - 1, &sc->bulk) ||
+      !json_uint(side.get("bulk_tag"), (1ull << 48) - 1, &sc->bulk_tag) || !jbp ||
+      jbp->kind != Json::Array || !jp || jp->kind != Json::Array)
+    return false;
+  if (sc->bulk && !(sc->bulk_tag & 1)) return false;  // vsvc_bulk_generate sets bit 0
+  for (const auto& e : jbp->arr) {
+    uint64_t row = 0;
+    if (e.kind != Json::Array || e.arr.size() != 2 || !json_uint(&e.arr[0], sc->bulk - 1, &row) ||
+        sc->bulk == 0 || e.arr[1].kind != Json::Object)
+      return false;
+    sc->bulk_payload.emplace_back(row, e.arr[1]);
+  }
+  std::unordered_map<std::string, uint64_t> seen;
+  CollState probe;
+  probe.bulk = sc->bulk;
+  probe.bulk_tag = sc->bulk_tag;
+  for (const auto& e : jp->arr) {
+    std::string canon;
+    uint64_t r;
+    if (e.kind != Json::Array || e.arr.size() != 2 || e.arr[0].kind != Json::String ||
+        e.arr[1].kind != Json::Object || !canonical_uuid(e.arr[0].str, &canon) ||
+        canon != e.arr[0].str || bulk_row(probe, canon, &r) ||
+        !seen.emplace(canon, sc->uuids.size()).second)
+      return false;
+    sc->uuids.push_back(canon);
+    sc->payloads.push_back(e.arr[1]);
+  }
+  return true;
+}
+}  // namespace
+
 int vsvc_restore(vsvc* svc, const char* dir) {
   if (!svc || !dir) return VS_ERR_INVALID_ARG;
   for (const std::string& name : svc->listed) {
@@ -782,16 +844,8 @@ int vsvc_restore(vsvc* svc, const char* dir) {
     size_t n;
     while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, n);
     std::fclose(f);
-    Json side;
-    std::string err;
-    if (!vsjson::parse(text.data(), text.size(), &side, &err)) return VS_ERR_IO;
-    const Json* jb = side.get("bulk");
-    const Json* jt = side.get("bulk_tag");
-    const Json* jbp = side.get("bulk_payload");
-    const Json* jp = side.get("points");
-    if (!jb || jb->kind != Json::Number || !jt || jt->kind != Json::Number || !jbp ||
-        jbp->kind != Json::Array || !jp || jp->kind != Json::Array)
-      return VS_ERR_IO;
+    Sidecar sc;
+    if (!parse_sidecar(text, &sc)) return VS_ERR_IO;  // nothing touched yet
     std::unique_lock<std::shared_mutex> wl(cs->mu);
     if (cs->nrows() != 0) return VS_ERR_EXISTS;  // restore only into an empty service
     uint32_t dim = 0;
@@ -802,26 +856,24 @@ int vsvc_restore(vsvc* svc, const char* dir) {
     rc = vs_restore(svc->eng, name.c_str(), (base + ".vsnap").c_str());
     uint64_t rows = 0;
     uint32_t rdim = 0;
-    if (rc == VS_OK) rc = vs_collection_info(svc->eng, name.c_str(), &rdim, &rows, nullptr, nullptr);
-    const uint64_t bulk = (uint64_t)jb->num;
-    if (rc == VS_OK && (rdim != dim || rows != bulk + jp->arr.size())) rc = VS_ERR_IO;
+    int rmetric = 0, rdtype = 0;
+    if (rc == VS_OK)
+      rc = vs_collection_info(svc->eng, name.c_str(), &rdim, &rows, &rmetric, &rdtype);
+    if (rc == VS_OK && (rdim != dim || rmetric != metric || rdtype != dtype ||
+                        rows != sc.bulk + sc.uuids.size()))
+      rc = VS_ERR_IO;
     if (rc != VS_OK) {  // leave the collection as it was: empty
       (void)vs_collection_drop(svc->eng, name.c_str());
       (void)vs_collection_create(svc->eng, name.c_str(), dim, metric, dtype, 0, 0);
       return rc;
     }
-    cs->bulk = bulk;
-    cs->bulk_tag = (uint64_t)jt->num;
-    for (const auto& e : jbp->arr)
-      if (e.kind == Json::Array && e.arr.size() == 2) cs->bulk_payload[(uint64_t)e.arr[0].num] = e.arr[1];
-    cs->uuid_of.reserve(jp->arr.size());
-    cs->payload_of.reserve(jp->arr.size());
-    for (const auto& e : jp->arr) {
-      if (e.kind != Json::Array || e.arr.size() != 2 || e.arr[0].kind != Json::String) return VS_ERR_IO;
-      cs->row_of[e.arr[0].str] = cs->bulk + cs->uuid_of.size();
-      cs->uuid_of.push_back(e.arr[0].str);
-      cs->payload_of.push_back(e.arr[1]);
-    }
+    cs->bulk = sc.bulk;
+    cs->bulk_tag = sc.bulk_tag;
+    for (auto& e : sc.bulk_payload) cs->bulk_payload[e.first] = std::move(e.second);
+    cs->row_of.reserve(sc.uuids.size());
+    for (size_t i = 0; i < sc.uuids.size(); ++i) cs->row_of[sc.uuids[i]] = sc.bulk + i;
+    cs->uuid_of = std::move(sc.uuids);
+    cs->payload_of = std::move(sc.payloads);
     ++cs->version;
   }
   return VS_OK;

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -66,6 +67,7 @@ struct DevBuf {
 
 struct Collection {
   std::string name;
+  uint64_t gen = 0;  // unique per created collection (never reused in a process)
   uint32_t dim = 0;
   int metric = VS_METRIC_COSINE;
   int dtype = VS_DTYPE_F32;
@@ -106,6 +108,7 @@ struct vs_engine {
   // device-resident filters (vs_filter_create), guarded by work_mu
   struct DevFilter {
     std::string coll;
+    uint64_t coll_gen = 0;           // Collection::gen it was built for
     uint64_t rows = 0, allowed = 0;  // collection rows it was built over
     DevBuf bits, list;               // bitmap; compacted rows when selective
   };
@@ -123,6 +126,8 @@ struct vs_engine {
 };
 
 namespace {
+
+std::atomic<uint64_t> g_coll_gen{1};
 
 std::shared_ptr<Collection> find_coll(vs_engine* eng, const char* name) {
   std::lock_guard<std::mutex> g(eng->map_mu);
@@ -252,6 +257,22 @@ struct PinnedPair {  // two staging buffers: one in flight, one on disk I/O
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  }
+};
+
+// A snapshot's own stream and checksum word (vs_snapshot runs outside work_mu).
+struct SnapStream {
+  hipStream_t st = nullptr;
+  uint64_t* sum = nullptr;
+  hipError_t open() {
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&sum, 8);
+    return e;
+  }
+  ~SnapStream() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (sum) (void)hipFree(sum);
+    if (st) (void)hipStreamDestroy(st);
   }
 };
 
@@ -589,6 +610,7 @@ int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim, int met
   VS_HIP(set_dev(eng), "hipSetDevice");
   auto c = std::make_shared<Collection>();
   c->name = name;
+  c->gen = g_coll_gen.fetch_add(1);
   c->dim = dim;
   c->metric = metric;
   c->dtype = dtype;
@@ -644,6 +666,10 @@ int vs_collection_drop(vs_engine* eng, const char* name) {
   (void)set_dev(eng);
   VS_HIP(use_stream(eng, eng->own), "stream order");
   (void)hipStreamSynchronize(eng->stream);
+  // the collection's resident filters go with it (their HBM, and no later
+  // collection of the same name and row count can pick them up)
+  for (auto it = eng->filters.begin(); it != eng->filters.end();)
+    it = it->second->coll_gen == c->gen ? eng->filters.erase(it) : std::next(it);
   return VS_OK;  // memory released with the last reference
 }
 
@@ -835,7 +861,7 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
     if (it == eng->filters.end())
       return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
     df = it->second.get();
-    if (df->coll != coll || df->rows != c->rows)
+    if (df->coll_gen != c->gen || df->rows != c->rows)
       return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
                                           " was built for another collection state");
   }
@@ -907,6 +933,7 @@ int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
   VS_HIP(use_stream(eng, eng->own), "stream order");
   auto f = std::make_unique<vs_engine::DevFilter>();
   f->coll = coll;
+  f->coll_gen = c->gen;
   f->rows = c->rows;
   f->allowed = popcount_rows(allow, c->rows);
   VS_HIP(f->bits.ensure(std::max<uint64_t>(nw, 1) * 8), "alloc filter bitmap");
@@ -1020,10 +1047,15 @@ int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
                                             " not found");
-  std::shared_lock<std::shared_mutex> rl(c->mu);  // upserts wait, searches proceed
-  std::lock_guard<std::mutex> g(eng->work_mu);
+  // Upserts wait (reader lock: the rows and their buffer stay put); searches
+  // and every other engine call proceed. The snapshot touches none of the
+  // engine's scratch or its stream: it runs on a stream and an 8-byte
+  // checksum buffer of its own, so it never takes work_mu, and a multi-GB
+  // disk write does not hold up /search or /health.
+  std::shared_lock<std::shared_mutex> rl(c->mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
-  VS_HIP(use_stream(eng, eng->own), "stream order");
+  SnapStream ss;
+  VS_HIP(ss.open(), "snapshot stream");
   SnapHeader h{};
   std::memcpy(h.magic, kSnapMagic, 8);
   h.version = 1;
@@ -1035,8 +1067,10 @@ int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
   h.rows = c->rows;
   h.row_base = c->row_base;
   h.data_bytes = c->rows * c->row_bytes();
-  int rc = device_checksum(eng, *c, &h.data_checksum);
-  if (rc != VS_OK) return rc;
+  VS_HIP(vsk::launch_checksum(c->data, h.data_bytes, ss.sum, ss.st), "checksum");
+  VS_HIP(hipMemcpyAsync(&h.data_checksum, ss.sum, 8, hipMemcpyDeviceToHost, ss.st),
+         "checksum D2H");
+  VS_HIP(hipStreamSynchronize(ss.st), "checksum sync");
   h.header_checksum = header_sum(h);
   const std::string tmp = std::string(path) + ".tmp";
   FileCloser fc;
@@ -1051,18 +1085,18 @@ int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
   uint64_t nchunks = (h.data_bytes + chunk - 1) / chunk;
   if (nchunks)
     VS_HIP(hipMemcpyAsync(pin.p[0], src, std::min<uint64_t>(chunk, h.data_bytes),
-                          hipMemcpyDeviceToHost, eng->stream),
+                          hipMemcpyDeviceToHost, ss.st),
            "snapshot D2H");
   for (uint64_t i = 0; i < nchunks; ++i) {
     const uint64_t off = i * chunk, n = std::min<uint64_t>(chunk, h.data_bytes - off);
-    VS_HIP(hipStreamSynchronize(eng->stream), "snapshot sync");
+    VS_HIP(hipStreamSynchronize(ss.st), "snapshot sync");
     if (i + 1 < nchunks)
       VS_HIP(hipMemcpyAsync(pin.p[(i + 1) & 1], src + off + n,
                             std::min<uint64_t>(chunk, h.data_bytes - off - n),
-                            hipMemcpyDeviceToHost, eng->stream),
+                            hipMemcpyDeviceToHost, ss.st),
              "snapshot D2H");
     if (std::fwrite(pin.p[i & 1], 1, n, fc.f) != n) {
-      (void)hipStreamSynchronize(eng->stream);
+      (void)hipStreamSynchronize(ss.st);
       return fail(VS_ERR_IO, "write failed: " + tmp);
     }
   }

@@ -2148,6 +2148,32 @@ __device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
   }
 }
 
+// buf[0, c) sorted descending -> its distinct non-zero keys moved to the
+// front, in order (wave 0, 64 keys per round, in place: a key is written at
+// or before the slot it was read from, after its whole round was read).
+// Returns the number of distinct keys to every thread (through cnt_sh).
+__device__ __forceinline__ uint32_t dedupe_sorted(uint64_t* buf, uint32_t c, uint32_t& cnt_sh) {
+  if (threadIdx.x < 64) {
+    const int lane = (int)threadIdx.x;
+    uint32_t w = 0;
+    uint64_t prev = 0;  // the (original) key before this round; keys are non-zero
+    for (uint32_t b = 0; b < c; b += 64) {
+      const uint32_t i = b + (uint32_t)lane;
+      const uint64_t x = i < c ? buf[i] : 0ull;
+      uint64_t p = shfl_up64(x);
+      if (lane == 0) p = prev;
+      prev = readlane64(x, 63);
+      const bool keep = x != 0 && x != p;
+      const uint64_t bal = __ballot(keep);
+      if (keep) buf[w + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = x;
+      w += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) cnt_sh = w;
+  }
+  __syncthreads();
+  return cnt_sh;
+}
+
 // Top-k of query q over L lists (merge_keys_kernel; also select_slab_kernel's
 // overflow fallback). buf holds >= kMergeCap keys; red / cnt are the
 // caller's shared scratch. One workgroup of kMergeThreads threads.
@@ -2160,15 +2186,16 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   // Fast path (single-query GEMV merges and shard merges at k <= 32): all
   // L * kin keys fit kMergeHeld per thread, so they are read in ONE memory
   // round trip, and the top k is taken by tournament: each wave extracts its
-  // k largest (wave max by xor-shuffles, k rounds; keys are unique, 0 =
-  // empty), then wave 0 extracts the k largest of the 8 waves' winners. The
+  // k largest (wave max by xor-shuffles, k rounds; 0 = empty; every copy of
+  // an extracted key is dropped, so a key listed twice comes out once), then
+  // wave 0 extracts the k largest of the 8 waves' winners. The
   // general path below filters against max_l list_l[k-1], which admitted
   // hundreds of keys here (a weak bound over many short lists) and paid a
   // block-wide bitonic sort for them.
   const uint64_t total0 = (uint64_t)L * kin;
   // Few keys (cross-shard merges: P x k; small collections): one key per
   // thread, and each key's output slot is its rank, the number of keys above
-  // it (a loop of LDS broadcast reads; keys are unique, 0 = empty). No
+  // it among the distinct keys (a loop of LDS broadcast reads; 0 = empty). No
   // shuffle rounds: P = 8, k = 10 was 10 + 10 dependent wave-max rounds.
   if (total0 <= (uint64_t)kMergeThreads) {
     const uint32_t t = threadIdx.x, tot = (uint32_t)total0;
@@ -2179,12 +2206,19 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
     }
     buf[t] = x;
     __syncthreads();
-    if (x != 0) {
+    // a key listed more than once (overlapping or replicated lists) is kept
+    // at its first position only, so ranks are distinct and every slot below
+    // the number of distinct keys is written
+    bool first = x != 0;
+    for (uint32_t i = 0; first && i < t; ++i) first = buf[i] != x;
+    buf[kMergeThreads + t] = first ? x : 0ull;
+    __syncthreads();
+    if (first) {
       uint32_t rank = 0;
-      for (uint32_t i = 0; i < tot; ++i) rank += buf[i] > x ? 1u : 0u;
+      for (uint32_t i = 0; i < tot; ++i) rank += buf[kMergeThreads + i] > x ? 1u : 0u;
       if (rank < k) out[(size_t)q * k + rank] = x;
     }
-    const uint32_t nz = (uint32_t)__syncthreads_count(x != 0);  // also: buf reads done
+    const uint32_t nz = (uint32_t)__syncthreads_count(first);  // also: buf reads done
     for (uint32_t r = nz + t; r < k; r += kMergeThreads) out[(size_t)q * k + r] = 0;
     return;
   }
@@ -2220,7 +2254,7 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
     for (uint32_t r = 0; r < k; ++r) {
       const uint64_t wm = wave_max(lm);
       if (lane == 0) buf[w * 32 + r] = wm;
-      if (wm != 0 && lm == wm) {  // the one lane holding it (keys are unique)
+      if (wm != 0 && lm == wm) {  // every lane holding it drops all its copies
 #pragma unroll
         for (int u = 0; u < kMergeHeld; ++u) x[u] = x[u] == wm ? 0ull : x[u];
         lm = lane_max();
@@ -2302,7 +2336,8 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
       for (int i = (int)c + threadIdx.x; i < p2; i += kMergeThreads) buf[i] = 0;
       __syncthreads();
       bitonic_sort_desc(buf, p2);
-      nR = c < k ? c : k;
+      const uint32_t u = dedupe_sorted(buf, c, cnt);
+      nR = u < k ? u : k;
       if (nR == k) {
         const uint64_t kth = buf[k - 1];
         thr = kth > thr ? kth : thr;

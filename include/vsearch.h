@@ -197,7 +197,10 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries,
 
 /* Merges `n_lists` per-shard key lists into the global top-k on the device:
  * d_lists is [n_lists][nq][k_in] (e.g. the result of an all-gather of
- * vs_search_keys outputs); d_out_keys is [nq][k]. */
+ * vs_search_keys outputs); d_out_keys is [nq][k]. Each list is sorted
+ * descending without repeats, 0-padded (as vs_search_keys writes it). A key
+ * found in more than one list (overlapping or replicated shards) is returned
+ * once; slots past the number of distinct non-zero keys hold 0. */
 int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists,
                   uint32_t nq, uint32_t k_in, uint32_t k, uint64_t* d_out_keys,
                   void* stream);

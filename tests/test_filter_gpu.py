@@ -224,4 +224,13 @@ def test_device_resident_filters(engine, orc, pkg, fcorpus):
     with pytest.raises(pkg.VSError):
         engine.search_filter_id("fres", base[:2], 5, fid)  # rows were added: stale
     engine.filter_drop(fid)
+    # a filter dies with its collection: after a drop and a re-create with
+    # the same name and row count its id is gone
+    fid = engine.filter_create("fres", np.arange(5000) % 3 == 0)
+    engine.drop_collection("fres")
+    engine.create_collection("fres", 128, 0, 0)
+    engine.upsert("fres", np.arange(5000), base)
+    with pytest.raises(pkg.VSError) as ei:
+        engine.search_filter_id("fres", base[:2], 5, fid)
+    assert ei.value.code == -2  # not found: freed with the dropped collection
     engine.drop_collection("fres")

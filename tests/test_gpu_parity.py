@@ -445,3 +445,47 @@ def test_scan_timing(orc, sample, expect):
             eng.search("t", Q, 10)
         t = eng.timing(reset=True)
         assert t["scan_n"] == expect and t["scan_ms"] > 0
+
+
+_MERGE_DUP = r"""
+import sys, json
+sys.path.insert(0, ROOT)
+import numpy as np, torch
+import __graft_entry__ as ge
+pkg = ge.load_package()
+eng = pkg.VectorEngine(device=0)
+rng = np.random.default_rng(5)
+bad = []
+# (lists, k_in, k, distinct keys): rank path (<= 512 keys), tournament path
+# (<= 8192 keys, k <= 32), general path (k > 32)
+for L, kin, k, nd in ((8, 10, 10, 6), (8, 10, 64, 30), (40, 100, 20, 15), (40, 100, 20, 300),
+                      (12, 100, 100, 50), (12, 100, 100, 700), (100, 100, 100, 2000)):
+    nq = 3
+    pool = np.unique(rng.integers(1 << 40, 1 << 62, size=nd * 2, dtype=np.uint64))[:nd]
+    lists = np.zeros((L, nq, kin), np.uint64)
+    for l in range(L):
+        for q in range(nq):
+            m = min(kin, int(rng.integers(0, kin + 1)), nd)
+            pick = np.sort(rng.choice(pool, size=m, replace=False))[::-1]
+            lists[l, q, :m] = pick
+    d = torch.from_numpy(lists.view(np.int64)).cuda()
+    out = torch.full((nq, k), 12345, dtype=torch.int64, device="cuda")  # poisoned
+    st = torch.cuda.current_stream().cuda_stream
+    eng.merge_keys(d.data_ptr(), L, nq, kin, k, out.data_ptr(), st)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    for q in range(nq):
+        u = np.unique(lists[:, q, :][lists[:, q, :] != 0])[::-1]
+        want = np.zeros(k, np.uint64)
+        want[:min(k, u.size)] = u[:k]
+        if not np.array_equal(got[q], want):
+            bad.append([L, kin, k, nd, q, got[q][:8].tolist(), want[:8].tolist()])
+print(json.dumps({"bad": bad[:5]}))
+"""
+
+
+def test_merge_dedupes_and_zero_fills():
+    """vs_merge_keys with keys repeated across lists (overlapping shards), fewer
+    distinct keys than k and a poisoned output: each key once, the rest 0, on
+    the rank, tournament and general paths."""
+    assert _run_py(_MERGE_DUP)["bad"] == []

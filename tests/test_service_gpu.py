@@ -477,3 +477,13 @@ def test_batcher_groups_filtered_requests(pkg, svcmod, orc):
     finally:
         s.close()
         eng.close()
+
+
+def test_negative_top_k_is_a_bad_request(service):
+    """uint64(req.TopK) would wrap a negative top_k to a limit near 2^64 (its
+    Qdrant reply is unpinned); the mirror answers 400."""
+    q = [0.1] * 768
+    st, body, _ = _post(service, "/search", {"collection": "kyc_docs", "query": q, "top_k": -3})
+    assert (st, body) == (400, b'{"error":"top_k must not be negative"}\n')
+    st, body, _ = _post(service, "/search", {"collection": "kyc_docs", "query": q, "top_k": 0})
+    assert st == 200 and json.loads(body) == {"results": [], "count": 0}

@@ -153,3 +153,117 @@ def test_service_snapshot_restore(pkg, orc, tmp_path):
     finally:
         s.close()
         eng.close()
+
+
+def test_search_runs_while_snapshot_writes(pkg, orc, tmp_path):
+    """vs_snapshot holds only the collection's reader lock, never
+    the engine's work lock, so searches (other collections and the same one)
+    and /health complete while a large snapshot is being written."""
+    import threading
+    import time
+    eng = pkg.VectorEngine(device=0)
+    try:
+        eng.create_collection("big", 768, 1, 1)
+        eng.generate("big", 2_000_000, orc.SEED_CORPUS)  # 3.07 GB to write
+        eng.create_collection("small", 768, 1, 1)
+        eng.generate("small", 5000, orc.SEED_CORPUS)
+        Q = orc.generate(orc.SEED_QUERY, 0, 4, 768)
+        eng.search("small", Q, 10)  # warm
+        done = threading.Event()
+        err = []
+
+        def snap():
+            try:
+                eng.snapshot("big", str(tmp_path / "big.vsnap"))
+            except Exception as e:  # pragma: no cover - reported below
+                err.append(e)
+            finally:
+                done.set()
+
+        t = threading.Thread(target=snap)
+        t.start()
+        during = 0
+        t0 = time.time()
+        while not done.is_set() and time.time() - t0 < 60:
+            eng.search("small", Q, 10)
+            eng.search("big", Q[:1], 10)
+            eng.health()
+            if not done.is_set():
+                during += 1
+        t.join()
+        assert not err, err
+        assert during >= 1, "no search completed while the snapshot was being written"
+        assert os.path.getsize(tmp_path / "big.vsnap") == 128 + 2_000_000 * 768 * 2
+    finally:
+        eng.close()
+
+
+def _bulk_uuid(tag, r):
+    """vector_service.cpp bulk_uuid: v4 UUID carrying the tag and the row."""
+    hi, lo = (tag << 16) | 0x4000, (1 << 63) | r
+    return (f"{hi >> 32:08x}-{(hi >> 16) & 0xFFFF:04x}-{hi & 0xFFFF:04x}-"
+            f"{lo >> 48:04x}-{lo & 0xFFFFFFFFFFFF:012x}")
+
+
+def _sidecar_service(pkg, svcmod, orc, d):
+    cfg = {"collections": [{"name": "docs", "dim": 64, "dtype": "bf16"}]}
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng, cfg)
+    s.bulk_generate("docs", 100, orc.SEED_CORPUS)
+    X = orc.generate(9, 0, 3, 64)
+    pts = [{"id": f"00000000-0000-4000-8000-{i:012x}", "vector": X[i].tolist(),
+            "payload": {"p": i}} for i in range(3)]
+    pts.append({"id": s.point_id("docs", 7), "vector": X[0].tolist(), "payload": {"b": 1}})
+    st, body, _ = s.handle("POST", "/upsert", json.dumps({"collection": "docs", "points": pts}).encode())
+    assert st == 200, body
+    s.snapshot(str(d))
+    s.close()
+    eng.close()
+
+
+def test_service_restore_refuses_corrupt_sidecar(pkg, orc, tmp_path):
+    """the whole sidecar is checked before the collection is
+    touched; a malformed one leaves the service empty and usable."""
+    from importlib import import_module
+    svcmod = import_module(pkg.__name__ + ".service")
+    _sidecar_service(pkg, svcmod, orc, tmp_path)
+    good = json.loads((tmp_path / "docs.points.json").read_text())
+    assert good["bulk"] == 100 and len(good["points"]) == 3 and good["bulk_payload"][0][0] == 7
+    bad = {
+        "bulk_fraction": dict(good, bulk=100.5),
+        "bulk_negative": dict(good, bulk=-1),
+        "payload_row_out_of_range": dict(good, bulk_payload=[[100, {"b": 1}]]),
+        "payload_not_object": dict(good, bulk_payload=[[7, 3]]),
+        "point_not_pair": dict(good, points=good["points"][:2] + [[good["points"][2][0]]]),
+        "point_bad_uuid": dict(good, points=good["points"][:2] + [["zzz", {}]]),
+        "point_duplicate": dict(good, points=good["points"][:2] + [good["points"][0]]),
+        "point_is_bulk_id": dict(good, points=good["points"][:2] + [[_bulk_uuid(good["bulk_tag"], 5), {}]]),
+        "count_mismatch": dict(good, points=good["points"][:2]),
+    }
+    cfg = {"collections": [{"name": "docs", "dim": 64, "dtype": "bf16"}]}
+    for tag, side in bad.items():
+        (tmp_path / "docs.points.json").write_text(json.dumps(side))
+        eng = pkg.VectorEngine(device=0)
+        s = svcmod.VectorService(eng, cfg)
+        try:
+            with pytest.raises(pkg.VSError) as ei:
+                s.restore(str(tmp_path))
+            assert ei.value.code in (-8,), (tag, ei.value)
+            assert eng.collection_info("docs")["rows"] == 0, tag
+            # still a working, empty collection
+            st, body, _ = s.handle("POST", "/search", json.dumps(
+                {"collection": "docs", "query": [0.1] * 64, "top_k": 3}).encode())
+            assert (st, json.loads(body)) == (200, {"results": [], "count": 0}), tag
+        finally:
+            s.close()
+            eng.close()
+    # the untouched sidecar still restores
+    (tmp_path / "docs.points.json").write_text(json.dumps(good))
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng, cfg)
+    try:
+        s.restore(str(tmp_path))
+        assert eng.collection_info("docs")["rows"] == 103
+    finally:
+        s.close()
+        eng.close()
