@@ -60,6 +60,9 @@ def lib():
         L.oracle_cpu_scan.restype = i32
         L.oracle_f32_to_bf16.argtypes = [ctypes.c_float]
         L.oracle_f32_to_bf16.restype = ctypes.c_uint16
+        L.oracle_search_generated.argtypes = [u64, u64, u64, u32, i32, vp, u32, u32, i32, vp,
+                                              vp, vp]
+        L.oracle_rescore_generated.argtypes = [u64, u32, i32, vp, u32, u32, vp, vp, vp]
         L.oracle_checksum.argtypes = [vp, u64]
         L.oracle_checksum.restype = u64
         _lib = L
@@ -106,6 +109,35 @@ def search(X: np.ndarray, Q: np.ndarray, k: int, row_base: int = 0):
     lib().oracle_search(_p(X), X.shape[0], dim, _p(Q), nq, k, row_base, _p(s32), _p(s64),
                         _p(rows), _p(cnt))
     return s32, s64, rows, cnt
+
+
+def search_generated(seed: int, grow0: int, n: int, Q: np.ndarray, k: int, bf16: bool,
+                     threads: int = 0):
+    """Exact top-k over generator rows grow0 .. grow0+n-1 (a vs_generate corpus)
+    without materialising it: rows are regenerated per thread block.
+
+    Returns (scores_f64, rows, counts); rows are global row numbers."""
+    Q = np.ascontiguousarray(Q, np.float32)
+    nq, dim = Q.shape
+    s64 = np.zeros((nq, k), np.float64)
+    rows = np.zeros((nq, k), np.uint64)
+    cnt = np.zeros(nq, np.uint32)
+    lib().oracle_search_generated(seed, grow0, n, dim, int(bf16), _p(Q), nq, k, threads,
+                                  _p(s64), _p(rows), _p(cnt))
+    return s64, rows, cnt
+
+
+def rescore_generated(seed: int, Q: np.ndarray, rows: np.ndarray, counts: np.ndarray,
+                      bf16: bool) -> np.ndarray:
+    """Exact fp64 scores of (query, global row) pairs of a generated corpus."""
+    Q = np.ascontiguousarray(Q, np.float32)
+    rows = np.ascontiguousarray(rows, np.uint64)
+    counts = np.ascontiguousarray(counts, np.uint32)
+    nq, k = rows.shape
+    out = np.zeros((nq, k), np.float64)
+    lib().oracle_rescore_generated(seed, Q.shape[1], int(bf16), _p(Q), nq, k, _p(rows),
+                                   _p(counts), _p(out))
+    return out
 
 
 def rescore(X: np.ndarray, Q: np.ndarray, rows: np.ndarray, counts: np.ndarray,

@@ -242,6 +242,132 @@ void oracle_rescore(const float* X, uint32_t dim, const float* Q, uint32_t nq, u
     }
 }
 
+/* ---- streaming oracle over a generated corpus ----
+ * Exact top-k of preprocessed queries Q (nq x dim, fp32) against the rows a
+ * collection filled by vs_generate holds: global rows grow0 .. grow0+n-1 of
+ * `seed`, bf16-rounded when bf16 != 0. Rows are regenerated
+ * block by block inside each thread, so no n x dim host array exists: this is
+ * what lets the tests check C3 (10M rows) and C4 (100M rows) at their full
+ * size. Scores are fp64 dot products of the stored values (same rule as
+ * oracle_search); ties by row ascending. Each row's score is computed by one
+ * thread in a fixed order, so the result does not depend on the thread count. */
+static void o_gen_row(uint64_t seed, uint64_t row, uint32_t dim, int bf16, int32_t* m,
+                      double* out) {
+  const uint64_t rk = o_splitmix64(seed ^ (row * 0xD1B54A32D192ED03ull));
+  int64_t s = 0;
+  for (uint32_t d = 0; d < dim; ++d) {
+    const uint64_t h = o_splitmix64(rk + (uint64_t)d);
+    m[d] = (int32_t)((h & 0xFFFFu) + ((h >> 16) & 0xFFFFu) + ((h >> 32) & 0xFFFFu) + (h >> 48)) -
+           131070;
+    s += (int64_t)m[d] * m[d];
+  }
+  const double nrm = sqrt((double)s);
+  for (uint32_t d = 0; d < dim; ++d) {
+    float y = s > 0 ? (float)((double)m[d] / nrm) : 0.0f;
+    if (bf16) y = o_bf16_round(y);
+    out[d] = (double)y;
+  }
+}
+
+static double o_dot64(const double* x, const double* q, uint32_t dim) {
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  uint32_t d = 0;
+  for (; d + 4 <= dim; d += 4) {
+    a0 += x[d] * q[d];
+    a1 += x[d + 1] * q[d + 1];
+    a2 += x[d + 2] * q[d + 2];
+    a3 += x[d + 3] * q[d + 3];
+  }
+  for (; d < dim; ++d) a0 += x[d] * q[d];
+  return (a0 + a1) + (a2 + a3);
+}
+
+void oracle_search_generated(uint64_t seed, uint64_t grow0, uint64_t n, uint32_t dim, int bf16,
+                             const float* Q, uint32_t nq, uint32_t k, int threads,
+                             double* out_scores64, uint64_t* out_rows, uint32_t* out_count) {
+  int nth = threads > 0 ? threads : 1;
+#ifdef _OPENMP
+  if (threads <= 0) nth = omp_get_max_threads();
+#else
+  nth = 1;
+#endif
+  double* q64 = (double*)malloc(sizeof(double) * (size_t)nq * dim);
+  for (size_t i = 0; i < (size_t)nq * dim; ++i) q64[i] = (double)Q[i];
+  o_hit* heaps = (o_hit*)malloc(sizeof(o_hit) * (size_t)nth * nq * k);
+  uint32_t* cnts = (uint32_t*)calloc((size_t)nth * nq, sizeof(uint32_t));
+#pragma omp parallel num_threads(nth)
+  {
+    int t = 0;
+#ifdef _OPENMP
+    t = omp_get_thread_num();
+#endif
+    int32_t* m = (int32_t*)malloc(sizeof(int32_t) * dim);
+    double* x = (double*)malloc(sizeof(double) * dim);
+    o_hit* h = heaps + (size_t)t * nq * k;
+    uint32_t* c = cnts + (size_t)t * nq;
+#pragma omp for schedule(dynamic, 4096)
+    for (int64_t r = 0; r < (int64_t)n; ++r) {
+      const uint64_t row = grow0 + (uint64_t)r;
+      o_gen_row(seed, row, dim, bf16, m, x);
+      for (uint32_t qi = 0; qi < nq; ++qi) {
+        const double sc = o_dot64(x, q64 + (size_t)qi * dim, dim);
+        o_hit* hq = h + (size_t)qi * k;
+        if (c[qi] == k && !(sc > hq[k - 1].s || (sc == hq[k - 1].s && row < hq[k - 1].row)))
+          continue;
+        o_hit hit = {sc, row};
+        o_push(hq, &c[qi], k, hit);
+      }
+    }
+    free(m);
+    free(x);
+  }
+  o_hit* best = (o_hit*)malloc(sizeof(o_hit) * k);
+  for (uint32_t qi = 0; qi < nq; ++qi) {
+    uint32_t nb = 0;
+    for (int t = 0; t < nth; ++t)
+      for (uint32_t j = 0; j < cnts[(size_t)t * nq + qi]; ++j)
+        o_push(best, &nb, k, heaps[((size_t)t * nq + qi) * k + j]);
+    for (uint32_t j = 0; j < k; ++j) {
+      const size_t o = (size_t)qi * k + j;
+      if (out_scores64) out_scores64[o] = j < nb ? best[j].s : 0.0;
+      if (out_rows) out_rows[o] = j < nb ? best[j].row : 0;
+    }
+    if (out_count) out_count[qi] = nb;
+  }
+  free(best);
+  free(q64);
+  free(heaps);
+  free(cnts);
+}
+
+/* Exact fp64 scores of (query, global row) pairs of a generated corpus. */
+void oracle_rescore_generated(uint64_t seed, uint32_t dim, int bf16, const float* Q, uint32_t nq,
+                              uint32_t k, const uint64_t* rows, const uint32_t* count,
+                              double* out) {
+#pragma omp parallel
+  {
+    int32_t* m = (int32_t*)malloc(sizeof(int32_t) * dim);
+    double* x = (double*)malloc(sizeof(double) * dim);
+    double* q = (double*)malloc(sizeof(double) * dim);
+#pragma omp for schedule(static)
+    for (int64_t qi = 0; qi < (int64_t)nq; ++qi) {
+      for (uint32_t d = 0; d < dim; ++d) q[d] = (double)Q[(size_t)qi * dim + d];
+      for (uint32_t j = 0; j < k; ++j) {
+        const size_t o = (size_t)qi * k + j;
+        if (j >= count[qi]) {
+          out[o] = 0.0;
+          continue;
+        }
+        o_gen_row(seed, rows[o], dim, bf16, m, x);
+        out[o] = o_dot64(x, q, dim);
+      }
+    }
+    free(m);
+    free(x);
+    free(q);
+  }
+}
+
 /* ---- CPU baseline: restatement of Qdrant's plain exact scan ----
  * fp32 dot with 8 independent accumulators (Qdrant's AVX path keeps four
  * 8-wide accumulators), OpenMP over row blocks, per-thread fixed-length
