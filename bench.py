@@ -33,22 +33,36 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_DENSE_TFLOPS = 2516.6       # 256 CU x 4096 flop/clk x 2.4 GHz (dense, no sparsity)
+F32_MFMA_TFLOPS = 157.3          # v_mfma_f32_16x16x4_f32: 1/16 of bf16 (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (rows, dim, dtype, metric, batch, k, description)
+    # name: (rows, dim, dtype, metric, batch, k, description; {rows} = the corpus size)
     "c3": (10_000_000, 768, "bf16", "dot", 256, 10,
-           "C3: 10M x 768 bf16 corpus, 256-query batches, exact top-10, inner product"),
+           "C3: {rows} x 768 bf16 corpus, 256-query batches, exact top-10, inner product"),
     "c3b1": (10_000_000, 768, "bf16", "dot", 1, 10,
-             "10M x 768 bf16 corpus, single query, exact top-10, inner product (GEMV)"),
+             "{rows} x 768 bf16 corpus, single query, exact top-10, inner product (GEMV)"),
     "c2": (1_000_000, 768, "f32", "cosine", 1, 10,
-           "C2: 1M x 768 fp32 corpus, single query, exact top-10, cosine (GEMV)"),
+           "C2: {rows} x 768 fp32 corpus, single query, exact top-10, cosine (GEMV)"),
+    # the reference's collection type (fp32) batched: f32 MFMA pass
+    "c2b256": (1_000_000, 768, "f32", "cosine", 256, 10,
+               "C2 corpus batched: {rows} x 768 fp32, 256-query batches, exact top-10, cosine "
+               "(f32 MFMA)"),
     # C4 is quoted on 8 GPUs (12.5M rows each); on fewer GPUs each holds more
     # (100M x 768 bf16 = 153.6 GB fits one MI355X's 288 GB)
     "c4": (100_000_000, 768, "bf16", "dot", 256, 100,
-           "C4: 100M x 768 bf16 corpus row-sharded, 256-query batches, exact top-100, IP"),
+           "C4: {rows} x 768 bf16 corpus row-sharded, 256-query batches, exact top-100, IP"),
     "c4b1": (100_000_000, 768, "bf16", "dot", 1, 100,
-             "C4: 100M x 768 bf16 corpus row-sharded, single query, exact top-100, IP (GEMV)"),
+             "C4: {rows} x 768 bf16 corpus row-sharded, single query, exact top-100, IP (GEMV)"),
 }
+
+
+def fmt_rows(n: int) -> str:
+    """10_000_000 -> '10M', 1_250_000 -> '1.25M', 300_000 -> '300k'."""
+    if n >= 1_000_000:
+        return f"{n / 1e6:g}M"
+    if n >= 1000:
+        return f"{n / 1e3:g}k"
+    return str(n)
 METRIC_NAME = "exact top-10 QPS on 10M×768 corpus at 1/2/4/8 GPUs; % of HBM/MFMA peak"
 # configs other than c3 report their own workload under the same metric name
 # only as secondary measurements (the driver's headline run uses the default)
@@ -75,16 +89,23 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def kernel_roofline(cfg_rows_local, dim, elem, batch, k, t_ms, bound):
-    """Algorithmic work of one scan launch / its measured duration."""
-    bytes_ = cfg_rows_local * dim * elem + batch * dim * elem + batch * k * 12
-    flops = 2.0 * batch * cfg_rows_local * dim
+def kernel_roofline(cfg_rows_local, dim, elem, batch, k, t_ms, bound, queries_per_pass=256):
+    """Algorithmic work of one scan launch / its measured duration.
+
+    A launch covers at most `queries_per_pass` queries (fp32 at dim 768: 128),
+    so a batch of `batch` queries takes ceil(batch / qpp) launches; the work
+    of ONE launch is priced against one launch's average duration."""
+    per_launch = min(batch, queries_per_pass)
+    passes = -(-batch // per_launch)
+    bytes_ = cfg_rows_local * dim * elem + per_launch * dim * elem + per_launch * k * 12
+    flops = 2.0 * per_launch * cfg_rows_local * dim
     t = t_ms / 1e3
     gbs = bytes_ / t / 1e9
     tfs = flops / t / 1e12
     if bound == "mfma":
-        return {"bound": "mfma", "achieved": round(tfs, 2), "peak": BF16_DENSE_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(tfs / BF16_DENSE_TFLOPS, 4),
+        peak = BF16_DENSE_TFLOPS if elem == 2 else F32_MFMA_TFLOPS
+        return {"bound": "mfma", "achieved": round(tfs, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(tfs / peak, 4), "launches_per_step": passes,
                 "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                 "kernel_ms": round(t_ms, 4), "bytes_per_launch": int(bytes_),
                 "flops_per_launch": int(flops)}
@@ -184,6 +205,9 @@ def main():
     n_full, dim, dtype, metric, batch, k, desc = cfg
     if args.rows:
         n_full = args.rows
+    desc = desc.format(rows=fmt_rows(n_full))
+    if args.rows:
+        desc += " (--rows override of the config's corpus size)"
     lo, hi = shard.shard_range(n_full, world, rank)
     eng = pkg.VectorEngine(device=local, timing=True, timing_sample=True)
     coll = "bench"
@@ -201,8 +225,9 @@ def main():
     el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
                             stream_fn, 0)
     elem = 2 if dtype == "bf16" else 4
-    bound = "mfma" if batch > 1 and dtype == "bf16" else "hbm"
-    roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound)
+    bound = "mfma" if batch > 1 else "hbm"
+    qpp = 256 if (dtype == "bf16" and dim <= 768) or (dtype == "f32" and dim <= 384) else 128
+    roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound, qpp)
     # PMC traffic is recorded per default-size workload only
     roof["traffic"] = None if args.rows else pmc_traffic(args.config)
     roof["kernel_launches_timed"] = tm["scan_n"]

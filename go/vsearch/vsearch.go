@@ -1,0 +1,312 @@
+// Package vsearch binds the MI355X exact top-k search engine (include/vsearch.h)
+// for rag/vector-service. It replaces the github.com/qdrant/go-client stubs
+// the reference dials (rag/vector-service/main.go:14, :44-51, :56-65): the
+// five engine calls of the reference map to Info, Create, Health, Upsert and
+// Search. The engine deals in dense row numbers; UUIDs and payloads stay in
+// the caller (see ../vector-service).
+//
+// Memory rules: Go slices are passed to C directly. The library copies every
+// input before it returns and never keeps a pointer, which is what cgo's
+// pointer-passing rules require. Every function is safe for concurrent use.
+package vsearch
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/lib -lvsearch -Wl,-rpath,${SRCDIR}/../../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/lib
+#include <stdlib.h>
+#include "vsearch.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"unsafe"
+)
+
+// Metric and dtype of a collection (qdrant.Distance_Cosine is main.go:108).
+const (
+	MetricCosine = int(C.VS_METRIC_COSINE)
+	MetricDot    = int(C.VS_METRIC_DOT)
+	DtypeF32     = int(C.VS_DTYPE_F32)
+	DtypeBF16    = int(C.VS_DTYPE_BF16)
+	MaxK         = 1024 // largest k of one search
+)
+
+// Status codes of the C-ABI.
+var (
+	ErrInvalidArg  = errors.New("invalid argument")
+	ErrNotFound    = errors.New("not found")
+	ErrDimMismatch = errors.New("dimension mismatch")
+	ErrOOM         = errors.New("out of memory")
+	ErrDevice      = errors.New("device error")
+	ErrExists      = errors.New("already exists")
+	ErrInternal    = errors.New("internal error")
+	ErrIO          = errors.New("i/o error")
+)
+
+// Error carries the status and the library's message (vs_last_error).
+type Error struct {
+	Code int
+	Msg  string
+}
+
+func (e *Error) Error() string { return e.Msg }
+
+// Unwrap lets errors.Is(err, vsearch.ErrNotFound) replace the reference's
+// status.Code(err) == codes.NotFound test (main.go:96).
+func (e *Error) Unwrap() error {
+	switch e.Code {
+	case int(C.VS_ERR_INVALID_ARG):
+		return ErrInvalidArg
+	case int(C.VS_ERR_NOT_FOUND):
+		return ErrNotFound
+	case int(C.VS_ERR_DIM_MISMATCH):
+		return ErrDimMismatch
+	case int(C.VS_ERR_OOM):
+		return ErrOOM
+	case int(C.VS_ERR_DEVICE):
+		return ErrDevice
+	case int(C.VS_ERR_EXISTS):
+		return ErrExists
+	case int(C.VS_ERR_IO):
+		return ErrIO
+	}
+	return ErrInternal
+}
+
+// vs_last_error is thread-local: read it on the OS thread of the failed call.
+// cgo runs a call and the Go code right after it on the same thread as long
+// as the goroutine does not yield in between, which holds here.
+func check(rc C.int) error {
+	if rc == 0 {
+		return nil
+	}
+	return &Error{Code: int(rc), Msg: C.GoString(C.vs_last_error())}
+}
+
+// Engine is one engine handle: one GPU (Open) or row shards over several
+// (OpenShards).
+type Engine struct{ h *C.vs_engine }
+
+// Open binds the engine to one HIP device (-1: the current one). It replaces
+// grpc.DialContext + the New*Client calls (main.go:56-65).
+func Open(device int) (*Engine, error) {
+	cfg := C.vs_config{device: C.int32_t(device)}
+	var h *C.vs_engine
+	if err := check(C.vs_open(&cfg, &h)); err != nil {
+		return nil, err
+	}
+	return &Engine{h}, nil
+}
+
+// OpenShards opens one engine over row shards: shard s on HIP device
+// devices[s] (a device may repeat). Collections are then row-striped over
+// the shards and each search ends in one RCCL all-gather; every other call
+// is unchanged.
+func OpenShards(devices []int) (*Engine, error) {
+	if len(devices) == 0 {
+		return nil, fmt.Errorf("vsearch: no devices: %w", ErrInvalidArg)
+	}
+	devs := (*C.int32_t)(C.malloc(C.size_t(len(devices)) * 4))
+	defer C.free(unsafe.Pointer(devs))
+	ds := unsafe.Slice(devs, len(devices))
+	for i, d := range devices {
+		ds[i] = C.int32_t(d)
+	}
+	cfg := C.vs_config_multi{devices: devs, n_shards: C.uint32_t(len(devices))}
+	var h *C.vs_engine
+	if err := check(C.vs_open_multi(&cfg, &h)); err != nil {
+		return nil, err
+	}
+	return &Engine{h}, nil
+}
+
+// Close releases the device memory of every collection.
+func (e *Engine) Close() {
+	if e.h != nil {
+		C.vs_close(e.h)
+		e.h = nil
+	}
+}
+
+// Layout reports the engine's shards and distinct devices.
+func (e *Engine) Layout() (shards, devices int, err error) {
+	var s, d C.uint32_t
+	err = check(C.vs_engine_layout(e.h, &s, &d))
+	return int(s), int(d), err
+}
+
+// Info mirrors collectionsClient.Get (main.go:91).
+func (e *Engine) Info(name string) (dim uint32, rows uint64, err error) {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var d C.uint32_t
+	var r C.uint64_t
+	err = check(C.vs_collection_info(e.h, cs, &d, &r, nil, nil))
+	return uint32(d), uint64(r), err
+}
+
+// Create mirrors collectionsClient.Create (main.go:102-112).
+func (e *Engine) Create(name string, dim uint32, metric, dtype int, capacity uint64) error {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	return check(C.vs_collection_create(e.h, cs, C.uint32_t(dim), C.int(metric), C.int(dtype),
+		C.uint64_t(capacity), 0))
+}
+
+// Drop frees a collection.
+func (e *Engine) Drop(name string) error {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	return check(C.vs_collection_drop(e.h, cs))
+}
+
+// Upsert writes len(rows) vectors (vecs is len(rows)*dim float32, row-major)
+// into rows; rows at or past the row count append (contiguously). It mirrors
+// pointsClient.Upsert(wait=true) (main.go:208-213): it returns once the data
+// is resident.
+func (e *Engine) Upsert(name string, dim uint32, rows []uint64, vecs []float32) error {
+	if len(rows) == 0 {
+		return nil
+	}
+	if len(vecs) != len(rows)*int(dim) {
+		return fmt.Errorf("vsearch: %d vectors of dim %d need %d floats, got %d: %w",
+			len(rows), dim, len(rows)*int(dim), len(vecs), ErrInvalidArg)
+	}
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	return check(C.vs_upsert(e.h, cs, C.uint64_t(len(rows)), C.uint32_t(dim),
+		(*C.uint64_t)(unsafe.Pointer(&rows[0])), (*C.float)(unsafe.Pointer(&vecs[0]))))
+}
+
+// Generate appends n synthetic unit rows made on the device (benchmarks).
+func (e *Engine) Generate(name string, n, seed uint64) error {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	return check(C.vs_generate(e.h, cs, C.uint64_t(n), C.uint64_t(seed)))
+}
+
+// Hits of one query: rows and scores, best first.
+type Hits struct {
+	Rows   []uint64
+	Scores []float32
+}
+
+// SearchBatch searches nq = len(queries)/dim queries at once (the batched
+// MFMA path from 2 queries on) and returns each query's top k. It mirrors
+// pointsClient.Search (main.go:249-254) for many queries in one call.
+func (e *Engine) SearchBatch(name string, queries []float32, dim, k uint32) ([]Hits, error) {
+	return e.search(name, queries, dim, k, nil, 0)
+}
+
+// Search is SearchBatch for one query.
+func (e *Engine) Search(name string, query []float32, k uint32) ([]uint64, []float32, error) {
+	h, err := e.search(name, query, uint32(len(query)), k, nil, 0)
+	if err != nil {
+		return nil, nil, err
+	}
+	return h[0].Rows, h[0].Scores, nil
+}
+
+// SearchFiltered restricts a search to the rows whose bit is set in allow
+// (bit r of word r/64); the reference parses SearchRequest.Filter
+// (main.go:30) but never applies it.
+func (e *Engine) SearchFiltered(name string, queries []float32, dim, k uint32,
+	allow []uint64) ([]Hits, error) {
+	if len(allow) == 0 {
+		return nil, fmt.Errorf("vsearch: empty filter bitmap: %w", ErrInvalidArg)
+	}
+	return e.search(name, queries, dim, k, allow, 0)
+}
+
+// FilterCreate uploads a filter bitmap once; SearchFilterID then ships no
+// bitmap per call.
+func (e *Engine) FilterCreate(name string, allow []uint64) (uint64, error) {
+	if len(allow) == 0 {
+		return 0, fmt.Errorf("vsearch: empty filter bitmap: %w", ErrInvalidArg)
+	}
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var id C.uint64_t
+	err := check(C.vs_filter_create(e.h, cs, (*C.uint64_t)(unsafe.Pointer(&allow[0])),
+		C.uint64_t(len(allow)), &id))
+	return uint64(id), err
+}
+
+// FilterDrop frees a resident filter.
+func (e *Engine) FilterDrop(id uint64) error { return check(C.vs_filter_drop(e.h, C.uint64_t(id))) }
+
+// SearchFilterID searches with a resident filter (stale after an upsert
+// that added rows: rebuild it).
+func (e *Engine) SearchFilterID(name string, queries []float32, dim, k uint32,
+	id uint64) ([]Hits, error) {
+	return e.search(name, queries, dim, k, nil, id)
+}
+
+func (e *Engine) search(name string, queries []float32, dim, k uint32, allow []uint64,
+	fid uint64) ([]Hits, error) {
+	if dim == 0 || len(queries) == 0 || len(queries)%int(dim) != 0 {
+		return nil, fmt.Errorf("vsearch: %d floats are not whole queries of dim %d: %w",
+			len(queries), dim, ErrInvalidArg)
+	}
+	if k == 0 || k > MaxK {
+		return nil, fmt.Errorf("vsearch: k must be in [1, %d]: %w", MaxK, ErrInvalidArg)
+	}
+	nq := len(queries) / int(dim)
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	rows := make([]uint64, nq*int(k))
+	scores := make([]float32, nq*int(k))
+	count := make([]uint32, nq)
+	q := (*C.float)(unsafe.Pointer(&queries[0]))
+	pr := (*C.uint64_t)(unsafe.Pointer(&rows[0]))
+	ps := (*C.float)(unsafe.Pointer(&scores[0]))
+	pc := (*C.uint32_t)(unsafe.Pointer(&count[0]))
+	var rc C.int
+	switch {
+	case fid != 0:
+		rc = C.vs_search_filter_id(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
+			C.uint64_t(fid), ps, pr, pc)
+	case allow != nil:
+		rc = C.vs_search_filtered(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
+			(*C.uint64_t)(unsafe.Pointer(&allow[0])), C.uint64_t(len(allow)), ps, pr, pc)
+	default:
+		rc = C.vs_search(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k), ps, pr, pc)
+	}
+	if err := check(rc); err != nil {
+		return nil, err
+	}
+	out := make([]Hits, nq)
+	for i := range out {
+		lo, n := i*int(k), int(count[i])
+		out[i] = Hits{Rows: rows[lo : lo+n], Scores: scores[lo : lo+n]}
+	}
+	return out, nil
+}
+
+// Snapshot writes a collection's stored rows to path (replaces Qdrant's
+// persistent volume, docker-compose.yml:9-10,14-15); searches proceed meanwhile.
+func (e *Engine) Snapshot(name, path string) error {
+	cn, cp := C.CString(name), C.CString(path)
+	defer C.free(unsafe.Pointer(cn))
+	defer C.free(unsafe.Pointer(cp))
+	return check(C.vs_snapshot(e.h, cn, cp))
+}
+
+// Restore creates a collection from a snapshot (bit-exact, checksum-verified).
+func (e *Engine) Restore(name, path string) error {
+	cn, cp := C.CString(name), C.CString(path)
+	defer C.free(unsafe.Pointer(cn))
+	defer C.free(unsafe.Pointer(cp))
+	return check(C.vs_restore(e.h, cn, cp))
+}
+
+// Health mirrors systemClient.HealthCheck (main.go:126): the engine's JSON
+// status object ({"status":"healthy"|"degraded","engine":"vsearch-hip",...}).
+func (e *Engine) Health() (string, error) {
+	buf := (*C.char)(C.malloc(4096))
+	defer C.free(unsafe.Pointer(buf))
+	err := check(C.vs_health(e.h, buf, 4096))
+	return C.GoString(buf), err
+}

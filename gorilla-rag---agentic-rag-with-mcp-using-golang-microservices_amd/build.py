@@ -22,8 +22,9 @@ ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
 SOURCES = {
     "vs_kernels.o": (["vs_kernels.hip"], ["--offload-arch=" + ARCH, "-O3"]),
     "vs_engine.o": (["vs_engine.cpp"], ["-O2", "-Wall"]),
+    "vs_api.o": (["vs_api.cpp"], ["-O2", "-Wall"]),
 }
-HEADERS = ["vs_common.h", "vs_kernels.h"]
+HEADERS = ["vs_common.h", "vs_kernels.h", "vs_dev.h"]
 
 
 def _mtime(p):
@@ -48,7 +49,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         subprocess.run(cmd, check=True)
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB, *objs,
-               "-Wl,-rpath,/opt/rocm/lib", "-Wl,-soname,libvsearch.so"]
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib",
+               "-Wl,-soname,libvsearch.so"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -1,0 +1,194 @@
+// vs_dev.h — one device's engine (internal; the public boundary is
+// include/vsearch.h). A DevEngine owns one HIP device, its stream, its
+// scratch and the collections (or collection shards) resident on it;
+// vs_api.cpp builds the C-ABI's vs_engine from one DevEngine (a single-GPU
+// engine) or several (a row-sharded multi-GPU engine).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/vsearch.h"
+
+namespace vsd {
+
+int fail(int code, const std::string& msg);
+int fail_hip(hipError_t e, const char* what);
+#define VS_HIP(call, what)                           \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return ::vsd::fail_hip(e_, what); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // Grows the buffer; the caller has drained the stream that used it.
+  hipError_t ensure(size_t want) {
+    if (want <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t b = std::max(want, (size_t)4096);
+    hipError_t e = hipMalloc(&p, b);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+  template <typename T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+struct Collection {
+  std::string name;
+  uint64_t gen = 0;  // unique per created collection (never reused in a process)
+  uint32_t dim = 0;
+  int metric = VS_METRIC_COSINE;
+  int dtype = VS_DTYPE_F32;
+  uint64_t row_base = 0;
+  void* data = nullptr;  // cap x dim elements
+  uint64_t rows = 0, cap = 0;
+  std::shared_mutex mu;
+  size_t elem() const { return dtype == VS_DTYPE_BF16 ? 2 : 4; }
+  size_t row_bytes() const { return elem() * dim; }
+  ~Collection() {
+    if (data) (void)hipFree(data);
+  }
+};
+
+struct EventPair {
+  hipEvent_t a, b;
+};
+
+
+struct DevEngine {
+  int device = 0;
+  uint32_t flags = 0;
+  hipStream_t own = nullptr;     // the engine's stream
+  hipStream_t stream = nullptr;  // the stream device work is enqueued on now (own or a caller's)
+  hipEvent_t xev = nullptr;      // orders a newly used stream after the previous one
+  std::string device_name;
+  std::mutex map_mu;
+  std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
+  std::mutex work_mu;  // scratch buffers + stream
+  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
+  DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
+  DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
+  DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
+  DevBuf scratch8;                  // u64 result of the snapshot checksum
+  DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
+  DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch
+  // device-resident filters (vs_filter_create), guarded by work_mu
+  struct DevFilter {
+    std::string coll;
+    uint64_t coll_gen = 0;           // Collection::gen it was built for
+    uint64_t rows = 0, allowed = 0;  // collection rows it was built over
+    DevBuf bits, list;               // bitmap; compacted rows when selective
+  };
+  std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
+  uint64_t next_filter = 1;
+  uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
+  DevBuf ovf_slots;                 // u32 flag words of deferred passes (DeferredCheck)
+  uint32_t ovf_next = 0;            // next free slot of the current multi-shard call
+  std::vector<uint64_t> h_keys;
+  // timing
+  std::vector<EventPair> scan_ev, merge_ev;
+  std::vector<hipEvent_t> ev_pool;  // recycled timing events (none created on the hot path)
+  double scan_ms = 0, merge_ms = 0;
+  uint64_t scan_n = 0, merge_n = 0;
+  uint64_t scan_tick = 0;   // scan launches seen (VS_FLAG_TIMING_SAMPLE)
+  bool scan_skip = false;   // the current scan launch is not bracketed
+};
+
+// A batched pass whose overflow flag is read after every shard's scans were
+// enqueued (k > kMfmaListMaxK; multi-shard searches): a set flag re-runs the
+// pass's queries on the GEMV path before the keys are consumed.
+struct DeferredCheck {
+  Collection* coll;
+  float* qp;        // preprocessed fp32 queries of the call (device)
+  uint32_t q0, nv;  // the pass's queries
+  uint32_t k;
+  uint64_t* out;    // its keys [nv][k]
+  uint32_t slot;    // flag word in DevEngine::ovf_slots
+};
+
+// ---- per-device operations (vs_engine.cpp); same contracts as the C-ABI
+// functions of the same name, for one device and its local rows ----
+int open(int device, uint32_t flags, DevEngine** out);
+void close(DevEngine* eng);
+std::shared_ptr<Collection> find_coll(DevEngine* eng, const char* name);
+hipError_t set_dev(DevEngine* eng);
+hipError_t use_stream(DevEngine* eng, hipStream_t s);
+int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric, int dtype,
+                      uint64_t capacity_hint, uint64_t row_base);
+int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* rows, int* metric,
+                    int* dtype);
+int collection_drop(DevEngine* eng, const char* name);
+int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim, const uint64_t* rows,
+           const float* vecs);
+// appends n generator rows whose global numbers are g0, g0 + stride, ...
+int generate(DevEngine* eng, const char* coll, uint64_t n, uint64_t seed, uint64_t g0,
+             uint64_t stride);
+int generate_vectors(DevEngine* eng, uint64_t seed, uint64_t row0, uint64_t n, uint32_t dim,
+                     float* d_out, void* stream);
+int read_rows(DevEngine* eng, const char* coll, uint64_t first, uint64_t n, float* out);
+int read_raw(DevEngine* eng, const char* coll, uint64_t first, uint64_t n, void* out);
+int append_raw(DevEngine* eng, const char* coll, uint64_t n, const void* rows);
+int checksum_shard(DevEngine* eng, const char* coll, uint64_t stride, uint64_t offset,
+                   uint64_t* out);
+const char* last_error();
+int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t nq,
+                uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
+                float* out_scores, uint64_t* out_rows, uint32_t* out_count,
+                uint64_t filter_id = 0);
+int filter_create(DevEngine* eng, const char* coll, const uint64_t* allow, uint64_t allow_words,
+                  uint64_t* filter_id);
+int filter_drop(DevEngine* eng, uint64_t filter_id);
+int search_keys(DevEngine* eng, const char* coll, const float* d_queries, uint32_t nq,
+                uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream);
+int merge_keys(DevEngine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
+               uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream);
+int decode_keys(DevEngine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
+                float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream);
+void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores, uint64_t* rows,
+                 uint32_t* count);
+int checksum(DevEngine* eng, const char* coll, uint64_t* out);
+int snapshot(DevEngine* eng, const char* coll, const char* path);
+int restore(DevEngine* eng, const char* coll, const char* path);
+int health(DevEngine* eng, char* buf, size_t len);
+int timing(DevEngine* eng, double* scan_ms_sum, uint64_t* scan_count, double* merge_ms_sum,
+           uint64_t* merge_count, int reset);
+uint64_t popcount_rows(const uint64_t* allow, uint64_t rows);
+
+// Search of device queries d_q (nq x dim fp32 on this device, ordered on
+// eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and
+// the collection's reader lock held by the caller. With `defer`, a batched
+// pass's overflow check is appended there instead of synchronising.
+int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
+                uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
+                const uint32_t* allow_list = nullptr,
+                std::vector<DeferredCheck>* defer = nullptr);
+// GEMV re-run of a deferred pass whose flag was set (work_mu held).
+int rerun_deferred(DevEngine* eng, const DeferredCheck& d);
+
+}  // namespace vsd

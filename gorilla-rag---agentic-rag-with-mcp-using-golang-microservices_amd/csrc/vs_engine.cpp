@@ -22,9 +22,10 @@
 
 #include "../../include/vsearch.h"
 #include "vs_common.h"
+#include "vs_dev.h"
 #include "vs_kernels.h"
 
-namespace {
+namespace vsd {
 
 thread_local std::string g_last_error;
 
@@ -36,112 +37,24 @@ int fail_hip(hipError_t e, const char* what) {
   return fail(e == hipErrorOutOfMemory ? VS_ERR_OOM : VS_ERR_DEVICE,
               std::string(what) + ": " + hipGetErrorString(e));
 }
-#define VS_HIP(call, what)                       \
-  do {                                           \
-    hipError_t e_ = (call);                      \
-    if (e_ != hipSuccess) return fail_hip(e_, what); \
-  } while (0)
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  // Grows the buffer; the caller has drained the stream that used it.
-  hipError_t ensure(size_t want) {
-    if (want <= bytes) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    size_t b = std::max(want, (size_t)4096);
-    hipError_t e = hipMalloc(&p, b);
-    if (e == hipSuccess) bytes = b;
-    return e;
-  }
-  template <typename T>
-  T* as() const {
-    return (T*)p;
-  }
-};
 
-struct Collection {
-  std::string name;
-  uint64_t gen = 0;  // unique per created collection (never reused in a process)
-  uint32_t dim = 0;
-  int metric = VS_METRIC_COSINE;
-  int dtype = VS_DTYPE_F32;
-  uint64_t row_base = 0;
-  void* data = nullptr;  // cap x dim elements
-  uint64_t rows = 0, cap = 0;
-  std::shared_mutex mu;
-  size_t elem() const { return dtype == VS_DTYPE_BF16 ? 2 : 4; }
-  size_t row_bytes() const { return elem() * dim; }
-  ~Collection() {
-    if (data) (void)hipFree(data);
-  }
-};
-
-struct EventPair {
-  hipEvent_t a, b;
-};
-
-}  // namespace
-
-struct vs_engine {
-  int device = 0;
-  uint32_t flags = 0;
-  hipStream_t own = nullptr;     // the engine's stream
-  hipStream_t stream = nullptr;  // the stream device work is enqueued on now (own or a caller's)
-  hipEvent_t xev = nullptr;      // orders a newly used stream after the previous one
-  std::string device_name;
-  std::mutex map_mu;
-  std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
-  std::mutex work_mu;  // scratch buffers + stream
-  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
-  DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
-  DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
-  DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
-  DevBuf scratch8;                  // u64 result of the snapshot checksum
-  DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
-  DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch
-  // device-resident filters (vs_filter_create), guarded by work_mu
-  struct DevFilter {
-    std::string coll;
-    uint64_t coll_gen = 0;           // Collection::gen it was built for
-    uint64_t rows = 0, allowed = 0;  // collection rows it was built over
-    DevBuf bits, list;               // bitmap; compacted rows when selective
-  };
-  std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
-  uint64_t next_filter = 1;
-  uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
-  std::vector<uint64_t> h_keys;
-  // timing
-  std::vector<EventPair> scan_ev, merge_ev;
-  std::vector<hipEvent_t> ev_pool;  // recycled timing events (none created on the hot path)
-  double scan_ms = 0, merge_ms = 0;
-  uint64_t scan_n = 0, merge_n = 0;
-  uint64_t scan_tick = 0;   // scan launches seen (VS_FLAG_TIMING_SAMPLE)
-  bool scan_skip = false;   // the current scan launch is not bracketed
-};
-
-namespace {
 
 std::atomic<uint64_t> g_coll_gen{1};
 
-std::shared_ptr<Collection> find_coll(vs_engine* eng, const char* name) {
+std::shared_ptr<Collection> find_coll(DevEngine* eng, const char* name) {
   std::lock_guard<std::mutex> g(eng->map_mu);
   auto it = eng->colls.find(name ? name : "");
   return it == eng->colls.end() ? nullptr : it->second;
 }
 
-hipError_t set_dev(vs_engine* eng) { return hipSetDevice(eng->device); }
+hipError_t set_dev(DevEngine* eng) { return hipSetDevice(eng->device); }
 
 // Makes `s` the engine's current stream (work_mu held). Work enqueued on s
 // is ordered after everything enqueued so far on the previous stream, so the
 // scratch buffers are never used by two streams at once; a caller that keeps
 // using one stream (a serving loop on torch's current stream) pays nothing.
-hipError_t use_stream(vs_engine* eng, hipStream_t s) {
+hipError_t use_stream(DevEngine* eng, hipStream_t s) {
   if (s == eng->stream) return hipSuccess;
   hipError_t e = hipEventRecord(eng->xev, eng->stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->xev, 0);
@@ -149,13 +62,13 @@ hipError_t use_stream(vs_engine* eng, hipStream_t s) {
   return e;
 }
 
-bool timing_on(vs_engine* eng) { return (eng->flags & VS_FLAG_TIMING) != 0; }
+bool timing_on(DevEngine* eng) { return (eng->flags & VS_FLAG_TIMING) != 0; }
 
-bool timing_wanted(vs_engine* eng, const std::vector<EventPair>& v) {
+bool timing_wanted(DevEngine* eng, const std::vector<EventPair>& v) {
   return timing_on(eng) && (&v == &eng->scan_ev || (eng->flags & VS_FLAG_TIMING_MERGE));
 }
 
-hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
+hipError_t ev_begin(DevEngine* eng, std::vector<EventPair>& v) {
   if (!timing_wanted(eng, v)) return hipSuccess;
   if (&v == &eng->scan_ev && (eng->flags & VS_FLAG_TIMING_SAMPLE)) {
     eng->scan_skip = (eng->scan_tick++ & 3) != 0;  // bracket every 4th scan only
@@ -174,7 +87,7 @@ hipError_t ev_begin(vs_engine* eng, std::vector<EventPair>& v) {
   v.push_back(p);
   return hipEventRecord(p.a, eng->stream);
 }
-hipError_t ev_end(vs_engine* eng, std::vector<EventPair>& v) {
+hipError_t ev_end(DevEngine* eng, std::vector<EventPair>& v) {
   if (!timing_wanted(eng, v) || v.empty()) return hipSuccess;
   if (&v == &eng->scan_ev && (eng->flags & VS_FLAG_TIMING_SAMPLE) && eng->scan_skip)
     return hipSuccess;
@@ -192,9 +105,11 @@ constexpr uint64_t kGatherDensityDen = 8;
 // Per-query launch overhead of a gathered scan (scan + merge launches,
 // ~10 us) in bytes of HBM streaming, for the batch decision in search_core.
 constexpr uint64_t kGatherCallBytes = 64ull << 20;
+// Smallest batch of an fp32 collection that takes the MFMA pass.
+constexpr uint32_t kF32MfmaMinQueries = 4;
 
 // Grows a collection to hold `need` rows (writer lock held by the caller).
-int grow(vs_engine* eng, Collection& c, uint64_t need) {
+int grow(DevEngine* eng, Collection& c, uint64_t need) {
   if (need <= c.cap) return VS_OK;
   uint64_t ncap = std::max<uint64_t>({need, c.cap + c.cap / 2, 1024});
   void* nd = nullptr;
@@ -283,7 +198,7 @@ struct FileCloser {
   }
 };
 
-int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
+int device_checksum(DevEngine* eng, const Collection& c, uint64_t* out) {
   VS_HIP(eng->scratch8.ensure(8), "alloc checksum");
   VS_HIP(vsk::launch_checksum(c.data, c.rows * c.row_bytes(), eng->scratch8.as<uint64_t>(),
                               eng->stream),
@@ -298,7 +213,7 @@ int device_checksum(vs_engine* eng, const Collection& c, uint64_t* out) {
 // -> keys d_keys[i * k], one scan + merge per query. For bf16 collections qp
 // already holds bf16-rounded values (search_core's query prep). With `gather`
 // (n_gather device row indices) only those rows are scanned.
-int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
+int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr,
                 const uint32_t* gather = nullptr, uint32_t n_gather = 0) {
   const uint32_t dim = c.dim;
@@ -335,12 +250,13 @@ int search_gemv(vs_engine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
 //     exactly -- the sorted-list pass + merge for k <= 16 (device-side, no
 //     host sync: both launches are no-ops unless the flag is set), the GEMV
 //     path for larger k (after a host check of the flag).
-int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow) {
+int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
+                uint64_t* d_keys, const uint64_t* allow, std::vector<DeferredCheck>* defer) {
   const uint32_t dim = c.dim;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
-  const uint32_t P = vsk::mfma_queries(dim);  // queries per pass
+  const bool f32 = c.dtype == VS_DTYPE_F32;
+  const uint32_t P = vsk::mfma_queries(dim, f32);  // queries per pass
   const uint32_t PS = vsk::kMfmaQueries;      // query stride of the pass buffers
   const uint32_t npass = (nq + P - 1) / P;
   const uint32_t maxl = vsk::mfma_max_lists(n_rows);
@@ -377,18 +293,45 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
     }
   }
-  const uint16_t* X = (const uint16_t*)c.data;
+  const void* X = c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
-  uint32_t* ovf = eng->overflow.as<uint32_t>();
+  const bool dev_fb = k <= vsk::kMfmaListMaxK;
+  // a deferred pass gets a flag word of its own (its sample select clears
+  // it, its main pass sets it), read by the caller after every shard's
+  // scans were enqueued; the next deferred slots of this call follow
+  if (!dev_fb && defer) {
+    const size_t want = (eng->ovf_next + npass) * 4;
+    if (eng->ovf_slots.bytes < want) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      DevBuf grown;
+      VS_HIP(grown.ensure(std::max(want * 2, (size_t)1024)), "alloc flag slots");
+      if (eng->ovf_slots.p && eng->ovf_next)
+        VS_HIP(hipMemcpyAsync(grown.p, eng->ovf_slots.p, eng->ovf_next * 4,
+                              hipMemcpyDeviceToDevice, eng->stream),
+               "flag slots copy");
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      std::swap(grown.p, eng->ovf_slots.p);
+      std::swap(grown.bytes, eng->ovf_slots.bytes);
+    }
+  }
   for (uint32_t p = 0; p < npass; ++p) {
+    uint32_t slot = 0;
+    uint32_t* ovf = eng->overflow.as<uint32_t>();
+    if (!dev_fb && defer) {
+      slot = eng->ovf_next++;
+      ovf = eng->ovf_slots.as<uint32_t>() + slot;
+    }
     const uint32_t q0 = p * P;
     const uint32_t nv = std::min(P, nq - q0);
     uint64_t* out = d_keys + (size_t)q0 * k;
-    const uint16_t* qb = eng->q_bf16.as<uint16_t>() + (size_t)q0 * dim;
+    // the pass's queries in the collection's dtype: the bf16 copy, or the
+    // preprocessed fp32 queries themselves (zero-padded past nq)
+    const void* qb = f32 ? (const void*)(qp + (size_t)q0 * dim)
+                         : (const void*)(eng->q_bf16.as<uint16_t>() + (size_t)q0 * dim);
     uint32_t L = 0;
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
+      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
                                     lists, maxl, &L, eng->stream, allow),
              "mfma scan (lists)");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
@@ -400,7 +343,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     }
     // 1. sample pass -> bound keys skeys[q * k + k - 1]
     uint64_t* skeys = eng->sample_keys.as<uint64_t>();
-    VS_HIP(vsk::launch_mfma_sample(X, dim, n_rows, row_base, qb, nv, k, st,
+    VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qb, nv, k, st,
                                    eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), maxl,
                                    &L, eng->stream, allow),
            "mfma sample scan");
@@ -412,7 +355,7 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     float* slabs = eng->cand.as<float>();
     uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + sl_bytes);
-    VS_HIP(vsk::launch_mfma_cand(X, dim, n_rows, row_base, qb, nv, k, init, k, slabs, slab_tile,
+    VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, slabs, slab_tile,
                                  cap, eng->cand_cnt.as<uint32_t>(), ovf, maxl, &L, eng->stream,
                                  allow),
            "mfma scan");
@@ -420,10 +363,9 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // 3. overflow fallback, k <= 16: the sorted-list pass (a no-op launch
     // unless the main pass set the flag), whose lists the select then merges
     // in place of the slabs
-    const bool dev_fb = k <= vsk::kMfmaListMaxK;
     uint32_t Lf = 0;
     if (dev_fb)
-      VS_HIP(vsk::launch_mfma_lists(X, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
+      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
                                     maxl, &Lf, eng->stream, allow),
              "mfma scan (fallback)");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -433,7 +375,9 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                     eng->fallbacks.as<uint32_t>()),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
-    if (!dev_fb) {
+    if (!dev_fb && defer) {
+      defer->push_back(DeferredCheck{&c, qp, q0, nv, k, out, slot});
+    } else if (!dev_fb) {
       uint32_t h_ovf = 0;
       VS_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, eng->stream), "flag D2H");
       VS_HIP(hipStreamSynchronize(eng->stream), "flag sync");
@@ -450,9 +394,9 @@ int search_mfma(vs_engine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // Core search on device data. d_q: nq x dim fp32 on this device, ordered on
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
-int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
-                const uint32_t* allow_list = nullptr) {
+int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
+                uint64_t* d_keys, const uint64_t* allow, uint64_t allowed,
+                const uint32_t* allow_list, std::vector<DeferredCheck>* defer) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -463,14 +407,22 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   if (c.rows >= 0xFFFFFFFFull || c.row_base + c.rows >= 0xFFFFFFFFull)
     return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
 
-  // 1. query preprocessing (cosine normalise) -> q_pre (fp32)
-  const size_t qbytes = (size_t)nq * dim * 4;
+  // 1. query preprocessing (cosine normalise) -> q_pre (fp32). The fp32
+  // MFMA path reads q_pre directly, whole passes of kMfmaQueries rows: rows
+  // past nq are padding (zeroed at allocation; later only ever finite
+  // queries of earlier calls), masked by the kernels.
+  const size_t qbytes = (size_t)((nq + vsk::kMfmaQueries - 1) / vsk::kMfmaQueries) *
+                        vsk::kMfmaQueries * dim * 4;
   if (eng->q_pre.bytes < qbytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->q_pre.ensure(qbytes), "alloc query scratch");
+    VS_HIP(hipMemsetAsync(eng->q_pre.p, 0, eng->q_pre.bytes, eng->stream), "zero query scratch");
   }
   float* qp = eng->q_pre.as<float>();
-  bool use_mfma = bf16 && nq >= 2 && k <= vsk::kMfmaMaxK && vsk::mfma_supported(dim);
+  // batched path: bf16 collections from 2 queries, fp32 ones from 4 (the fp32
+  // pass is MFMA-bound at 1/16 of the bf16 rate: ~3 single-query HBM scans)
+  bool use_mfma = nq >= (bf16 ? 2u : kF32MfmaMinQueries) && k <= vsk::kMfmaMaxK &&
+                  vsk::mfma_supported(dim, !bf16);
   // selective filter: scan only the allowed rows, gathered through a
   // compacted row list (cost ~ allowed rows instead of all rows), one GEMV
   // per query. A batch leaves the MFMA pass for it only while nq gathers
@@ -481,10 +433,10 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                       (!use_mfma || (double)nq * (double)(allowed * rbytes + kGatherCallBytes) <=
                                         (double)c.rows * (double)rbytes);
   if (gather) use_mfma = false;
-  // the MFMA path reads a bf16 copy, 256 queries per pass (rows past nq are
-  // padding: finite, and masked by the kernels)
+  // the bf16 MFMA path reads a bf16 copy, 256 queries per pass (rows past nq
+  // are padding: finite, and masked by the kernels)
   uint16_t* qb = nullptr;
-  if (use_mfma) {
+  if (use_mfma && bf16) {
     const uint32_t P = vsk::kMfmaQueries;
     const size_t bbytes = (size_t)((nq + P - 1) / P) * P * dim * 2;
     if (eng->q_bf16.bytes < bbytes) {
@@ -494,13 +446,13 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     }
     qb = eng->q_bf16.as<uint16_t>();
   }
-  // the fp32 copy feeds the GEMV path only: the MFMA path needs it just for
-  // its k > 16 fallback
-  const bool need_qp = !use_mfma || k > vsk::kMfmaListMaxK;
+  // the fp32 copy feeds the GEMV path and the fp32 MFMA path; the bf16 MFMA
+  // path needs it just for its k > 16 fallback
+  const bool need_qp = !use_mfma || !bf16 || k > vsk::kMfmaListMaxK;
   VS_HIP(vsk::launch_query_prep(d_q, nq, dim, cosine, bf16, need_qp ? qp : nullptr, qb,
                                 eng->stream),
          "query preprocess");
-  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
+  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow, defer);
   if (gather) {
     if (allowed == 0) {
       VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
@@ -523,6 +475,12 @@ int search_core(vs_engine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
 }
 
+int rerun_deferred(DevEngine* eng, const DeferredCheck& d) {
+  const int rc = search_gemv(eng, *d.coll, d.qp, d.q0, d.nv, d.k, d.out);
+  if (rc == VS_OK) eng->host_fallbacks++;
+  return rc;
+}
+
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
                  uint64_t* rows, uint32_t* count) {
   for (uint32_t i = 0; i < nq; ++i) {
@@ -542,32 +500,22 @@ void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
   }
 }
 
-}  // namespace
 
-extern "C" {
+const char* last_error() { return g_last_error.c_str(); }
 
-const char* vs_last_error(void) { return g_last_error.c_str(); }
-
-int vs_device_count(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-  return n;
-}
-
-int vs_open(const vs_config* cfg, vs_engine** out) {
+int open(int dev, uint32_t flags, DevEngine** out) {
   if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
   *out = nullptr;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0)
     return fail(VS_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
-  int dev = cfg ? cfg->device : -1;
   if (dev < 0) VS_HIP(hipGetDevice(&dev), "hipGetDevice");
   if (dev >= n) return fail(VS_ERR_INVALID_ARG, "device ordinal out of range");
   VS_HIP(hipSetDevice(dev), "hipSetDevice");
-  auto eng = std::make_unique<vs_engine>();
+  auto eng = std::make_unique<DevEngine>();
   eng->device = dev;
-  eng->flags = cfg ? cfg->flags : 0;
+  eng->flags = flags;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
     eng->device_name = std::string(prop.name) + " " + prop.gcnArchName;
@@ -579,7 +527,7 @@ int vs_open(const vs_config* cfg, vs_engine** out) {
   return VS_OK;
 }
 
-void vs_close(vs_engine* eng) {
+void close(DevEngine* eng) {
   if (!eng) return;
   (void)hipSetDevice(eng->device);
   (void)hipStreamSynchronize(eng->stream);
@@ -599,7 +547,7 @@ void vs_close(vs_engine* eng) {
   delete eng;
 }
 
-int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim, int metric, int dtype,
+int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric, int dtype,
                          uint64_t capacity_hint, uint64_t row_base) {
   if (!eng || !name || !*name) return fail(VS_ERR_INVALID_ARG, "collection name required");
   if (dim == 0 || dim > 65536) return fail(VS_ERR_INVALID_ARG, "dim must be in [1, 65536]");
@@ -635,7 +583,7 @@ int vs_collection_create(vs_engine* eng, const char* name, uint32_t dim, int met
   return VS_OK;
 }
 
-int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim, uint64_t* rows,
+int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* rows,
                        int* metric, int* dtype) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   auto c = find_coll(eng, name);
@@ -649,7 +597,7 @@ int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim, uint64_t
   return VS_OK;
 }
 
-int vs_collection_drop(vs_engine* eng, const char* name) {
+int collection_drop(DevEngine* eng, const char* name) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   std::shared_ptr<Collection> c;
   {
@@ -673,7 +621,7 @@ int vs_collection_drop(vs_engine* eng, const char* name) {
   return VS_OK;  // memory released with the last reference
 }
 
-int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim_in,
+int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
               const uint64_t* rows, const float* vecs) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (n == 0) return VS_OK;
@@ -745,7 +693,8 @@ int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim_in,
   return VS_OK;
 }
 
-int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed) {
+int generate(DevEngine* eng, const char* coll, uint64_t n, uint64_t seed, uint64_t g0,
+             uint64_t stride) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
@@ -758,15 +707,17 @@ int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed) {
   VS_HIP(use_stream(eng, eng->own), "stream order");
   int rc = grow(eng, *c, c->rows + n);
   if (rc != VS_OK) return rc;
-  VS_HIP(vsk::launch_generate(seed, c->row_base + c->rows, n, c->dim,
-                              c->dtype == VS_DTYPE_BF16, c->data, c->rows, eng->stream),
+  // g0 == UINT64_MAX: the collection's own next global rows (row_base + rows)
+  if (g0 == UINT64_MAX) g0 = c->row_base + c->rows, stride = 1;
+  VS_HIP(vsk::launch_generate(seed, g0, n, c->dim, c->dtype == VS_DTYPE_BF16, c->data, c->rows,
+                              eng->stream, stride),
          "generate");
   VS_HIP(hipStreamSynchronize(eng->stream), "generate sync");
   c->rows += n;
   return VS_OK;
 }
 
-int vs_generate_vectors(vs_engine* eng, uint64_t seed, uint64_t row0, uint64_t n, uint32_t dim,
+int generate_vectors(DevEngine* eng, uint64_t seed, uint64_t row0, uint64_t n, uint32_t dim,
                         float* d_out, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (n == 0) return VS_OK;
@@ -777,7 +728,7 @@ int vs_generate_vectors(vs_engine* eng, uint64_t seed, uint64_t row0, uint64_t n
   return VS_OK;
 }
 
-int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, float* out) {
+int read_rows(DevEngine* eng, const char* coll, uint64_t first, uint64_t n, float* out) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
@@ -807,7 +758,70 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, f
   return VS_OK;
 }
 
-namespace {
+// Stored rows [first, first + n) as stored (bf16 / fp32 bytes) -> host.
+int read_raw(DevEngine* eng, const char* coll, uint64_t first, uint64_t n, void* out) {
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  if (first + n > c->rows || first + n < first)
+    return fail(VS_ERR_INVALID_ARG, "row range out of bounds");
+  if (n == 0) return VS_OK;
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  VS_HIP(hipMemcpyAsync(out, (const char*)c->data + first * c->row_bytes(), n * c->row_bytes(),
+                        hipMemcpyDeviceToHost, eng->stream),
+         "read D2H");
+  VS_HIP(hipStreamSynchronize(eng->stream), "read sync");
+  return VS_OK;
+}
+
+// Appends n rows given exactly as stored (no preprocessing): restore path.
+int append_raw(DevEngine* eng, const char* coll, uint64_t n, const void* rows) {
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  if (n == 0) return VS_OK;
+  std::unique_lock<std::shared_mutex> wl(c->mu);
+  if (c->rows + n >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  int rc = grow(eng, *c, c->rows + n);
+  if (rc != VS_OK) return rc;
+  VS_HIP(hipMemcpyAsync((char*)c->data + c->rows * c->row_bytes(), rows, n * c->row_bytes(),
+                        hipMemcpyHostToDevice, eng->stream),
+         "restore H2D");
+  VS_HIP(hipStreamSynchronize(eng->stream), "restore sync");
+  c->rows += n;
+  return VS_OK;
+}
+
+// Checksum contribution of one shard of a row-striped collection
+// (vsk::launch_checksum_rows); the collection's checksum is the sum.
+int checksum_shard(DevEngine* eng, const char* coll, uint64_t stride, uint64_t offset,
+                   uint64_t* out) {
+  auto c = find_coll(eng, coll);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  if (c->row_bytes() % 8)
+    return fail(VS_ERR_INVALID_ARG, "a sharded collection's checksum needs rows of whole "
+                                    "8-byte words (bf16: dim % 4 == 0, fp32: dim % 2 == 0)");
+  std::lock_guard<std::mutex> g(eng->work_mu);
+  VS_HIP(set_dev(eng), "hipSetDevice");
+  VS_HIP(use_stream(eng, eng->own), "stream order");
+  VS_HIP(eng->scratch8.ensure(8), "alloc checksum");
+  VS_HIP(vsk::launch_checksum_rows(c->data, c->rows, (uint32_t)c->row_bytes(), stride, offset,
+                                   eng->scratch8.as<uint64_t>(), eng->stream),
+         "checksum");
+  VS_HIP(hipMemcpyAsync(out, eng->scratch8.p, 8, hipMemcpyDeviceToHost, eng->stream),
+         "checksum D2H");
+  VS_HIP(hipStreamSynchronize(eng->stream), "checksum sync");
+  return VS_OK;
+}
+
 // vs_search / vs_search_filtered: host queries in, host results out.
 // Popcount of the bitmap over the collection's rows (on the host, which holds
 // the bitmap: 156k words at 10M rows). The build targets baseline x86-64, where
@@ -835,10 +849,10 @@ uint64_t popcount_rows(const uint64_t* allow, uint64_t rows) {
   return allowed + (uint64_t)__builtin_popcountll(w);
 }
 
-int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
+int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t nq,
                 uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count,
-                uint64_t filter_id = 0) {
+                uint64_t filter_id) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
   if (nq == 0) return VS_OK;
@@ -855,7 +869,7 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
                                         " words, the collection needs " +
                                         std::to_string((c->rows + 63) / 64));
   std::lock_guard<std::mutex> g(eng->work_mu);
-  const vs_engine::DevFilter* df = nullptr;
+  const DevEngine::DevFilter* df = nullptr;
   if (filter_id) {
     auto it = eng->filters.find(filter_id);
     if (it == eng->filters.end())
@@ -899,24 +913,8 @@ int search_host(vs_engine* eng, const char* coll, const float* queries, uint32_t
   decode_host(eng->h_keys.data(), nq, k, out_scores, out_rows, out_count);
   return VS_OK;
 }
-}  // namespace
 
-int vs_search(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
-              uint32_t dim, uint32_t k, float* out_scores, uint64_t* out_rows,
-              uint32_t* out_count) {
-  return search_host(eng, coll, queries, nq, dim, k, nullptr, 0, out_scores, out_rows,
-                     out_count);
-}
-
-int vs_search_filtered(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
-                       uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
-                       float* out_scores, uint64_t* out_rows, uint32_t* out_count) {
-  if (!allow) return fail(VS_ERR_INVALID_ARG, "allow bitmap is NULL");
-  return search_host(eng, coll, queries, nq, dim, k, allow, allow_words, out_scores, out_rows,
-                     out_count);
-}
-
-int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
+int filter_create(DevEngine* eng, const char* coll, const uint64_t* allow,
                      uint64_t allow_words, uint64_t* filter_id) {
   if (!eng || !allow || !filter_id) return fail(VS_ERR_INVALID_ARG, "NULL argument");
   auto c = find_coll(eng, coll);
@@ -931,7 +929,7 @@ int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(use_stream(eng, eng->own), "stream order");
-  auto f = std::make_unique<vs_engine::DevFilter>();
+  auto f = std::make_unique<DevEngine::DevFilter>();
   f->coll = coll;
   f->coll_gen = c->gen;
   f->rows = c->rows;
@@ -959,7 +957,7 @@ int vs_filter_create(vs_engine* eng, const char* coll, const uint64_t* allow,
   return VS_OK;
 }
 
-int vs_filter_drop(vs_engine* eng, uint64_t filter_id) {
+int filter_drop(DevEngine* eng, uint64_t filter_id) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   std::lock_guard<std::mutex> g(eng->work_mu);
   auto it = eng->filters.find(filter_id);
@@ -971,15 +969,7 @@ int vs_filter_drop(vs_engine* eng, uint64_t filter_id) {
   return VS_OK;
 }
 
-int vs_search_filter_id(vs_engine* eng, const char* coll, const float* queries, uint32_t nq,
-                        uint32_t dim, uint32_t k, uint64_t filter_id, float* out_scores,
-                        uint64_t* out_rows, uint32_t* out_count) {
-  if (!filter_id) return fail(VS_ERR_INVALID_ARG, "filter id 0");
-  return search_host(eng, coll, queries, nq, dim, k, nullptr, 0, out_scores, out_rows,
-                     out_count, filter_id);
-}
-
-int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uint32_t nq,
+int search_keys(DevEngine* eng, const char* coll, const float* d_queries, uint32_t nq,
                    uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
@@ -999,7 +989,7 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
   return search_core(eng, *c, d_queries, nq, k, d_keys);
 }
 
-int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
+int merge_keys(DevEngine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
                   uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (k == 0 || k > vsk::kMaxK || k_in == 0 || n_lists == 0)
@@ -1016,7 +1006,7 @@ int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uin
   return VS_OK;
 }
 
-int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
+int decode_keys(DevEngine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
                    float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (nq == 0 || k == 0) return VS_OK;
@@ -1030,7 +1020,7 @@ int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t
   return VS_OK;
 }
 
-int vs_checksum(vs_engine* eng, const char* coll, uint64_t* out) {
+int checksum(DevEngine* eng, const char* coll, uint64_t* out) {
   if (!eng || !out) return fail(VS_ERR_INVALID_ARG, "engine and out are required");
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
@@ -1042,7 +1032,7 @@ int vs_checksum(vs_engine* eng, const char* coll, uint64_t* out) {
   return device_checksum(eng, *c, out);
 }
 
-int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
+int snapshot(DevEngine* eng, const char* coll, const char* path) {
   if (!eng || !path) return fail(VS_ERR_INVALID_ARG, "engine and path are required");
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (coll ? coll : "") +
@@ -1107,7 +1097,7 @@ int vs_snapshot(vs_engine* eng, const char* coll, const char* path) {
   return VS_OK;
 }
 
-int vs_restore(vs_engine* eng, const char* coll, const char* path) {
+int restore(DevEngine* eng, const char* coll, const char* path) {
   if (!eng || !path || !coll || !*coll)
     return fail(VS_ERR_INVALID_ARG, "engine, collection and path are required");
   FileCloser fc;
@@ -1120,7 +1110,7 @@ int vs_restore(vs_engine* eng, const char* coll, const char* path) {
   const uint32_t elem = h.dtype == VS_DTYPE_BF16 ? 2 : 4;
   if (h.elem_bytes != elem || h.data_bytes != h.rows * h.dim * (uint64_t)elem)
     return fail(VS_ERR_IO, std::string("inconsistent snapshot header: ") + path);
-  int rc = vs_collection_create(eng, coll, h.dim, h.metric, h.dtype, h.rows, h.row_base);
+  int rc = collection_create(eng, coll, h.dim, h.metric, h.dtype, h.rows, h.row_base);
   if (rc != VS_OK) return rc;
   auto c = find_coll(eng, coll);
   if (!c) return fail(VS_ERR_INTERNAL, "restored collection vanished");
@@ -1158,7 +1148,7 @@ int vs_restore(vs_engine* eng, const char* coll, const char* path) {
     if (err == VS_OK) {
       c->rows = h.rows;
       err = device_checksum(eng, *c, &sum);
-      if (err != VS_OK) msg = vs_last_error();
+      if (err != VS_OK) msg = last_error();
       else if (sum != h.data_checksum) {
         err = VS_ERR_IO;
         msg = std::string("snapshot checksum mismatch: ") + path;
@@ -1167,13 +1157,13 @@ int vs_restore(vs_engine* eng, const char* coll, const char* path) {
   }
   wl.unlock();
   if (err != VS_OK) {
-    (void)vs_collection_drop(eng, coll);
+    (void)collection_drop(eng, coll);
     return fail(err, msg);
   }
   return VS_OK;
 }
 
-int vs_health(vs_engine* eng, char* buf, size_t len) {
+int health(DevEngine* eng, char* buf, size_t len) {
   if (!eng || !buf || len == 0) return fail(VS_ERR_INVALID_ARG, "bad health buffer");
   size_t freeb = 0, totalb = 0;
   std::string status = "healthy", err;
@@ -1212,8 +1202,8 @@ int vs_health(vs_engine* eng, char* buf, size_t len) {
   return e == hipSuccess ? VS_OK : fail(VS_ERR_DEVICE, err);
 }
 
-int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double* merge_ms_avg,
-              uint64_t* merge_count, int reset) {
+int timing(DevEngine* eng, double* scan_ms_sum, uint64_t* scan_count, double* merge_ms_sum,
+           uint64_t* merge_count, int reset) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
@@ -1232,9 +1222,9 @@ int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double*
   };
   drain(eng->scan_ev, eng->scan_ms, eng->scan_n);
   drain(eng->merge_ev, eng->merge_ms, eng->merge_n);
-  if (scan_ms_avg) *scan_ms_avg = eng->scan_n ? eng->scan_ms / eng->scan_n : 0.0;
+  if (scan_ms_sum) *scan_ms_sum = eng->scan_ms;
   if (scan_count) *scan_count = eng->scan_n;
-  if (merge_ms_avg) *merge_ms_avg = eng->merge_n ? eng->merge_ms / eng->merge_n : 0.0;
+  if (merge_ms_sum) *merge_ms_sum = eng->merge_ms;
   if (merge_count) *merge_count = eng->merge_n;
   if (reset) {
     eng->scan_ms = eng->merge_ms = 0;
@@ -1244,4 +1234,4 @@ int vs_timing(vs_engine* eng, double* scan_ms_avg, uint64_t* scan_count, double*
   return VS_OK;
 }
 
-}  // extern "C"
+}  // namespace vsd

@@ -40,9 +40,11 @@ hipError_t launch_query_prep(const float* in, uint32_t n, uint32_t dim, bool cos
 
 // Generate n synthetic unit rows with global numbers grow0 .. grow0+n-1 and
 // store them into dst rows dst0 .. (bf16 or fp32), or as fp32 when f32_out.
+// Global numbers advance by gstride per row (a shard of a row-striped
+// collection holds every gstride-th global row).
 hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
                            uint32_t dim, bool bf16, void* dst, uint64_t dst0,
-                           hipStream_t st);
+                           hipStream_t st, uint64_t gstride = 1);
 
 // Single-query scan (GEMV) with per-wave register top-k. Writes one sorted
 // key list of length k per workgroup to out[nlists][k]; returns nlists.
@@ -62,10 +64,11 @@ uint32_t compact_scratch_words(uint32_t n_rows);
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 
-// Batched bf16 scan on MFMA with fused top-k. Q is
-// kMfmaQueries x dim bf16 (zero-padded), nq_valid <= kMfmaQueries, k <=
-// kMfmaMaxK; one workgroup per CU streams a contiguous row range (nlists
-// workgroups).
+// Batched scan on MFMA with fused top-k: bf16 rows on
+// v_mfma_f32_16x16x32_bf16, or fp32 rows (f32) on v_mfma_f32_16x16x4_f32.
+// X and Q are the collection's dtype; Q is kMfmaQueries x dim (zero-padded),
+// nq_valid <= mfma_queries(dim, f32), k <= kMfmaMaxK; one workgroup per CU
+// streams a contiguous row range (nlists workgroups).
 //  * sample pass: first max_tiles 32-row tiles of every workgroup; each
 //    tile's maximum per query -> cand[nlists][kMfmaQueries][4 * max_tiles]
 //    with counts cand_cnt; launch_select(.., cap = 4 * max_tiles, k, ..) then
@@ -85,21 +88,21 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //    unless run_if is null or *run_if != 0.
 // `allow` (nullable, all passes): filter pre-mask, bit r of allow[r / 64]
 // admits local row r; masked rows are never candidates, maxima or results.
-bool mfma_supported(uint32_t dim);
-uint32_t mfma_queries(uint32_t dim);  // queries per launch at this dim
-hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
-                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+bool mfma_supported(uint32_t dim, bool f32);
+uint32_t mfma_queries(uint32_t dim, bool f32);  // queries per launch at this dim
+hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
                               uint32_t max_lists, uint32_t* nlists, hipStream_t st,
                               const uint64_t* allow = nullptr);
-hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
-                            const uint16_t* Q, uint32_t nq_valid, uint32_t k,
+hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                            uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, float* slabs,
                             uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
                             uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow = nullptr);
-hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
-                             uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
@@ -150,6 +153,13 @@ hipError_t launch_round_bf16(const float* in, uint64_t n, float* out,
 
 // Snapshot checksum of nbytes at p (vs::snap_word summed) -> *d_out (device).
 hipError_t launch_checksum(const void* p, uint64_t nbytes, uint64_t* d_out, hipStream_t st);
+// The same over one shard of a row-striped collection: rows x row_bytes
+// (row_bytes % 8 == 0), local row l = global row l * stride + offset.
+hipError_t launch_checksum_rows(const void* p, uint64_t rows, uint32_t row_bytes, uint64_t stride,
+                                uint64_t offset, uint64_t* d_out, hipStream_t st);
+// Shard keys (local rows) -> global rows base + local * stride + offset.
+hipError_t launch_remap_keys(uint64_t* keys, uint64_t n, uint32_t stride, uint32_t offset,
+                             uint32_t base, hipStream_t st);
 
 int device_cu_count();
 

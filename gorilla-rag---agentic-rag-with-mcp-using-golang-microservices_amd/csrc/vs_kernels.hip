@@ -255,6 +255,62 @@ __global__ __launch_bounds__(256) void checksum_kernel(const u32x4_ck* __restric
   if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)out, (unsigned long long)s);
 }
 
+// The same sum over the rows of one shard of a row-striped collection
+// (global row = local * stride + offset; row_bytes % 8 == 0, so a row is a
+// whole number of words): word w of local row l carries the global word
+// index (l * stride + offset) * row_bytes / 8 + w. Summing the shards' sums
+// gives the checksum of the collection in global row order.
+__global__ __launch_bounds__(256) void checksum_rows_kernel(const uint64_t* __restrict__ p,
+                                                            uint64_t nwords, uint32_t wpr,
+                                                            uint64_t stride, uint64_t offset,
+                                                            uint64_t* __restrict__ out) {
+  uint64_t s = 0;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nwords; j += step) {
+    const uint64_t l = j / wpr, w = j - l * wpr;
+    s += vs::snap_word(__builtin_nontemporal_load(p + j), (l * stride + offset) * wpr + w);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)out, (unsigned long long)s);
+}
+
+hipError_t launch_checksum_rows(const void* p, uint64_t rows, uint32_t row_bytes, uint64_t stride,
+                                uint64_t offset, uint64_t* d_out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(d_out, 0, 8, st);
+  if (e != hipSuccess || rows == 0) return e;
+  if ((uintptr_t)p % 8 || row_bytes % 8) return hipErrorInvalidValue;
+  const uint64_t nwords = rows * (row_bytes / 8);
+  uint64_t blocks = (nwords + 255) / 256;
+  const uint64_t cap = (uint64_t)device_cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(checksum_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const uint64_t*)p, nwords, row_bytes / 8, stride, offset, d_out);
+  return hipGetLastError();
+}
+
+// Shard keys (local rows) -> global rows of a row-striped collection:
+// global = base + local * stride + offset. Order-preserving within a shard
+// (local row order = global row order), so a shard's sorted list stays
+// sorted and ties keep the row-ascending rule. 0 (empty) stays 0.
+__global__ void remap_keys_kernel(uint64_t* __restrict__ keys, uint64_t n, uint32_t stride,
+                                  uint32_t offset, uint32_t base) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t key = keys[i];
+  if (key == 0) return;
+  const uint32_t local = vs::key_row(key);
+  keys[i] = (key & 0xFFFFFFFF00000000ull) | (uint32_t)(0xFFFFFFFFu - (base + local * stride + offset));
+}
+
+hipError_t launch_remap_keys(uint64_t* keys, uint64_t n, uint32_t stride, uint32_t offset,
+                             uint32_t base, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(remap_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, keys,
+                     n, stride, offset, base);
+  return hipGetLastError();
+}
+
 hipError_t launch_checksum(const void* p, uint64_t nbytes, uint64_t* d_out, hipStream_t st) {
   hipError_t e = hipMemsetAsync(d_out, 0, 8, st);
   if (e != hipSuccess || nbytes == 0) return e;
@@ -274,13 +330,13 @@ hipError_t launch_checksum(const void* p, uint64_t nbytes, uint64_t* d_out, hipS
 // division and sqrt are correctly rounded fp64 ops, so host and device agree.
 template <bool BF16>
 __global__ __launch_bounds__(256) void generate_kernel(uint64_t seed, uint64_t grow0,
-                                                       uint64_t n, uint32_t dim,
+                                                       uint64_t gstride, uint64_t n, uint32_t dim,
                                                        void* __restrict__ dst,
                                                        uint64_t dst0) {
   const int lane = threadIdx.x & 63;
   const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
-  const uint64_t rk = vs::gen_row_key(seed, grow0 + i);
+  const uint64_t rk = vs::gen_row_key(seed, grow0 + i * gstride);
   long long s = 0;
   for (uint32_t d = lane; d < dim; d += 64) {
     const long long m = vs::gen_int(rk, d);
@@ -301,18 +357,18 @@ __global__ __launch_bounds__(256) void generate_kernel(uint64_t seed, uint64_t g
 
 hipError_t launch_generate(uint64_t seed, uint64_t grow0, uint64_t n,
                            uint32_t dim, bool bf16, void* dst, uint64_t dst0,
-                           hipStream_t st) {
+                           hipStream_t st, uint64_t gstride) {
   if (n == 0) return hipSuccess;
   const uint64_t kChunk = 1ull << 24;  // keep gridDim.x well below 2^31
   for (uint64_t o = 0; o < n; o += kChunk) {
     const uint64_t m = (n - o < kChunk) ? n - o : kChunk;
     dim3 grid((unsigned)((m + 3) / 4)), block(256);
     if (bf16)
-      hipLaunchKernelGGL(generate_kernel<true>, grid, block, 0, st, seed, grow0 + o, m,
-                         dim, dst, dst0 + o);
+      hipLaunchKernelGGL(generate_kernel<true>, grid, block, 0, st, seed, grow0 + o * gstride,
+                         gstride, m, dim, dst, dst0 + o);
     else
-      hipLaunchKernelGGL(generate_kernel<false>, grid, block, 0, st, seed, grow0 + o, m,
-                         dim, dst, dst0 + o);
+      hipLaunchKernelGGL(generate_kernel<false>, grid, block, 0, st, seed, grow0 + o * gstride,
+                         gstride, m, dim, dst, dst0 + o);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -861,7 +917,11 @@ hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t*
 // SIMD, 512-register budget), which halves the LDS reads per MFMA.
 constexpr int kMfG = 2;
 constexpr int mf_waves(int g) { return g == 4 ? 4 : 8; }
-constexpr int mf_groups(int d) { return d <= 768 ? 2 : 1; }
+// query groups per wave from the row bytes: the B fragments of a wave's
+// queries take G * rby / 16 VGPRs, <= 192 (bf16 D <= 768 and fp32 D <= 384:
+// G = 2; bf16 D = 1024 / 1536 and fp32 D = 512 / 768: G = 1)
+constexpr int mf_groups_b(int rby) { return rby <= 1536 ? 2 : 1; }
+constexpr int mf_groups(int d) { return mf_groups_b(2 * d); }
 constexpr int kMfListLen = (int)kMfmaListMaxK;                  // entries per query list
 constexpr int kMfListBytes = (int)kMfmaQueries * kMfListLen * 8;  // 32 KiB
 constexpr int kMfRingBytes = 112 * 1024;
@@ -871,8 +931,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // Kernel arguments (one struct, passed by value in the kernarg segment).
 struct MfArgs {
-  const uint16_t* X;        // corpus rows, bf16, row-major, 32 rows of padding
-  const uint16_t* Q;        // kMfmaQueries x D bf16 (zero-padded)
+  const void* X;            // corpus rows (bf16 or fp32), row-major, 32 rows of padding
+  const void* Q;            // kMfmaQueries x D, the collection's dtype (zero-padded)
   const uint64_t* init_th;  // nullable: per-query lower-bound keys at [q * init_stride]
   uint64_t* lists;          // MODE 3 / 8: [nwg][kMfmaQueries][k] sorted keys
   uint64_t* cand;           // MODE 3: [nwg][kMfmaQueries][cand_cap] unsorted keys; MODE 0:
@@ -1007,21 +1067,26 @@ struct MfFull {
   static constexpr bool value = B;
 };
 
-template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8, int CSX = 0>
+// Byte geometry of the streamed rows (EB = element bytes: 2 bf16, 4 fp32).
+// A step is 64 bytes of a row: 32 k of bf16 (one 16x16x32 MFMA per row half
+// and query group) or 16 k of fp32 (four 16x16x4 MFMAs).
+template <int D, int RING = kMfRingBytes, int TAIL = kMfListBytes, int WAVES = 8, int CSX = 0,
+          int EB = 2>
 struct MfShape {
-  static constexpr int T = D / 32;                        // 32-k MFMA steps per row
+  static constexpr int RBY = D * EB;                      // bytes per row
+  static constexpr int T = RBY / 64;                      // 64-B MFMA steps per row
   // 128-B pieces per row per chunk (CSX overrides: ablation of chunk sizes)
-  static constexpr int CS4 = CSX ? CSX : ((D % 256 == 0) ? 4 : 2);
-  static constexpr int CT = CS4 * 2;                      // 32-k steps per chunk
-  static constexpr int CPT = D / (64 * CS4);              // chunks per 32-row tile
+  static constexpr int CS4 = CSX ? CSX : ((RBY % 512 == 0) ? 4 : 2);
+  static constexpr int CT = CS4 * 2;                      // steps per chunk
+  static constexpr int CPT = RBY / (128 * CS4);           // chunks per 32-row tile
   static constexpr int PIECES = CS4 * 4;                  // 1 KiB LDS-DMA pieces per chunk
   static constexpr int PPW = PIECES / WAVES;              // pieces per wave per chunk
   static constexpr int CHUNK_BYTES = PIECES * 1024;       // 32 rows x CS4*128 B
   static constexpr int NSLOT = RING / CHUNK_BYTES;
   static constexpr int AHEAD = NSLOT - 1;                 // chunks in flight
   static constexpr int LDS_BYTES = NSLOT * CHUNK_BYTES + TAIL;  // ring + lists / counters
-  static_assert(D % 256 == 0 || D % 128 == 0, "MFMA scan needs D % 128 == 0");
-  static_assert(D % (64 * CS4) == 0, "whole chunks per tile");
+  static_assert(RBY % 256 == 0, "MFMA scan needs whole 256-B row segments");
+  static_assert(RBY % (128 * CS4) == 0, "whole chunks per tile");
   static_assert(AHEAD >= 2, "at least two chunks in the ring ahead");
   static_assert(PPW >= 1 && PPW * WAVES == PIECES, "pieces split evenly over waves");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -1040,12 +1105,18 @@ struct MfShape {
 // VAR 1024: flips the corpus stream's load policy (MODE 0 default: non-temporal
 // LDS-DMA; other modes: default policy). VAR 131072 (MODE 0): append counters
 // in LDS instead of registers (the r01-v13 form).
-template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D)>
+// F32: fp32 rows and queries on v_mfma_f32_16x16x4_f32 (exact f32 products,
+// fp32 accumulation; 1/16 of the bf16 rate, so the pass is MFMA-bound): same
+// stream, layout and epilogue, a step's 16-B fragment holding 4 k of each
+// lane's k-quarter, consumed by four MFMAs.
+template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D), bool F32 = false>
 __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
   constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
+  constexpr int EB = F32 ? 4 : 2;
+  constexpr int RBY = D * EB;
   static_assert(WAVES * QPW <= (int)kMfmaQueries, "one launch covers <= kMfmaQueries");
-  static_assert(G * (D / 32) * 4 <= (mf_waves(G) == 4 ? 400 : 192),
+  static_assert(G * (RBY / 64) * 4 <= (mf_waves(G) == 4 ? 400 : 192),
                 "B fragments must fit the register budget");
   // VAR 256: a 144 KiB ring (more chunks in flight); LDS lists only in MODE 8
   constexpr bool kBigRing = (VAR & 256) != 0 && MODE != 8;
@@ -1056,7 +1127,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // then drops the A-fragment prefetch of the streaming loop: r01)
   constexpr int kCntBytes = (MODE == 0 || MODE == 3) ? 64 * WAVES * G * 4 : 0;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
-                    MODE == 8 ? kMfListBytes : 16 + kCntBytes, WAVES, kCsx>;
+                    MODE == 8 ? kMfListBytes : 16 + kCntBytes, WAVES, kCsx, EB>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 8;
   constexpr bool kCand = MODE == 0 || MODE == 3;
@@ -1123,7 +1194,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     }
     ql[g] = (uint32_t)(w * QPW + g * 16 + col);
     qvalid[g] = ql[g] < a.nq_valid;
-    const uint4* qrow = (const uint4*)(a.Q + (size_t)ql[g] * D);
+    const uint4* qrow = (const uint4*)((const unsigned char*)a.Q + (size_t)ql[g] * RBY);
 #pragma unroll
     for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
     const uint64_t it = (a.init_th && qvalid[g]) ? a.init_th[(size_t)ql[g] * a.init_stride] : 0;
@@ -1144,10 +1215,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     const int b = w + WAVES * i;
     const int s4l = b >> 2, rg = b & 3;
     const int g_ri = lane >> 3, c16 = (lane & 7) ^ mf_swz(g_ri, rg);
-    loff[i] = (uint32_t)(((rg * 8 + g_ri) * D + s4l * 64 + c16 * 8) * 2);
+    loff[i] = (uint32_t)((rg * 8 + g_ri) * RBY + s4l * 128 + c16 * 16);
   }
   constexpr bool kSpread = (VAR & 512) != 0;  // pieces spread over the chunk's steps
-  const unsigned char* xnext = (const unsigned char*)(a.X + (size_t)wr0 * D);  // next chunk to issue
+  const unsigned char* xnext = (const unsigned char*)a.X + (size_t)wr0 * RBY;  // next chunk to issue
   uint32_t unext = 0;     // its chunk index within the tile
   uint32_t snext = 0;     // its ring slot byte offset
   auto issue_piece = [&](int i) {
@@ -1160,7 +1231,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   };
   auto advance = [&]() {
     const bool last = unext == S::CPT - 1;
-    xnext += last ? (size_t)(32 * D - (S::CPT - 1) * S::CS4 * 64) * 2 : (size_t)S::CS4 * 128;
+    xnext += last ? (size_t)(32 * RBY - (S::CPT - 1) * S::CS4 * 128) : (size_t)S::CS4 * 128;
     unext = last ? 0 : unext + 1;
     snext = snext + S::CHUNK_BYTES == (uint32_t)(S::NSLOT * S::CHUNK_BYTES) ? 0
                                                                            : snext + S::CHUNK_BYTES;
@@ -1268,13 +1339,30 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
                   sp < S::CT ? lds_a(sb, sp, hr) : lds_a(sbn, sp - S::CT, hr);
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+          if constexpr (F32) {
+            // lane (col, kq) holds k = 16 step + 4 kq + j in element j of both
+            // fragments: MFMA j sums those k over the four lane quarters
 #pragma unroll
-          for (int hr = 0; hr < 2; ++hr) {
-            const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][MODE == 10 ? 0 : hr];
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-              acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][u * S::CT + s],
-                                                                   acc[hr][g], 0, 0, 0);
+              for (int hr = 0; hr < 2; ++hr) {
+                const f32x4_t av = __builtin_bit_cast(f32x4_t, afr[sig % NB][hr]);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                  const f32x4_t bv = __builtin_bit_cast(f32x4_t, qf[g][u * S::CT + s]);
+                  acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc[hr][g], 0, 0,
+                                                                    0);
+                }
+              }
+          } else {
+#pragma unroll
+            for (int hr = 0; hr < 2; ++hr) {
+              const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][MODE == 10 ? 0 : hr];
+#pragma unroll
+              for (int g = 0; g < G; ++g)
+                acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][u * S::CT + s],
+                                                                     acc[hr][g], 0, 0, 0);
+            }
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
           if constexpr (kSpread) {
@@ -1485,13 +1573,14 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   }
 }
 
-bool mfma_supported(uint32_t dim) {
+bool mfma_supported(uint32_t dim, bool f32) {
+  if (f32) return dim == 768 || dim == 512 || dim == 384 || dim == 256 || dim == 128;
   return dim == 768 || dim == 512 || dim == 384 || dim == 256 || dim == 128 || dim == 1024 ||
          dim == 1536;
 }
 
-uint32_t mfma_queries(uint32_t dim) {
-  const int g = dim <= 768 ? 2 : 1;
+uint32_t mfma_queries(uint32_t dim, bool f32) {
+  const int g = mf_groups_b((int)dim * (f32 ? 4 : 2));
   return (uint32_t)(mf_waves(g) * 16 * g);
 }
 
@@ -1520,38 +1609,52 @@ uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
   return (rpw + 31) / 32;
 }
 
-template <int MODE, int D>
+template <int MODE, int D, bool F32>
 static void mfma_launch_d(uint32_t nwg, const MfArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mfma_topk_kernel<D, MODE>), dim3(nwg), dim3(64 * mf_waves(mf_groups(D))),
+  constexpr int G = mf_groups_b(D * (F32 ? 4 : 2));
+  hipLaunchKernelGGL((mfma_topk_kernel<D, MODE, 0, G, F32>), dim3(nwg), dim3(64 * mf_waves(G)),
                      0, st, a);
 }
 
 template <int MODE>
-static hipError_t mfma_launch_mode(uint32_t dim, uint32_t nwg, const MfArgs& a, hipStream_t st) {
+static hipError_t mfma_launch_mode(uint32_t dim, bool f32, uint32_t nwg, const MfArgs& a,
+                                   hipStream_t st) {
+  if (f32) {
+    switch (dim) {
+      case 768: mfma_launch_d<MODE, 768, true>(nwg, a, st); break;
+      case 512: mfma_launch_d<MODE, 512, true>(nwg, a, st); break;
+      case 384: mfma_launch_d<MODE, 384, true>(nwg, a, st); break;
+      case 256: mfma_launch_d<MODE, 256, true>(nwg, a, st); break;
+      case 128: mfma_launch_d<MODE, 128, true>(nwg, a, st); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (dim) {
-    case 768: mfma_launch_d<MODE, 768>(nwg, a, st); break;
-    case 512: mfma_launch_d<MODE, 512>(nwg, a, st); break;
-    case 384: mfma_launch_d<MODE, 384>(nwg, a, st); break;
-    case 256: mfma_launch_d<MODE, 256>(nwg, a, st); break;
-    case 128: mfma_launch_d<MODE, 128>(nwg, a, st); break;
-    case 1024: mfma_launch_d<MODE, 1024>(nwg, a, st); break;
-    case 1536: mfma_launch_d<MODE, 1536>(nwg, a, st); break;
+    case 768: mfma_launch_d<MODE, 768, false>(nwg, a, st); break;
+    case 512: mfma_launch_d<MODE, 512, false>(nwg, a, st); break;
+    case 384: mfma_launch_d<MODE, 384, false>(nwg, a, st); break;
+    case 256: mfma_launch_d<MODE, 256, false>(nwg, a, st); break;
+    case 128: mfma_launch_d<MODE, 128, false>(nwg, a, st); break;
+    case 1024: mfma_launch_d<MODE, 1024, false>(nwg, a, st); break;
+    case 1536: mfma_launch_d<MODE, 1536, false>(nwg, a, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-static bool mfma_args_ok(uint32_t dim, uint32_t n_rows, uint32_t nq_valid, uint32_t k) {
-  return mfma_supported(dim) && k >= 1 && k <= kMfmaMaxK && n_rows > 0 && nq_valid >= 1 &&
-         nq_valid <= mfma_queries(dim);
+static bool mfma_args_ok(uint32_t dim, bool f32, uint32_t n_rows, uint32_t nq_valid, uint32_t k) {
+  return mfma_supported(dim, f32) && k >= 1 && k <= kMfmaMaxK && n_rows > 0 && nq_valid >= 1 &&
+         nq_valid <= mfma_queries(dim, f32);
 }
 
-hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
-                              uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
                               uint32_t max_lists, uint32_t* nlists, hipStream_t st,
                               const uint64_t* allow) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || max_tiles == 0 || max_tiles > kMfmaMaxCandCap)
+  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || max_tiles == 0 ||
+      max_tiles > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
@@ -1559,31 +1662,32 @@ hipError_t launch_mfma_sample(const uint16_t* X, uint32_t dim, uint32_t n_rows,
   a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = 4 * max_tiles;
   a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
   a.k = k, a.allow = allow;
-  return mfma_launch_mode<3>(dim, *nlists, a, st);
+  return mfma_launch_mode<3>(dim, f32, *nlists, a, st);
 }
 
-hipError_t launch_mfma_lists(const uint16_t* X, uint32_t dim, uint32_t n_rows,
-                             uint32_t row_base, const uint16_t* Q, uint32_t nq_valid,
+hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
                              const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || k > kMfmaListMaxK) return hipErrorInvalidValue;
+  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || k > kMfmaListMaxK)
+    return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.lists = lists;
   a.run_if = run_if, a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
   a.allow = allow;
-  return mfma_launch_mode<8>(dim, *nlists, a, st);
+  return mfma_launch_mode<8>(dim, f32, *nlists, a, st);
 }
 
-hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, uint32_t row_base,
-                            const uint16_t* Q, uint32_t nq_valid, uint32_t k,
+hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
+                            uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, float* slabs,
                             uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
                             uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow) {
-  if (!mfma_args_ok(dim, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
+  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
@@ -1592,7 +1696,7 @@ hipError_t launch_mfma_cand(const uint16_t* X, uint32_t dim, uint32_t n_rows, ui
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = (uint64_t*)slabs;
   a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
-  return mfma_launch_mode<0>(dim, *nlists, a, st);
+  return mfma_launch_mode<0>(dim, f32, *nlists, a, st);
 }
 
 uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {

@@ -45,7 +45,8 @@ EXPORTS = (
     "vs_read_rows", "vs_search", "vs_search_keys", "vs_merge_keys",
     "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
-    "vs_filter_create", "vs_filter_drop", "vs_search_filter_id",
+    "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
+    "vs_engine_layout",
 )
 
 
@@ -58,6 +59,11 @@ class VSError(RuntimeError):
 
 class _Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class _ConfigMulti(ctypes.Structure):
+    _fields_ = [("devices", ctypes.POINTER(ctypes.c_int32)), ("n_shards", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
 
 
 _lib = None
@@ -76,6 +82,8 @@ def load_library(path: str = LIB_PATH):
     cp = ctypes.c_char_p
     sig = {
         "vs_open": ([ctypes.POINTER(_Config), ctypes.POINTER(vp)], i32),
+        "vs_open_multi": ([ctypes.POINTER(_ConfigMulti), ctypes.POINTER(vp)], i32),
+        "vs_engine_layout": ([vp, vp, vp], i32),
         "vs_close": ([vp], None),
         "vs_device_count": ([], i32),
         "vs_collection_create": ([vp, cp, u32, i32, i32, u64, u64], i32),
@@ -144,18 +152,36 @@ def keys_decode(keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
 
 
 class VectorEngine:
-    """One engine = one HIP device (vs_open). Mirrors the C-ABI 1:1."""
+    """One engine handle (vs_open, or vs_open_multi when `shards` is given).
+    Mirrors the C-ABI 1:1.
+
+    ``shards``: HIP device ordinal of every shard (may repeat), e.g.
+    ``[0, 1, 2, 3, 4, 5, 6, 7]`` for one shard per GPU of a node; collections
+    are then row-striped over the shards and searched with one RCCL
+    all-gather per call (include/vsearch.h "multi-GPU engine")."""
 
     def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False,
-                 timing_sample: bool = False):
+                 timing_sample: bool = False, shards: Optional[Sequence[int]] = None):
         L = load_library()
-        cfg = _Config(device, (FLAG_TIMING if timing else 0) |
-                      (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
-                      (FLAG_TIMING_SAMPLE if timing and timing_sample else 0))
+        flags = ((FLAG_TIMING if timing else 0) |
+                 (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
+                 (FLAG_TIMING_SAMPLE if timing and timing_sample else 0))
         h = ctypes.c_void_p()
-        _check(L.vs_open(ctypes.byref(cfg), ctypes.byref(h)))
+        if shards is None:
+            cfg = _Config(device, flags)
+            _check(L.vs_open(ctypes.byref(cfg), ctypes.byref(h)))
+        else:
+            devs = (ctypes.c_int32 * len(shards))(*[int(x) for x in shards])
+            cfgm = _ConfigMulti(devs, len(shards), flags)
+            _check(L.vs_open_multi(ctypes.byref(cfgm), ctypes.byref(h)))
         self._h = h
         self._L = L
+
+    def layout(self) -> Tuple[int, int]:
+        """(shards, distinct devices) of this engine."""
+        s, d = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(self._L.vs_engine_layout(self._h, ctypes.byref(s), ctypes.byref(d)))
+        return s.value, d.value
 
     def close(self):
         if getattr(self, "_h", None):

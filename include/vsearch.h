@@ -97,6 +97,31 @@ typedef struct vs_config {
 int vs_open(const vs_config* cfg, vs_engine** out);
 void vs_close(vs_engine* eng);
 
+/* ---- multi-GPU engine ------------------------------------
+ * One process drives several devices, one engine handle for all of them
+ * (the reference keeps one client handle per process, main.go:44-65).
+ * Shard s lives on HIP device devices[s] (NULL: device s); a device may
+ * hold several shards. Every collection of such an engine is row-striped:
+ * global row g is stored by shard g % n_shards as its local row
+ * g / n_shards, so appends (upsert, generate) spread evenly. Every entry
+ * point below serves it unchanged: a search scans all shards, merges the
+ * shards of each device on that device, all-gathers one [nq][k] key list per
+ * device over RCCL (one communicator from ncclCommInitAll) and merges them on
+ * the first device, whose stream and memory the device-pointer forms use.
+ * row_base must be 0 (stripes, not blocks). Snapshots of a sharded
+ * collection hold its rows in global order: the file is the same as that of
+ * the collection on one device. n_shards == 1 is vs_open on devices[0]. */
+typedef struct vs_config_multi {
+  const int32_t* devices; /* n_shards HIP ordinals (may repeat); NULL = 0 .. n_shards-1 */
+  uint32_t n_shards;
+  uint32_t flags; /* VS_FLAG_* */
+} vs_config_multi;
+
+int vs_open_multi(const vs_config_multi* cfg, vs_engine** out);
+
+/* Shards and distinct devices of an engine (1 and 1 for vs_open). */
+int vs_engine_layout(vs_engine* eng, uint32_t* n_shards, uint32_t* n_devices);
+
 /* Number of visible HIP devices (0 when none). Never fails. */
 int vs_device_count(void);
 

@@ -1,0 +1,277 @@
+"""Row-sharded collections behind the C-ABI (vs_open_multi).
+
+One engine handle drives every shard; the shards of a device are merged on
+it and the devices' lists are exchanged with one RCCL all-gather
+(ncclCommInitAll). On the one-GPU test box the shards share device 0, so the
+communicator has one rank: the RCCL calls run for real, the xGMI transport
+is the driver's 8-GPU run. Results must equal the oracle on the whole
+collection (global rows), exactly like an unsharded collection's.
+
+C4 (BASELINE.json configs[3]: 100M x 768 bf16, top-100, 8 shards) is checked
+at its full size here: 8 shards on the box's one GPU (153.6 GB of HBM), a
+256-query batch and a single query, against the streaming oracle.
+Reference anchor: Points.Search, rag/vector-service/main.go:249-254; one
+client handle per process, main.go:44-65.
+"""
+import json
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(orc, s, r, c, s64, rr, cc, resc, tol=1e-5):
+    bad = orc.check_topk(s, r, c, s64, rr, cc, resc, score_rtol=tol)
+    assert not bad, bad[:8]
+
+
+@pytest.fixture(scope="module")
+def sharded(pkg):
+    eng = pkg.VectorEngine(shards=[0, 0, 0, 0])
+    yield eng
+    eng.close()
+
+
+def test_layout_and_health(sharded, pkg):
+    assert sharded.layout() == (4, 1)
+    h = json.loads(sharded.health())
+    assert h["status"] == "healthy" and h["shards"] == 4 and len(h["devices"]) == 1
+    with pytest.raises(pkg.VSError):
+        sharded.create_collection("x", 64, 0, 1, 0, 5)  # row_base: stripes, not blocks
+    one = pkg.VectorEngine(shards=[0])
+    try:
+        assert one.layout() == (1, 1)
+    finally:
+        one.close()
+
+
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_sharded_generated_search(sharded, orc, dtype):
+    n, dim = 300_001, 768  # not a multiple of the shard count
+    name = f"sg{dtype}"
+    sharded.create_collection(name, dim, 1, dtype, n)
+    try:
+        sharded.generate(name, n, orc.SEED_CORPUS)
+        assert sharded.collection_info(name)["rows"] == n
+        Q = orc.generate(orc.SEED_QUERY, 0, 256, dim)
+        Qp = orc.preprocess(Q, cosine=False, bf16=bool(dtype))
+        for nq, k in ((256, 10), (1, 10), (40, 100), (3, 1), (17, 16)):
+            s, r, c = sharded.search(name, Q[:nq], k)
+            s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp[:nq], k, bool(dtype))
+            resc = orc.rescore_generated(orc.SEED_CORPUS, Qp[:nq], r, c, bool(dtype))
+            _check(orc, s, r, c, s64, rr, cc, resc)
+        # the stored rows, read back in global order, are the generator's
+        x = sharded.read_rows(name, 99_998, 7)
+        assert np.array_equal(x, orc.generate(orc.SEED_CORPUS, 99_998, 7, dim, bf16=bool(dtype)))
+    finally:
+        sharded.drop_collection(name)
+
+
+def test_sharded_overflow_fallbacks(sharded, orc):
+    """700k identical rows over 4 shards (> 16 tiles per workgroup, so a lane's
+    quarter of a candidate buffer overflows): k <= 16 takes the on-device
+    lists fallback and k > 16 the deferred GEMV re-run (flags read after all
+    shards were enqueued); ties in row order."""
+    dim, n = 128, 700_000
+    base = orc.generate(orc.SEED_CORPUS, 0, 10, dim)
+    sharded.create_collection("sov", dim, 0, 1, n)
+    try:
+        sharded.upsert("sov", np.arange(n), np.tile(base[7:8], (n, 1)))
+        Q = np.concatenate([base[7:8], orc.generate(orc.SEED_QUERY, 11, 7, dim)])
+        for k in (10, 16, 50, 100):
+            s, r, c = sharded.search("sov", Q, k)
+            assert np.all(c == k)
+            assert np.all(r == np.arange(k)[None, :]), k
+        h = json.loads(sharded.health())
+        assert h["mfma_fallbacks"] >= 4
+    finally:
+        sharded.drop_collection("sov")
+
+
+def test_sharded_upsert_equals_single_device(sharded, engine, orc, pkg):
+    dim = 256
+    base = orc.generate(5, 0, 2000, dim) * 2.5
+    for e in (sharded, engine):
+        e.create_collection("su", dim, 0, 1)
+        e.upsert("su", np.arange(1000), base[:1000])
+        e.upsert("su", np.arange(1000, 2000)[::-1], base[1000:][::-1])  # any order
+        e.upsert("su", np.array([7, 1500, 7]), base[[1, 2, 3]])  # overwrite; last wins
+        with pytest.raises(pkg.VSError):
+            e.upsert("su", np.array([2001]), base[:1])  # a hole
+    try:
+        a = sharded.read_rows("su", 0, 2000)
+        b = engine.read_rows("su", 0, 2000)
+        assert np.array_equal(a, b)
+        assert sharded.checksum("su") == engine.checksum("su")
+        Q = orc.generate(orc.SEED_QUERY, 3, 20, dim)
+        X = orc.preprocess(np.concatenate([base[:7], base[3:4], base[8:1500], base[2:3],
+                                           base[1501:]]), True, True)
+        Qp = orc.preprocess(Q, True, True)
+        for k in (5, 50):
+            s, r, c = sharded.search("su", Q, k)
+            s32, s64, rr, cc = orc.search(X, Qp, k)
+            _check(orc, s, r, c, s64, rr, cc, orc.rescore(X, Qp, r, c))
+    finally:
+        sharded.drop_collection("su")
+        engine.drop_collection("su")
+
+
+def test_sharded_filters(sharded, orc, pkg):
+    n, dim = 120_000, 768
+    sharded.create_collection("sf", dim, 0, 1, n)
+    sharded.generate("sf", n, orc.SEED_CORPUS)
+    try:
+        X = orc.generate(orc.SEED_CORPUS, 0, n, dim, bf16=True)
+        Q = orc.generate(orc.SEED_QUERY, 50, 32, dim)
+        Qp = orc.preprocess(Q, True, True)
+        rng = np.random.default_rng(3)
+        for dens in (0.6, 0.05):
+            mask = rng.random(n) < dens
+            idx = np.flatnonzero(mask)
+            fid = sharded.filter_create("sf", mask)
+            for nq, k in ((32, 10), (1, 20)):
+                a = sharded.search_filtered("sf", Q[:nq], k, mask)
+                b = sharded.search_filter_id("sf", Q[:nq], k, fid)
+                assert all(np.array_equal(x, y) for x, y in zip(a, b))
+                s, r, c = a
+                assert np.all(mask[r[c > 0].astype(np.int64)] if r.size else True)
+                s32, s64, rr, cc = orc.search(X[idx], Qp[:nq], k)
+                rr = idx[rr.astype(np.int64)].astype(np.uint64)
+                loc = np.searchsorted(idx, r.astype(np.int64)).astype(np.uint64)
+                _check(orc, s, r, c, s64, rr, cc, orc.rescore(X[idx], Qp[:nq], loc, c))
+            sharded.filter_drop(fid)
+            with pytest.raises(pkg.VSError):
+                sharded.search_filter_id("sf", Q[:1], 10, fid)
+    finally:
+        sharded.drop_collection("sf")
+
+
+def test_sharded_snapshot_portable(sharded, engine, orc, pkg, tmp_path):
+    """A sharded snapshot is the unsharded file: it restores on one device
+    and on another shard count, bit-exact, same answers."""
+    n, dim = 50_003, 128
+    sharded.create_collection("ss", dim, 0, 1)
+    sharded.generate("ss", n, orc.SEED_CORPUS)
+    engine.create_collection("ss1", dim, 0, 1)
+    engine.generate("ss1", n, orc.SEED_CORPUS)
+    try:
+        p = str(tmp_path / "s.vsnap")
+        p1 = str(tmp_path / "s1.vsnap")
+        sharded.snapshot("ss", p)
+        engine.snapshot("ss1", p1)
+        assert open(p, "rb").read() == open(p1, "rb").read()
+        engine.restore("ss2", p)
+        three = pkg.VectorEngine(shards=[0, 0, 0])
+        try:
+            three.restore("ss3", p1)
+            Q = orc.generate(orc.SEED_QUERY, 0, 30, dim)
+            want = engine.search("ss1", Q, 12)
+            for e, nm in ((engine, "ss2"), (three, "ss3"), (sharded, "ss")):
+                got = e.search(nm, Q, 12)
+                assert np.array_equal(got[1], want[1]), nm
+                assert e.checksum(nm) == engine.checksum("ss1")
+        finally:
+            three.close()
+        bad = bytearray(open(p, "rb").read())
+        bad[128 + 999] ^= 1
+        (tmp_path / "bad.vsnap").write_bytes(bytes(bad))
+        with pytest.raises(pkg.VSError) as ei:
+            sharded.restore("ssb", str(tmp_path / "bad.vsnap"))
+        assert ei.value.code == -8
+        with pytest.raises(pkg.VSError):
+            sharded.collection_info("ssb")
+    finally:
+        sharded.drop_collection("ss")
+        engine.drop_collection("ss1")
+        engine.drop_collection("ss2")
+
+
+def test_service_over_sharded_engine(pkg, orc):
+    """The vector-service mirror runs unchanged on a sharded engine."""
+    from importlib import import_module
+    svcmod = import_module(pkg.__name__ + ".service")
+    eng = pkg.VectorEngine(shards=[0, 0, 0])
+    s = svcmod.VectorService(eng)  # the reference's 3 x 768 Cosine fp32 collections
+    try:
+        n = 50
+        X = orc.generate(orc.SEED_CORPUS, 0, n, 768) * 4.0
+        ids = [f"00000000-0000-4000-8000-{i:012x}" for i in range(n)]
+        pts = [{"id": ids[i], "vector": X[i].tolist(), "payload": {"text": f"t{i}"}} for i in range(n)]
+        st, body, _ = s.handle("POST", "/upsert", json.dumps({"collection": "kyc_docs",
+                                                             "points": pts}).encode())
+        assert st == 200, body
+        Xp = orc.preprocess(X, True)
+        for i in (0, 17, 49):
+            st, body, _ = s.handle("POST", "/search", json.dumps(
+                {"collection": "kyc_docs", "query": X[i].tolist(), "top_k": 5}).encode())
+            res = json.loads(body)
+            assert st == 200 and res["count"] == 5 and res["results"][0]["id"] == ids[i]
+            rows = np.array([[ids.index(h["id"]) for h in res["results"]]], np.uint64)
+            sc = np.array([[h["score"] for h in res["results"]]])
+            qp = orc.preprocess(X[i:i + 1], True)
+            s32, s64, rr, cc = orc.search(Xp, qp, 5)
+            _check(orc, sc, rows, np.array([5], np.uint32), s64, rr, cc,
+                   orc.rescore(Xp, qp, rows, np.array([5], np.uint32)))
+        st, body, _ = s.handle("GET", "/health")
+        assert json.loads(body)["status"] == "healthy"
+    finally:
+        s.close()
+        eng.close()
+
+
+_KEYS = r"""
+import sys, json
+sys.path.insert(0, ROOT)
+import numpy as np, torch
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+eng = pkg.VectorEngine(shards=[0, 0])
+n, dim, nq, k = 200_000, 768, 64, 10
+eng.create_collection("dk", dim, 1, 1, n)
+eng.generate("dk", n, orc.SEED_CORPUS)
+st = torch.cuda.Stream()
+with torch.cuda.stream(st):
+    dq = torch.empty((nq, dim), dtype=torch.float32, device="cuda")
+    eng.generate_vectors(orc.SEED_QUERY, 0, nq, dim, dq.data_ptr(), st.cuda_stream)
+    out = torch.zeros((nq, k), dtype=torch.int64, device="cuda")
+    eng.search_keys("dk", dq.data_ptr(), nq, dim, k, out.data_ptr(), st.cuda_stream)
+    s, r, c = eng.decode_keys(out.data_ptr(), nq, k, st.cuda_stream)
+Qp = orc.preprocess(orc.generate(orc.SEED_QUERY, 0, nq, dim), False, True)
+s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp, k, True)
+resc = orc.rescore_generated(orc.SEED_CORPUS, Qp, r, c, True)
+print(json.dumps({"bad": orc.check_topk(s, r, c, s64, rr, cc, resc, 1e-5)[:5]}))
+"""
+
+
+def test_sharded_device_pointer_search():
+    """vs_search_keys on a sharded engine: device queries and keys on the first
+    device, ordered on the caller's (torch) stream."""
+    from test_gpu_parity import _run_py
+    assert _run_py(_KEYS)["bad"] == []
+
+
+@pytest.mark.timeout(1200)
+def test_c4_100m_eight_shards(pkg, orc):
+    """C4 at its shape: 100M x 768 bf16, 8 row shards, top-100, B=256 and B=1,
+    against the streaming oracle (4 + 1 queries)."""
+    n, dim, k = 100_000_000, 768, 100
+    eng = pkg.VectorEngine(shards=[0] * 8)
+    try:
+        eng.create_collection("c4", dim, 1, 1, n)
+        eng.generate("c4", n, orc.SEED_CORPUS)
+        Q = orc.generate(orc.SEED_QUERY, 0, 256, dim)
+        s, r, c = eng.search("c4", Q, k)  # the batched MFMA path on every shard
+        s1, r1, c1 = eng.search("c4", Q[:1], k)  # GEMV on every shard
+        assert np.all(c == k) and np.all(np.diff(s, axis=1) <= 0)
+        Qp = orc.preprocess(Q, cosine=False, bf16=True)
+        resc = orc.rescore_generated(orc.SEED_CORPUS, Qp, r, c, True)
+        assert np.all(np.abs(s - resc) <= 1e-5 * np.abs(resc) + 1e-6)
+        sel = np.array([0, 85, 170, 255])
+        s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp[sel], k, True)
+        _check(orc, s[sel], r[sel], c[sel], s64, rr, cc, resc[sel])
+        resc1 = orc.rescore_generated(orc.SEED_CORPUS, Qp[:1], r1, c1, True)
+        _check(orc, s1, r1, c1, s64[:1], rr[:1], cc[:1], resc1)
+    finally:
+        eng.close()

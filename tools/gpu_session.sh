@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box session helper (run through gpurun). Every GPU step has its own
 # time limit; a step that crashes/hangs stops the script (no retries).
-#   tools/gpu_session.sh [tests] [bench ARGS...] [prof ARGS...]
+#   tools/gpu_session.sh [tests] [testsel TAG FILES.. --] [bench TAG ARGS.. --] [prof TAG ARGS.. --]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
@@ -16,6 +16,12 @@ while [ $# -gt 0 ]; do
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
         > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest_rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; stop_if_bad $rc pytest ;;
+    testsel)  # testsel TAG PYTEST_ARGS... --
+      shift; tag="$1"; shift; args=()
+      while [ $# -gt 0 ] && [ "$1" != "--" ]; do args+=("$1"); shift; done; [ $# -gt 0 ] && shift
+      timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 600 --timeout-method thread \
+        > "gpurun_out/pytest_$tag.log" 2>&1
+      rc=$?; echo "pytest_${tag}_rc=$rc"; tail -3 "gpurun_out/pytest_$tag.log"; stop_if_bad $rc pytest ;;
     smoke)
       shift
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
