@@ -153,12 +153,11 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
                    const SFilter* fid, uint64_t* d_out) {
   const uint32_t S = E->shards(), D = (uint32_t)E->dev.size(), dim = sc.dim;
   const size_t qbytes = (size_t)nq * dim * 4, lbytes = (size_t)nq * k * 8;
-  std::vector<std::vector<vsd::DeferredCheck>> defer(D);
   std::vector<std::vector<std::shared_ptr<vsd::Collection>>> held(D);
   std::vector<std::shared_lock<std::shared_mutex>> rlocks;
   if (h_allow) bits_keep->assign(S, {});
-  // 1. every shard's scan, device by device (asynchronous; a batched pass
-  //    whose overflow check needs the host is deferred, not waited for)
+  // 1. every shard's scan, device by device (all asynchronous: the devices
+  //    scan in parallel)
   for (uint32_t d = 0; d < D; ++d) {
     DevEngine* de = E->dev[d];
     auto& sc_d = E->scr[d];
@@ -189,7 +188,6 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
              "query peer copy");
       q_d = sc_d.q.as<float>();
     }
-    de->ovf_next = 0;
     for (uint32_t j = 0; j < m; ++j) {
       const uint32_t s = E->dev_shards[d][j];
       auto c = vsd::find_coll(de, sc.iname[s].c_str());
@@ -219,29 +217,11 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
         f.list = df->list.p ? df->list.as<uint32_t>() : nullptr;
       }
       uint64_t* keys = sc_d.keys.as<uint64_t>() + (size_t)j * nq * k;
-      const int rc = vsd::search_core(de, *c, q_d, nq, k, keys, f.bits, f.allowed, f.list,
-                                      &defer[d]);
+      const int rc = vsd::search_core(de, *c, q_d, nq, k, keys, f.bits, f.allowed, f.list);
       if (rc != VS_OK) return rc;
     }
   }
-  // 2. deferred overflow checks (k > 16): one flag read per device
-  for (uint32_t d = 0; d < D; ++d) {
-    if (defer[d].empty()) continue;
-    DevEngine* de = E->dev[d];
-    VS_HIP(vsd::set_dev(de), "hipSetDevice");
-    std::vector<uint32_t> flags(de->ovf_next);
-    VS_HIP(hipMemcpyAsync(flags.data(), de->ovf_slots.p, flags.size() * 4,
-                          hipMemcpyDeviceToHost, de->stream),
-           "flags D2H");
-    VS_HIP(hipStreamSynchronize(de->stream), "flags sync");
-    for (const auto& dc : defer[d])
-      if (flags[dc.slot]) {
-        const int rc = vsd::rerun_deferred(de, dc);
-        if (rc != VS_OK) return rc;
-      }
-    de->ovf_next = 0;
-  }
-  // 3. local rows -> global rows; the shards of a device merged on it
+  // 2. local rows -> global rows; the shards of a device merged on it
   std::vector<const uint64_t*> send(D);
   for (uint32_t d = 0; d < D; ++d) {
     DevEngine* de = E->dev[d];
@@ -261,7 +241,7 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
       send[d] = sc_d.keys.as<uint64_t>();
     }
   }
-  // 4. one all-gather of the devices' lists over RCCL, merged on dev 0
+  // 3. one all-gather of the devices' lists over RCCL, merged on dev 0
   ncclResult_t r = ncclGroupStart();
   if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
   for (uint32_t d = 0; d < D; ++d) {
@@ -937,10 +917,9 @@ int vs_restore(vs_engine* eng, const char* coll, const char* path) {
 int vs_health(vs_engine* eng, char* buf, size_t len) {
   if (!eng || !buf || len == 0) return fail(VS_ERR_INVALID_ARG, "bad health buffer");
   if (!eng->sharded) return vsd::health(eng->dev[0], buf, len);
-  // {"status","engine","shards","device_name","collections","mfma_fallbacks","devices":[...]}
+  // {"status","engine","shards","device_name","collections","devices":[...]}
   std::string devs;
   bool healthy = true;
-  uint64_t fallbacks = 0;
   std::string name0;
   for (size_t d = 0; d < eng->dev.size(); ++d) {
     char one[1024];
@@ -948,8 +927,6 @@ int vs_health(vs_engine* eng, char* buf, size_t len) {
     healthy = healthy && rc == VS_OK;
     if (d) devs.push_back(',');
     devs.append(one);
-    const char* fb = std::strstr(one, "\"mfma_fallbacks\":");
-    if (fb) fallbacks += std::strtoull(fb + 17, nullptr, 10);
     if (d == 0) {
       const char* dn = std::strstr(one, "\"device_name\":\"");
       if (dn) {
@@ -966,10 +943,10 @@ int vs_health(vs_engine* eng, char* buf, size_t len) {
   }
   const int n = std::snprintf(buf, len,
                               "{\"status\":\"%s\",\"engine\":\"vsearch-hip\",\"shards\":%u,"
-                              "\"device_name\":\"%s\",\"collections\":%zu,\"mfma_fallbacks\":%llu,"
+                              "\"device_name\":\"%s\",\"collections\":%zu,"
                               "\"devices\":[%s]}",
                               healthy ? "healthy" : "degraded", eng->shards(), name0.c_str(), ncoll,
-                              (unsigned long long)fallbacks, devs.c_str());
+                              devs.c_str());
   if (n < 0 || (size_t)n >= len) return fail(VS_ERR_INVALID_ARG, "health buffer too small");
   return healthy ? VS_OK : fail(VS_ERR_DEVICE, "a device is degraded");
 }

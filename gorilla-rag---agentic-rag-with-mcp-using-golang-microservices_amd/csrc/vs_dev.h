@@ -92,9 +92,8 @@ struct DevEngine {
   std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
-  DevBuf cand, cand_cnt, overflow;  // MFMA main pass candidates (vs_kernels.h)
+  DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
   DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
-  DevBuf fallbacks;                 // u32: MFMA passes re-run by the overflow fallback
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
   DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch
@@ -107,9 +106,6 @@ struct DevEngine {
   };
   std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
   uint64_t next_filter = 1;
-  uint32_t host_fallbacks = 0;      // ... of which GEMV re-runs (k > 16)
-  DevBuf ovf_slots;                 // u32 flag words of deferred passes (DeferredCheck)
-  uint32_t ovf_next = 0;            // next free slot of the current multi-shard call
   std::vector<uint64_t> h_keys;
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
@@ -118,18 +114,6 @@ struct DevEngine {
   uint64_t scan_n = 0, merge_n = 0;
   uint64_t scan_tick = 0;   // scan launches seen (VS_FLAG_TIMING_SAMPLE)
   bool scan_skip = false;   // the current scan launch is not bracketed
-};
-
-// A batched pass whose overflow flag is read after every shard's scans were
-// enqueued (k > kMfmaListMaxK; multi-shard searches): a set flag re-runs the
-// pass's queries on the GEMV path before the keys are consumed.
-struct DeferredCheck {
-  Collection* coll;
-  float* qp;        // preprocessed fp32 queries of the call (device)
-  uint32_t q0, nv;  // the pass's queries
-  uint32_t k;
-  uint64_t* out;    // its keys [nv][k]
-  uint32_t slot;    // flag word in DevEngine::ovf_slots
 };
 
 // ---- per-device operations (vs_engine.cpp); same contracts as the C-ABI
@@ -182,13 +166,10 @@ uint64_t popcount_rows(const uint64_t* allow, uint64_t rows);
 
 // Search of device queries d_q (nq x dim fp32 on this device, ordered on
 // eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and
-// the collection's reader lock held by the caller. With `defer`, a batched
-// pass's overflow check is appended there instead of synchronising.
+// the collection's reader lock held by the caller. Asynchronous: nothing
+// waits on the device unless a scratch buffer has to grow.
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
-                const uint32_t* allow_list = nullptr,
-                std::vector<DeferredCheck>* defer = nullptr);
-// GEMV re-run of a deferred pass whose flag was set (work_mu held).
-int rerun_deferred(DevEngine* eng, const DeferredCheck& d);
+                const uint32_t* allow_list = nullptr);
 
 }  // namespace vsd

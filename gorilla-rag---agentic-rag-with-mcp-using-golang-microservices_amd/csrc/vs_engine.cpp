@@ -242,16 +242,17 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
   return VS_OK;
 }
 
-// Batched bf16 scan on MFMA, 256 queries per pass:
+// Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
+// queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
 //  1. sample pass over 1/64 of every workgroup's tiles -> top-k of the tile
 //     maxima -> per-query lower bound on the global k-th key;
-//  2. main pass: rows reaching the bound -> candidate buffers -> select;
-//  3. if a candidate buffer overflowed (adversarial ties): redo the pass
-//     exactly -- the sorted-list pass + merge for k <= 16 (device-side, no
-//     host sync: both launches are no-ops unless the flag is set), the GEMV
-//     path for larger k (after a host check of the flag).
+//  2. main pass: rows reaching the bound -> candidate buffers -> select. A
+//     full buffer quarter keeps its best slabs (exact, vs_kernels.h), so no
+//     pass is ever re-run and nothing here waits on the device.
+// Small collections (fewer than 8 tiles per workgroup) take the sorted-list
+// pass (k <= 16) or the GEMV path.
 int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow, std::vector<DeferredCheck>* defer) {
+                uint64_t* d_keys, const uint64_t* allow) {
   const uint32_t dim = c.dim;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
@@ -261,22 +262,20 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t npass = (nq + P - 1) / P;
   const uint32_t maxl = vsk::mfma_max_lists(n_rows);
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
-  // the candidate pass needs the sample bound from a few tiles per workgroup;
-  // small collections take the sorted-list pass (k <= 16) or the GEMV path
   const bool fast = tpw >= 8;
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
-  const size_t lbytes = (size_t)maxl * PS * std::min(k, vsk::kMfmaListMaxK) * 8;
+  const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * k * 8;
-  // main pass slabs: 32 B of scores + a 4-B tile row per slot
-  const size_t sl_bytes = (size_t)maxl * PS * cap * 32;
-  const size_t cbytes = sl_bytes + (size_t)maxl * PS * cap * 4;
+  // main pass slabs: 32 B of scores + a 4-B tile row + a 4-B maximum per slot
+  const size_t slots = (size_t)maxl * PS * cap;
+  const size_t cbytes = slots * 40;
   const size_t scbytes = (size_t)maxl * PS * 4 * st * 8;
   const size_t nbytes = (size_t)maxl * PS * 4 * 4;
   if (eng->lists.bytes < lbytes || eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
       eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes ||
-      eng->scand_cnt.bytes < nbytes || eng->overflow.bytes < 4 || eng->fallbacks.bytes < 4) {
+      eng->scand_cnt.bytes < nbytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
     VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
@@ -284,43 +283,13 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     VS_HIP(eng->scand.ensure(scbytes), "alloc sample candidate scratch");
     VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
     VS_HIP(eng->scand_cnt.ensure(nbytes), "alloc sample candidate counts");
-    if (eng->overflow.bytes < 4) {
-      VS_HIP(eng->overflow.ensure(4), "alloc overflow flag");
-      VS_HIP(hipMemsetAsync(eng->overflow.p, 0, 4, eng->stream), "clear overflow flag");
-    }
-    if (eng->fallbacks.bytes < 4) {
-      VS_HIP(eng->fallbacks.ensure(4), "alloc fallback counter");
-      VS_HIP(hipMemsetAsync(eng->fallbacks.p, 0, 4, eng->stream), "clear fallback counter");
-    }
   }
   const void* X = c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
-  const bool dev_fb = k <= vsk::kMfmaListMaxK;
-  // a deferred pass gets a flag word of its own (its sample select clears
-  // it, its main pass sets it), read by the caller after every shard's
-  // scans were enqueued; the next deferred slots of this call follow
-  if (!dev_fb && defer) {
-    const size_t want = (eng->ovf_next + npass) * 4;
-    if (eng->ovf_slots.bytes < want) {
-      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-      DevBuf grown;
-      VS_HIP(grown.ensure(std::max(want * 2, (size_t)1024)), "alloc flag slots");
-      if (eng->ovf_slots.p && eng->ovf_next)
-        VS_HIP(hipMemcpyAsync(grown.p, eng->ovf_slots.p, eng->ovf_next * 4,
-                              hipMemcpyDeviceToDevice, eng->stream),
-               "flag slots copy");
-      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-      std::swap(grown.p, eng->ovf_slots.p);
-      std::swap(grown.bytes, eng->ovf_slots.bytes);
-    }
-  }
+  float* slabs = eng->cand.as<float>();
+  uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + slots * 32);
+  float* slab_max = (float*)((char*)eng->cand.p + slots * 36);
   for (uint32_t p = 0; p < npass; ++p) {
-    uint32_t slot = 0;
-    uint32_t* ovf = eng->overflow.as<uint32_t>();
-    if (!dev_fb && defer) {
-      slot = eng->ovf_next++;
-      ovf = eng->ovf_slots.as<uint32_t>() + slot;
-    }
     const uint32_t q0 = p * P;
     const uint32_t nv = std::min(P, nq - q0);
     uint64_t* out = d_keys + (size_t)q0 * k;
@@ -331,8 +300,8 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     uint32_t L = 0;
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, nullptr, 0, nullptr,
-                                    lists, maxl, &L, eng->stream, allow),
+      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, nullptr, 0, lists,
+                                    maxl, &L, eng->stream, allow),
              "mfma scan (lists)");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -348,45 +317,21 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                    &L, eng->stream, allow),
            "mfma sample scan");
     VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, 4 * st,
-                              nv, k, skeys, eng->stream, ovf),
-           "sample select (clears the overflow flag)");
+                              nv, k, skeys, eng->stream),
+           "sample select");
     const uint64_t* init = skeys + (k - 1);
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-    float* slabs = eng->cand.as<float>();
-    uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + sl_bytes);
-    VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, slabs, slab_tile,
-                                 cap, eng->cand_cnt.as<uint32_t>(), ovf, maxl, &L, eng->stream,
-                                 allow),
+    VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, slabs,
+                                 slab_tile, slab_max, cap, eng->cand_cnt.as<uint32_t>(), maxl,
+                                 &L, eng->stream, allow),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
-    // 3. overflow fallback, k <= 16: the sorted-list pass (a no-op launch
-    // unless the main pass set the flag), whose lists the select then merges
-    // in place of the slabs
-    uint32_t Lf = 0;
-    if (dev_fb)
-      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, ovf, lists,
-                                    maxl, &Lf, eng->stream, allow),
-             "mfma scan (fallback)");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
     VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                                    k, out, eng->stream, row_base, allow,
-                                    dev_fb ? ovf : nullptr, lists, Lf, (uint64_t)PS * k,
-                                    eng->fallbacks.as<uint32_t>()),
+                                    k, out, eng->stream, row_base, allow),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
-    if (!dev_fb && defer) {
-      defer->push_back(DeferredCheck{&c, qp, q0, nv, k, out, slot});
-    } else if (!dev_fb) {
-      uint32_t h_ovf = 0;
-      VS_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, eng->stream), "flag D2H");
-      VS_HIP(hipStreamSynchronize(eng->stream), "flag sync");
-      if (h_ovf) {
-        int rc = search_gemv(eng, c, qp, q0, nv, k, out, allow);
-        if (rc != VS_OK) return rc;
-        eng->host_fallbacks++;
-      }
-    }
   }
   return VS_OK;
 }
@@ -396,7 +341,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // reader lock are held by the caller.
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow, uint64_t allowed,
-                const uint32_t* allow_list, std::vector<DeferredCheck>* defer) {
+                const uint32_t* allow_list) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -447,12 +392,13 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     qb = eng->q_bf16.as<uint16_t>();
   }
   // the fp32 copy feeds the GEMV path and the fp32 MFMA path; the bf16 MFMA
-  // path needs it just for its k > 16 fallback
-  const bool need_qp = !use_mfma || !bf16 || k > vsk::kMfmaListMaxK;
+  // path needs it only where small collections send k > 16 to the GEMV path
+  const bool need_qp = !use_mfma || !bf16 ||
+                       (k > vsk::kMfmaListMaxK && vsk::mfma_tiles_per_wg((uint32_t)c.rows) < 8);
   VS_HIP(vsk::launch_query_prep(d_q, nq, dim, cosine, bf16, need_qp ? qp : nullptr, qb,
                                 eng->stream),
          "query preprocess");
-  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow, defer);
+  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
   if (gather) {
     if (allowed == 0) {
       VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
@@ -473,12 +419,6 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     return search_gemv(eng, c, qp, 0, nq, k, d_keys, nullptr, allow_list, (uint32_t)allowed);
   }
   return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
-}
-
-int rerun_deferred(DevEngine* eng, const DeferredCheck& d) {
-  const int rc = search_gemv(eng, *d.coll, d.qp, d.q0, d.nv, d.k, d.out);
-  if (rc == VS_OK) eng->host_fallbacks++;
-  return rc;
 }
 
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
@@ -1178,25 +1118,12 @@ int health(DevEngine* eng, char* buf, size_t len) {
     std::lock_guard<std::mutex> g(eng->map_mu);
     ncoll = eng->colls.size();
   }
-  uint32_t fallbacks = 0;
-  if (e == hipSuccess) {
-    std::lock_guard<std::mutex> g(eng->work_mu);
-    if (eng->fallbacks.bytes >= 4) {
-      e = hipMemcpyAsync(&fallbacks, eng->fallbacks.p, 4, hipMemcpyDeviceToHost, eng->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(eng->stream);
-    }
-    fallbacks += eng->host_fallbacks;
-    if (e != hipSuccess) {
-      status = "degraded";
-      err = hipGetErrorString(e);
-    }
-  }
   int n = std::snprintf(buf, len,
                         "{\"status\":\"%s\",\"engine\":\"vsearch-hip\",\"device\":%d,"
                         "\"device_name\":\"%s\",\"hbm_free_bytes\":%zu,\"hbm_total_bytes\":%zu,"
-                        "\"collections\":%zu,\"mfma_fallbacks\":%u%s%s%s}",
+                        "\"collections\":%zu%s%s%s}",
                         status.c_str(), eng->device, eng->device_name.c_str(), freeb, totalb,
-                        ncoll, fallbacks, err.empty() ? "" : ",\"error\":\"", err.c_str(),
+                        ncoll, err.empty() ? "" : ",\"error\":\"", err.c_str(),
                         err.empty() ? "" : "\"");
   if (n < 0 || (size_t)n >= len) return fail(VS_ERR_INVALID_ARG, "health buffer too small");
   return e == hipSuccess ? VS_OK : fail(VS_ERR_DEVICE, err);

@@ -77,15 +77,16 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //  * main pass: every row; a lane whose 8 scores of a tile reach the
 //    per-query lower bound init_th[q * init_stride] appends them as one slab
 //    (8 f32, the accumulator layout) and the tile's first global row to the
-//    query's buffer: slabs[nlists][kMfmaQueries][cap][8] and
-//    slab_tile[nlists][kMfmaQueries][cap] (cap % 4 == 0: quarter j of a
-//    buffer is lane j's, counts in slabs cand_cnt[nlists][256][4]);
+//    query's buffer: slabs[nlists][kMfmaQueries][cap][8],
+//    slab_tile[nlists][kMfmaQueries][cap] and each slab's masked maximum
+//    slab_max[..][cap] (cap % 4 == 0, cap >= 4 k: quarter j of a buffer is
+//    lane j's, counts in slabs cand_cnt[nlists][256][4]); a full quarter
+//    keeps its cap / 4 best slabs (exact for k <= cap / 4, never overflows);
 //    launch_select_slabs picks the top k;
-//    sets *overflow = 1 when a quarter would overflow (the caller then
-//    redoes the batch exactly: lists pass or GEMV);
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
-//    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; a no-op
-//    unless run_if is null or *run_if != 0.
+//    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; collections
+//    of fewer than 8 tiles per workgroup, where the sample bound has too
+//    few tiles to be worth a pass.
 // `allow` (nullable, all passes): filter pre-mask, bit r of allow[r / 64]
 // admits local row r; masked rows are never candidates, maxima or results.
 bool mfma_supported(uint32_t dim, bool f32);
@@ -98,35 +99,26 @@ hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, float* slabs,
-                            uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
-                            uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
+                            uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
+                            uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow = nullptr);
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
-                             const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
+                             uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
 // Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap] (4
 // quarters, counts cand_cnt[nwg][kMfmaQueries][4]) for queries 0 .. nq-1 ->
 // out[nq][k], sorted, 0-padded.
-// *clear (nullable) is zeroed by the launch (the main pass's overflow flag,
-// folded in to save a launch).
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
-                         uint32_t* clear = nullptr);
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st);
 // The same over the main pass's slab buffers (see launch_mfma_cand); the
 // main pass leaves masked rows in its slabs, so the select applies the same
 // pre-mask `allow` (local rows = global - row_base).
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,
-                               const uint64_t* allow = nullptr,
-                               // overflow fallback (k <= kMfmaListMaxK): when *fb_flag is
-                               // set, merge the lists pass's [fb_L][kMfmaQueries][k] lists
-                               // (list stride fb_lstride keys) instead; fb_ran counts it
-                               const uint32_t* fb_flag = nullptr,
-                               const uint64_t* fb_lists = nullptr, uint32_t fb_L = 0,
-                               uint64_t fb_lstride = 0, uint32_t* fb_ran = nullptr);
+                               const uint64_t* allow = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows);
@@ -137,12 +129,9 @@ void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);
 
 // Merge L sorted key lists per query -> out [nq][k] (global top-k by key).
 // List l of query q starts at lists[l * lstride + q * qstride], kin entries.
-// A no-op unless run_if is null or *run_if != 0; when it runs, *ran (if
-// non-null) is incremented once.
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k,
-                        uint64_t* out, hipStream_t st, const uint32_t* run_if = nullptr,
-                        uint32_t* ran = nullptr);
+                        uint64_t* out, hipStream_t st);
 
 // Convert fp32 queries (nq x dim) to bf16 (after preprocessing).
 hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out,

@@ -901,10 +901,9 @@ hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t*
 // in global memory (slot from an LDS counter, fire-and-forget stores), and
 // select_cand_kernel picks the top k of all workgroups' candidates. No wave
 // ever waits on a list in the loop, so no stall reaches the other seven
-// waves through the per-chunk barrier. A buffer that would overflow sets
-// *overflow instead; the engine then re-runs the batch with MODE 8 (same
-// scan, per-query sorted lists in LDS maintained by mf_insert), whose launch
-// and merge are no-ops unless that flag is set.
+// waves through the per-chunk barrier. A full buffer quarter (many
+// near-equal rows) keeps its best slabs in place (mf_replace_min): exact,
+// so no batch is ever re-run and the host never waits on the device.
 //
 // Sample pass (MODE 3): the same scan over the first 1/64 of every
 // workgroup's tiles, keeping per query the top k of the TILE MAXIMA (mf_insert
@@ -939,9 +938,8 @@ struct MfArgs {
                             // [nwg][kMfmaQueries][cand_cap] slabs of 8 f32 scores (32 B);
                             // quarter kq of a query's buffer belongs to its lane kq
   uint32_t* cand_tile;      // MODE 0: first global row of each slab's tile
+  float* cand_max;          // MODE 0: each slab's (masked) maximum score
   uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys / slabs per quarter
-  uint32_t* overflow;       // MODE 0: set to 1 when a buffer would overflow
-  const uint32_t* run_if;   // nullable: the launch does nothing unless *run_if != 0
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
   const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
@@ -1062,6 +1060,46 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
   }
 }
 
+// A full quarter of a main-pass candidate buffer (slots [base, base + sub),
+// their masked maximum scores in cand_max): the new slab (scores v0, v1 of
+// global tile row tile, masked maximum mx) replaces the slot whose maximum is
+// smallest -- among equal maxima the latest tile (highest rows) -- if mx is
+// larger. Exact for k <= sub: every slab dropped this way (or never stored)
+// is beaten by sub >= k keys of distinct rows, one per slot kept (a larger
+// score, or an equal score of an earlier, lower-row tile of this
+// workgroup's ascending scan). Rare path; reads back this lane's own stores.
+template <typename Args>
+__device__ __forceinline__ void mf_replace_min(const Args& a, uint32_t base, uint32_t sub,
+                                               f32x4_t v0, f32x4_t v1, uint32_t tile, float mx) {
+  // opaque: no address built from it is hoisted out of this rare path into
+  // the tile loop (whose registers are all taken)
+  asm volatile("" : "+v"(base));
+  float msel = INFINITY;
+  uint32_t tsel = 0, jsel = 0;
+  for (uint32_t j = 0; j < sub; ++j) {
+    const float m = a.cand_max[base + j];
+    const uint32_t t = a.cand_tile[base + j];
+    // selects, not branches: both loads are consumed on every path
+    const bool lt = m < msel || (m == msel && t > tsel);
+    msel = lt ? m : msel;
+    tsel = lt ? t : tsel;
+    jsel = lt ? j : jsel;
+  }
+  if (mx > msel) {
+    const size_t e = base + jsel;
+    f32x4_t* sl = (f32x4_t*)a.cand + 2 * e;
+    sl[0] = v0;
+    sl[1] = v1;
+    a.cand_tile[e] = tile;
+    a.cand_max[e] = mx;
+  }
+  // Leave no load of this path outstanding: the compiler's wait analysis
+  // merges this path into the tile loop, and a pending load here became an
+  // unconditional vmcnt(0) in the loop, draining the DMA ring every chunk
+  // (+17% main pass, r02). vmcnt(0), expcnt / lgkmcnt untouched.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+
 template <bool B>
 struct MfFull {
   static constexpr bool value = B;
@@ -1138,7 +1176,6 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // prefetch survives scheduling (3.38 vs 3.63 ms at 10M rows); the sorted-list
   // pass would spill with it
   constexpr bool kPin = (VAR & 128) != 0 || MODE != 8;
-  if (a.run_if && *a.run_if == 0) return;  // fallback launch with nothing to redo
   // VAR 8192 (ablation): per-workgroup start / end wall clock into a.lists
   constexpr bool kClock = (VAR & 8192) != 0;
   uint64_t tclk0 = 0;
@@ -1241,6 +1278,34 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     for (int i = 0; i < PPW; ++i) issue_piece(i);
     advance();
   };
+  // Branch-free stream (default of the product passes, MODE 0 / 3 / 8; VAR
+  // 524288 flips it: back to the conditional stream, or on for ablation
+  // modes; r02: main pass -2.5 to -3.2% at 10M / 1.25M rows, back to back).
+  // Every chunk step issues its pieces: past
+  // the last chunk they re-read the workgroup's first chunk (valid memory, an
+  // L2 hit) into the slot being refilled, which is never read again; so the
+  // vmcnt waits are the same every step (no branches in the chunk loop, which
+  // let hipcc's waitcnt pass keep the fragment reads' order: lgkmcnt(2), not
+  // lgkmcnt(0), before a chunk's first MFMAs). Drained before the exit.
+  constexpr bool kBF = (((VAR & 524288) != 0) != (MODE == 0 || MODE == 3 || MODE == 8)) && !kSpread;
+  const unsigned char* const xsafe = (const unsigned char*)a.X + (size_t)wr0 * RBY;
+  auto issue_next_bf = [&](bool real) {
+    // wave-uniform by construction; readfirstlane keeps it in SGPRs for the
+    // asm's "s" operand whatever the divergence analysis concludes
+    const uint64_t sp = (uint64_t)(uintptr_t)(real ? xnext : xsafe);
+    const unsigned char* src = (const unsigned char*)(uintptr_t)(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sp >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp));
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int b = w + WAVES * i;
+      const int s4l = b >> 2, rg = b & 3;
+      glds16<kNtDma>(src, loff[i],
+                     (uint32_t)__builtin_amdgcn_readfirstlane(
+                         (int)(lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024))));
+    }
+    advance();
+  };
 
   // A operand read offsets: half hr (tile rows 16hr..16hr+15), lane reads row
   // 16hr + col, 16-B chunk 4*(t&1) + kq of piece t>>1.
@@ -1266,14 +1331,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     return;
   }
   __syncthreads();  // lists / counts initialised
-  if constexpr (kDma)
-    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
-      if (c < nchunks) issue_next();
-  // publish chunk 0
-  if ((uint32_t)S::AHEAD <= nchunks)
+  if constexpr (kDma && kBF) {
+#pragma unroll
+    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
     wait_vmcnt<PPW * (S::AHEAD - 1)>();
-  else
-    wait_vmcnt<0>();
+  } else {
+    if constexpr (kDma)
+      for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
+        if (c < nchunks) issue_next();
+    // publish chunk 0
+    if ((uint32_t)S::AHEAD <= nchunks)
+      wait_vmcnt<PPW * (S::AHEAD - 1)>();
+    else
+      wait_vmcnt<0>();
+  }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
@@ -1294,7 +1365,18 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // The sorted-list pass keeps one body with a runtime test (its register
   // allocation with the peeled form spilled; r01).
   constexpr bool kPeel = MODE != 8;
-  auto tile = [&](uint32_t t, auto full_tag) {
+  // VAR 1048576 (with the branch-free stream): waves 4-7 run half a chunk
+  // ahead of their SIMD partners 0-3. Their per-chunk wait + barrier + DMA
+  // issue sits between steps CT/2 - 1 and CT/2 of the chunk instead of before
+  // step 0 (same barrier count, same slots: a wave only reads chunks the
+  // barrier before its steps published, and the slot refilled at barrier c,
+  // chunk c - 1's, is done for every wave), so the two waves of a SIMD reach
+  // their LDS-read bursts and barriers half a chunk apart instead of in
+  // lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9).
+  constexpr bool kStag = (VAR & 1048576) != 0 && kBF && WAVES == 8;
+  auto tile = [&](uint32_t t, auto full_tag, auto stag_tag) {
+    constexpr bool STAG = decltype(stag_tag)::value;
+    constexpr int SYNC_STEP = STAG ? S::CT / 2 : 0;
     f32x4_t acc[2][G];  // [row half][query group]
 #pragma unroll
     for (int hr = 0; hr < 2; ++hr)
@@ -1314,21 +1396,32 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
           for (int hr = 0; hr < (MODE == 10 ? 1 : 2); ++hr) afr[p][hr] = lds_a(sb, p, hr);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
-      if constexpr (kDma) {
-        if (c + S::AHEAD <= nchunks)
-          wait_vmcnt<PPW * (S::AHEAD - 2)>();
-        else
-          wait_vmcnt<0>();
-      }
-      if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
-      __builtin_amdgcn_sched_barrier(0);
       const bool refill = kDma && c + S::AHEAD < nchunks;
-      if (!kSpread && refill) issue_next();
+      auto sync_chunk = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
+        if constexpr (kDma && kBF) {
+          wait_vmcnt<PPW * (S::AHEAD - 2)>();
+        } else if constexpr (kDma) {
+          if (c + S::AHEAD <= nchunks)
+            wait_vmcnt<PPW * (S::AHEAD - 2)>();
+          else
+            wait_vmcnt<0>();
+        }
+        if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kDma && kBF)
+          issue_next_bf(refill);
+        else if (!kSpread && refill)
+          issue_next();
+      };
+      if constexpr (!STAG || MODE == 2) sync_chunk();
       if constexpr (MODE != 2) {
 #pragma unroll
         for (int s = 0; s < S::CT; ++s) {
+          if constexpr (STAG) {
+            if (s == SYNC_STEP) sync_chunk();
+          }
           const int sig = u * S::CT + s;
           // prefetch step sig + PD (this chunk or the next one)
           if (MODE != 7 && sig + kPD < STEPS) {
@@ -1449,7 +1542,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           const uint32_t sub = a.cand_cap >> 2;
           const uint32_t cg = kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
           if (cg >= sub) {
-            *a.overflow = 1u;  // the caller re-runs the batch exactly
+            // VAR 131072 (LDS counters, ablation only) drops the slab: inexact
+            // The quarter is full (many near-equal rows): keep the sub slabs
+            // with the largest maximum keys. A slab this evicts (or never
+            // stores) has a maximum key below those of all sub slabs kept,
+            // i.e. below sub >= k keys of distinct rows, so none of its rows
+            // can be in the top k (mfma_cand_cap gives sub >= k): exact, with
+            // no re-run. Rare path: the slabs are read back from memory.
+            // VAR 2097152 (ablation): drops the slab, inexact
+            if constexpr (kRegCnt && (VAR & 2097152) == 0)
+              mf_replace_min(a, slot0[g], sub, acc[0][g], acc[1][g], a.row_base + trow0, mx);
           } else if constexpr (kRegCnt) {
             // VAR 262144 (ablation): the appending wave runs at raised
             // priority, so it reaches the next chunk barrier sooner
@@ -1459,6 +1561,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             sp[0] = acc[0][g];
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
+            if constexpr ((VAR & 4194304) == 0) a.cand_max[slot] = mx;
             cnt_r[g] = cg + 1;
             if constexpr ((VAR & 262144) != 0) __builtin_amdgcn_s_setprio(0);
           } else {
@@ -1516,11 +1619,9 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           const uint32_t sub = a.cand_cap >> 2;
           const uint32_t cg = n ? cntl[g * THREADS + threadIdx.x] : 0u;
           if (n) {
-            if (cg + n > sub) {
-              // main pass: the caller re-runs the batch exactly; sample pass:
-              // dropping tile maxima only lowers the bound (still valid)
-              if constexpr (MODE == 0) *a.overflow = 1u;
-            } else {
+            // a full quarter drops tile maxima: that only lowers the sample
+            // bound, which stays valid
+            if (cg + n <= sub) {
               // the address is rebuilt here from an opaque thread id, so none
               // of it is hoisted out of the tile loop (its register budget)
               uint32_t tid = threadIdx.x;
@@ -1544,12 +1645,23 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   };
   uint32_t nfull = (wr1 - wr0) / 32;
   if (nfull > ntiles) nfull = ntiles;
-  if constexpr (kPeel) {
-    for (uint32_t t = 0; t < nfull; ++t) tile(t, MfFull<true>{});
-    for (uint32_t t = nfull; t < ntiles; ++t) tile(t, MfFull<false>{});
+  auto run_tiles = [&](auto stag_tag) {
+    if constexpr (kPeel) {
+      for (uint32_t t = 0; t < nfull; ++t) tile(t, MfFull<true>{}, stag_tag);
+      for (uint32_t t = nfull; t < ntiles; ++t) tile(t, MfFull<false>{}, stag_tag);
+    } else {
+      for (uint32_t t = 0; t < ntiles; ++t) tile(t, MfFull<false>{}, stag_tag);
+    }
+  };
+  if constexpr (kStag) {
+    if (w >= 4)
+      run_tiles(MfFull<true>{});
+    else
+      run_tiles(MfFull<false>{});
   } else {
-    for (uint32_t t = 0; t < ntiles; ++t) tile(t, MfFull<false>{});
+    run_tiles(MfFull<false>{});
   }
+  if constexpr (kDma && kBF) wait_vmcnt<0>();  // no LDS-DMA outlives the workgroup
   if constexpr (kClock)
     if (threadIdx.x == 0) {
       a.lists[2 * blockIdx.x] = tclk0;
@@ -1668,7 +1780,7 @@ hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const uint64_t* init_th, uint32_t init_stride,
-                             const uint32_t* run_if, uint64_t* lists, uint32_t max_lists,
+                             uint64_t* lists, uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || k > kMfmaListMaxK)
     return hipErrorInvalidValue;
@@ -1676,7 +1788,7 @@ hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_r
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.lists = lists;
-  a.run_if = run_if, a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
+  a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
   a.allow = allow;
   return mfma_launch_mode<8>(dim, f32, *nlists, a, st);
 }
@@ -1684,17 +1796,18 @@ hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_r
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const uint64_t* init_th, uint32_t init_stride, float* slabs,
-                            uint32_t* slab_tile, uint32_t cand_cap, uint32_t* cand_cnt,
-                            uint32_t* overflow, uint32_t max_lists, uint32_t* nlists,
+                            uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
+                            uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow) {
-  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 || cand_cap % 4 ||
+  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 * k || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = (uint64_t*)slabs;
-  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.overflow = overflow, a.n_rows = n_rows, a.row_base = row_base;
+  a.cand_tile = slab_tile, a.cand_max = slab_max, a.cand_cnt = cand_cnt;
+  a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
   return mfma_launch_mode<0>(dim, f32, *nlists, a, st);
 }
@@ -1709,6 +1822,9 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
   const double want = 3.0 * e + 32.0;
   uint32_t cap = 64;
   while (cap < want && cap < kMfmaMaxCandCap) cap <<= 1;
+  // a lane's quarter holds sub = cap / 4 slabs; a full quarter keeps the
+  // sub best (mf_replace_min), exact while sub >= k
+  while (cap < 4 * k) cap <<= 1;
   return cap;
 }
 
@@ -1842,8 +1958,7 @@ __device__ __forceinline__ uint32_t slab_bits(SlabMask fm, uint32_t tile, uint32
 template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
-    uint32_t cap, uint32_t k, uint32_t* __restrict__ clear, uint64_t* __restrict__ out) {
-  if (clear && blockIdx.x == 0 && threadIdx.x == 0) *clear = 0u;  // a later launch's flag
+    uint32_t cap, uint32_t k, uint64_t* __restrict__ out) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -1978,28 +2093,11 @@ __global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
 constexpr int kSelHeld = 4;                      // slabs per thread per chunk
 constexpr uint32_t kSelChunk = kSelHeld * kSelThreads;  // 2048 slabs
 
-// The main pass's overflow fallback, folded into the select: when *flag is
-// set, the sorted-list pass (MODE 8, enqueued before the select) has re-run
-// the batch, and the select merges its lists [L][kMfmaQueries][k] instead of
-// reading slabs (one launch less per batch than a separate no-op merge).
-struct SlabFallback {
-  const uint32_t* flag;  // nullable
-  const uint64_t* lists;
-  uint32_t L;
-  uint64_t lstride;
-  uint32_t* ran;  // nullable: counts fallback batches
-};
-
-__device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, uint32_t L,
-                                            uint64_t lstride, uint64_t qstride, uint32_t kin,
-                                            uint32_t k, uint32_t q, uint64_t* __restrict__ out,
-                                            uint64_t* buf, uint64_t* red, uint32_t& cnt);
-
 template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
-    uint64_t* __restrict__ out, SlabMask fm, SlabFallback fb) {
+    uint64_t* __restrict__ out, SlabMask fm) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -2008,11 +2106,6 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
   __shared__ uint32_t fill, spill;
   __shared__ uint64_t thr_sh;
   static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two lists per thread");
-  if (fb.flag && *fb.flag) {
-    if (fb.ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(fb.ran, 1u);
-    merge_query(fb.lists, fb.L, fb.lstride, k, k, k, blockIdx.x, out, buf, lmax, fill);
-    return;
-  }
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
   // lists 2 tid, 2 tid + 1: counts (both loads in flight; past nl: 0)
@@ -2199,26 +2292,21 @@ static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) 
 }
 
 hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st,
-                         uint32_t* clear) {
+                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_cand_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt,
-                     nwg, cap, k, clear, out);
+                     nwg, cap, k, out);
   return hipGetLastError();
 }
 
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
-                               const uint64_t* allow, const uint32_t* fb_flag,
-                               const uint64_t* fb_lists, uint32_t fb_L, uint64_t fb_lstride,
-                               uint32_t* fb_ran) {
+                               const uint64_t* allow) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
-  if (fb_flag && (!fb_lists || fb_L == 0 || k > kMfmaListMaxK)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
                      (const f32x4_t*)slabs, slab_tile, cand_cnt, nwg, cap, k, out,
-                     SlabMask{allow, row_base},
-                     SlabFallback{fb_flag, fb_lists, fb_L, fb_lstride, fb_ran});
+                     SlabMask{allow, row_base});
   return hipGetLastError();
 }
 
@@ -2455,10 +2543,7 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
 
 __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
     const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
-    uint32_t kin, uint32_t k, const uint32_t* __restrict__ run_if, uint32_t* __restrict__ ran,
-    uint64_t* __restrict__ out) {
-  if (run_if && *run_if == 0) return;  // fallback launch with nothing to redo
-  if (ran && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ran, 1u);
+    uint32_t kin, uint32_t k, uint64_t* __restrict__ out) {
   __shared__ uint64_t buf[kMergeCap];
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t cnt;
@@ -2467,10 +2552,10 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
 
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out,
-                        hipStream_t st, const uint32_t* run_if, uint32_t* ran) {
+                        hipStream_t st) {
   if (k == 0 || k > kMaxK || nq == 0 || L == 0 || kin == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(merge_keys_kernel, dim3(nq), dim3(kMergeThreads), 0, st, lists, L,
-                     lstride, qstride, kin, k, run_if, ran, out);
+                     lstride, qstride, kin, k, out);
   return hipGetLastError();
 }
 

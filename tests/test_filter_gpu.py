@@ -1,7 +1,7 @@
 """Payload filter pre-mask through vs_search_filtered.
 
 The bitmap is applied inside every scan kernel (GEMV, MFMA sample / candidate
-/ sorted-list passes and the overflow fallbacks); the result must be the
+/ sorted-list passes and the full-quarter replacement); the result must be the
 oracle's exact top k over the allowed rows only, with the same (score desc,
 row asc) order.
 """
@@ -37,7 +37,7 @@ def fcorpus(engine, orc):
 @pytest.mark.parametrize("nq,k", [(1, 10), (256, 10), (300, 16), (64, 100)])
 def test_filtered_search_bf16(engine, orc, fcorpus, density, nq, k):
     """nq = 1: GEMV; nq >= 2: sample + candidate MFMA passes (k > 16 and a
-    selective mask may overflow into the exact fallbacks)."""
+    selective mask may fill candidate quarters: in-place replacement)."""
     name, X = fcorpus
     rng = np.random.default_rng(int(density * 1e4) + nq + k)
     mask = rng.random(X.shape[0]) < density
@@ -89,10 +89,10 @@ def test_filtered_small_collections(engine, orc, dtype, nq):
     engine.drop_collection(name)
 
 
-def test_filtered_overflow_fallback(engine, orc):
-    """Ties under a mask: the allowed identical rows overflow the candidate
-    buffers; the sorted-list (k <= 16) and GEMV (k > 16) fallbacks must also
-    honour the mask."""
+def test_filtered_full_quarters(engine, orc):
+    """Ties under a mask: the allowed identical rows fill the candidate
+    buffers' quarters; the in-place replacement compares masked slab maxima,
+    so filtered-out rows never displace allowed ones."""
     n, dim = 70_000, 768
     base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
     base[:40_000] = base[12_345]
@@ -102,7 +102,7 @@ def test_filtered_overflow_fallback(engine, orc):
     mask = np.ones(n, bool)
     mask[:20_000:2] = False  # half of the first tied rows are filtered out
     Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 7, 20, dim)])
-    for k in (10, 50):
+    for k in (10, 50, 128):
         s, r, c = engine.search_filtered("fties", Q, k, mask)
         assert r[0].tolist() == [2 * i + 1 for i in range(k)]
         _masked_parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k, mask)

@@ -58,7 +58,7 @@ def test_fp32_batched_dims(engine, orc, dim, nq, k):
 def test_fp32_batched_small_collection_and_ties(engine, orc):
     """Small collections take the sorted-list pass (k <= 16) or per-query
     GEMV; exact duplicates must come back in row order; 40k identical rows
-    force the overflow fallbacks."""
+    fill the candidate quarters (in-place replacement)."""
     dim = 768
     base = orc.generate(orc.SEED_CORPUS, 0, 3000, dim)
     engine.create_collection("f32s", dim, 0, 0)

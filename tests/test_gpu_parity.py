@@ -119,14 +119,10 @@ def corpus_fast(engine, orc):
 @pytest.mark.parametrize("nq,k", [(2, 10), (256, 10), (300, 16), (77, 1), (256, 5), (256, 17),
                                   (64, 50), (300, 100), (33, 128)])
 def test_mfma_candidate_path(engine, orc, corpus_fast, nq, k):
-    import json
     name, X = corpus_fast
-    before = json.loads(engine.health())["mfma_fallbacks"]
     Q = orc.generate(orc.SEED_QUERY, 1000, nq, 768)
     s, r, c = engine.search(name, Q, k)
     _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
-    # random unit rows never overflow the candidate buffers
-    assert json.loads(engine.health())["mfma_fallbacks"] == before
 
 
 @pytest.mark.parametrize("dim,nq,k", [(1024, 200, 10), (1536, 129, 50), (128, 256, 10),
@@ -144,14 +140,14 @@ def test_mfma_candidate_path_dims(engine, orc, dim, nq, k):
     engine.drop_collection(name)
 
 
-def test_mfma_overflow_fallback(engine, orc):
+def test_mfma_full_quarter_replacement(engine, orc):
     """Adversarial ties: 300k rows, the first 200k identical. Every identical
     row reaches the sample bound of the queries that match it, so every lane
-    of those queries appends a slab per tile (~24 per workgroup), the
-    16-slab quarters overflow, and the sorted-list pass (k <= 16) or the GEMV
-    re-run (k > 16) must give the exact answer (ties -> lowest rows) for
-    those queries and for the others alike."""
-    import json
+    of those queries appends a slab per tile (~24 per workgroup) and its
+    quarter of the candidate buffer fills; the main pass then keeps the best
+    slabs in place (ties -> the earlier tile) and must still give the exact
+    answer (ties -> lowest rows) for those queries and for the others alike,
+    with no re-run, at every k the quarter size covers."""
     n, dim = 300_000, 768
     base = orc.generate(orc.SEED_CORPUS, 0, n, dim)
     base[:200_000] = base[12_345]
@@ -160,12 +156,10 @@ def test_mfma_overflow_fallback(engine, orc):
     X = orc.preprocess(base, True, True)
     Q = np.concatenate([base[12_345:12_346], orc.generate(orc.SEED_QUERY, 7, 40, dim),
                         base[12_345:12_346] * 3.0])
-    before = json.loads(engine.health())["mfma_fallbacks"]
-    for k in (10, 16, 50):  # k <= 16: sorted-list pass; k > 16: GEMV re-run
+    for k in (1, 10, 16, 50, 128):
         s, r, c = engine.search("ties", Q, k)
         assert r[0].tolist() == list(range(k)) and r[-1].tolist() == list(range(k))
         _parity(orc, X, orc.preprocess(Q, True, True), s, r, c, k)
-    assert json.loads(engine.health())["mfma_fallbacks"] >= before + 3
     engine.drop_collection("ties")
 
 

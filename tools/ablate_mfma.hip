@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
   const uint32_t k = 10;
   uint16_t *X, *Q;
   uint64_t *out, *skeys, *cand, *scand;
-  uint32_t *cnt, *scnt, *ovf;
+  uint32_t *cnt, *scnt;
   CK(hipMalloc(&X, ((size_t)n + 32) * 768 * 2));
   CK(hipMemset(X, 0, ((size_t)n + 32) * 768 * 2));
   CK(hipMalloc(&Q, 256 * 768 * 2));
@@ -77,12 +77,12 @@ int main(int argc, char** argv) {
   const uint32_t st = st_over ? st_over : mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
   CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 32));  // main-pass slabs
   uint32_t* ctile;
+  float* cmax;
   CK(hipMalloc(&ctile, (size_t)c.nwg * 256 * cap * 4));
+  CK(hipMalloc(&cmax, (size_t)c.nwg * 256 * cap * 4));
   CK(hipMalloc(&scand, (size_t)c.nwg * 256 * 4 * st * 8));
   CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4 * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
-  CK(hipMalloc(&ovf, 4));
-  CK(hipMemset(ovf, 0, 4));
   CK(hipMalloc(&skeys, (size_t)256 * k * 8));
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
   std::vector<float> ts;
   for (int r = 0; r < reps; ++r) {
     hipEventRecord(a, 0);
-    CK(launch_mfma_sample(X, 768, n, 0, Q, 256, k, st, scand, scnt, c.nwg, &L, 0));
+    CK(launch_mfma_sample(X, false, 768, n, 0, Q, 256, k, st, scand, scnt, c.nwg, &L, 0));
     CK(launch_select(scand, scnt, L, 4 * st, 256, k, skeys, 0));
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   MfArgs& g = c.args;
   g.X = X, g.Q = Q, g.init_th = skeys + (k - 1), g.init_stride = k, g.lists = out;
-  g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.overflow = ovf, g.cand_cap = cap;
+  g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.cand_max = cmax, g.cand_cap = cap;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
@@ -144,7 +144,14 @@ int main(int argc, char** argv) {
   }
   c.wgt = wgt;
   std::vector<Arm> arms = {
-      {"main cand", run<0, 0, 2>, true, {}},                // regs + nt (default)
+      {"main bf", run<0, 0, 2>, true, {}},                  // default: branch-free stream
+      {"main branchy", run<0, 524288, 2>, true, {}},        // r01 conditional stream
+      {"bf no-replace", run<0, 2097152, 2>, true, {}},      // full quarter drops (inexact)
+      {"bf no-max", run<0, 2097152 + 4194304, 2>, true, {}},  // + no slab max store (r02a)
+      {"main bf stag", run<0, 1048576, 2>, true, {}},       // + waves 4-7 half a chunk ahead
+      {"bf ring144", run<0, 256, 2>, true, {}},             // 8 chunks in flight
+      {"bf 24k ring144", run<0, 2048 + 256, 2>, true, {}},  // 2 barriers / tile
+      {"bf 48k ring144", run<0, 4096 + 256, 2>, true, {}},  // 1 barrier / tile
       {"main cached-dma", run<0, 1024, 2>, true, {}},       // regs, default policy
       {"main lds-cnt", run<0, 131072, 2>, true, {}},        // LDS counters + nt
       {"main v13", run<0, 131072 + 1024, 2>, true, {}},     // LDS counters, default policy
@@ -201,7 +208,7 @@ int main(int argc, char** argv) {
         hipEventRecord(a, 0);
         hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const f32x4_t*)cand,
                            (const uint32_t*)ctile, (const uint32_t*)cnt, c.nwg, cap, k, out,
-                           SlabMask{nullptr, 0}, SlabFallback{});
+                           SlabMask{nullptr, 0});
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms = 0;
@@ -276,13 +283,11 @@ int main(int argc, char** argv) {
       printf("\n");
     }
   }
-  uint32_t of = 0;
-  CK(hipMemcpy(&of, ovf, 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
   uint64_t tot = 0, mx = 0;
   for (uint32_t v : hc) tot += v, mx = v > mx ? v : mx;
-  printf("cap %u; grid %u WGs x %u rows, sample tiles/wg %u, overflow %u, slabs/query %.1f, max per buffer %lu\n",
-         cap, c.nwg, rpw, st, of, (double)tot / 256, (unsigned long)mx);
+  printf("cap %u; grid %u WGs x %u rows, sample tiles/wg %u, slabs/query %.1f, max per buffer %lu\n",
+         cap, c.nwg, rpw, st, (double)tot / 256, (unsigned long)mx);
   return 0;
 }

@@ -6,7 +6,7 @@ durs = collections.defaultdict(dict)
 for f in sys.argv[1:]:
     for r in csv.DictReader(open(f)):
         nm = r["Kernel_Name"]
-        m = re.search(r"mfma_topk_kernel<(\d+), (\d+), (\d+)(?:, (\d+))?>", nm)
+        m = re.search(r"mfma_topk_kernel<(\d+), (\d+), (\d+)(?:, (\d+))?(?:, (?:true|false))?>", nm)
         nm = f"mfma<{m.group(2)},{m.group(3)},{m.group(4)}>" if m else nm[:30]
         rows[nm][r["Counter_Name"]].append(float(r["Counter_Value"]))
         durs[nm][(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
