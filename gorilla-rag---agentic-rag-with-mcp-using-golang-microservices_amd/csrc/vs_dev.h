@@ -91,9 +91,9 @@ struct DevEngine {
   std::mutex map_mu;
   std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
   std::mutex work_mu;  // scratch buffers + stream
-  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_keys, upsert_vecs, upsert_rows;
+  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound, upsert_vecs, upsert_rows;
   DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
-  DevBuf scand, scand_cnt;          // MFMA sample pass tile maxima
+  DevBuf scand;                     // MFMA sample pass tile maxima
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
   DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch

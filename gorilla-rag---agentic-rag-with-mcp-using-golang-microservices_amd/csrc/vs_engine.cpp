@@ -267,22 +267,20 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t st = vsk::mfma_sample_tiles(n_rows);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
-  const size_t sbytes = (size_t)PS * k * 8;
+  const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds
   // main pass slabs: 32 B of scores + a 4-B tile row + a 4-B maximum per slot
   const size_t slots = (size_t)maxl * PS * cap;
   const size_t cbytes = slots * 40;
-  const size_t scbytes = (size_t)maxl * PS * 4 * st * 8;
+  const size_t scbytes = (size_t)maxl * st * PS * 4;  // tile maxima, [query][wg * st]
   const size_t nbytes = (size_t)maxl * PS * 4 * 4;
-  if (eng->lists.bytes < lbytes || eng->sample_keys.bytes < sbytes || eng->cand.bytes < cbytes ||
-      eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes ||
-      eng->scand_cnt.bytes < nbytes) {
+  if (eng->lists.bytes < lbytes || eng->sample_bound.bytes < sbytes || eng->cand.bytes < cbytes ||
+      eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
-    VS_HIP(eng->sample_keys.ensure(sbytes), "alloc sample scratch");
+    VS_HIP(eng->sample_bound.ensure(sbytes), "alloc sample bounds");
     VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
-    VS_HIP(eng->scand.ensure(scbytes), "alloc sample candidate scratch");
+    VS_HIP(eng->scand.ensure(scbytes), "alloc sample tile maxima");
     VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
-    VS_HIP(eng->scand_cnt.ensure(nbytes), "alloc sample candidate counts");
   }
   const void* X = c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
@@ -300,7 +298,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     uint32_t L = 0;
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, nullptr, 0, lists,
+      VS_HIP(vsk::launch_mfma_lists(X, f32, dim, n_rows, row_base, qb, nv, k, nullptr, lists,
                                     maxl, &L, eng->stream, allow),
              "mfma scan (lists)");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
@@ -310,19 +308,16 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(ev_end(eng, eng->merge_ev), "event");
       continue;
     }
-    // 1. sample pass -> bound keys skeys[q * k + k - 1]
-    uint64_t* skeys = eng->sample_keys.as<uint64_t>();
-    VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qb, nv, k, st,
-                                   eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), maxl,
-                                   &L, eng->stream, allow),
+    // 1. sample pass -> tile maxima -> per-query bound (k-th largest maximum)
+    float* bound = eng->sample_bound.as<float>();
+    float* tmax = eng->scand.as<float>();
+    VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qb, nv, k, st, tmax, maxl, &L,
+                                   eng->stream, allow),
            "mfma sample scan");
-    VS_HIP(vsk::launch_select(eng->scand.as<uint64_t>(), eng->scand_cnt.as<uint32_t>(), L, 4 * st,
-                              nv, k, skeys, eng->stream),
-           "sample select");
-    const uint64_t* init = skeys + (k - 1);
+    VS_HIP(vsk::launch_sample_bound(tmax, L * st, nv, k, bound, eng->stream), "sample bound");
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-    VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, init, k, slabs,
+    VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
                                  slab_tile, slab_max, cap, eng->cand_cnt.as<uint32_t>(), maxl,
                                  &L, eng->stream, allow),
            "mfma scan");

@@ -70,12 +70,12 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 // nq_valid <= mfma_queries(dim, f32), k <= kMfmaMaxK; one workgroup per CU
 // streams a contiguous row range (nlists workgroups).
 //  * sample pass: first max_tiles 32-row tiles of every workgroup; each
-//    tile's maximum per query -> cand[nlists][kMfmaQueries][4 * max_tiles]
-//    with counts cand_cnt; launch_select(.., cap = 4 * max_tiles, k, ..) then
-//    gives per query the top k of those maxima, whose k-th key lower-bounds
-//    the global k-th key;
+//    tile's (masked) maximum score per query -> tmax[kMfmaQueries][m], m =
+//    nlists * max_tiles (-inf past a workgroup's last tile);
+//    launch_sample_bound then gives per query the k-th largest of those
+//    maxima: k distinct rows reach it, so it lower-bounds the k-th score;
 //  * main pass: every row; a lane whose 8 scores of a tile reach the
-//    per-query lower bound init_th[q * init_stride] appends them as one slab
+//    per-query lower bound init_score[q] appends them as one slab
 //    (8 f32, the accumulator layout) and the tile's first global row to the
 //    query's buffer: slabs[nlists][kMfmaQueries][cap][8],
 //    slab_tile[nlists][kMfmaQueries][cap] and each slab's masked maximum
@@ -93,28 +93,26 @@ bool mfma_supported(uint32_t dim, bool f32);
 uint32_t mfma_queries(uint32_t dim, bool f32);  // queries per launch at this dim
 hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const void* Q, uint32_t nq_valid,
-                              uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
-                              uint32_t max_lists, uint32_t* nlists, hipStream_t st,
-                              const uint64_t* allow = nullptr);
+                              uint32_t k, uint32_t max_tiles, float* tmax, uint32_t max_lists,
+                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
+// bound[q] = the k-th largest of tmax[q][0, m) (radix select; -inf if m < k).
+hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
+                               float* bound, hipStream_t st);
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
-                            const uint64_t* init_th, uint32_t init_stride, float* slabs,
+                            const float* init_score, float* slabs,
                             uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow = nullptr);
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
-                             uint32_t k, const uint64_t* init_th, uint32_t init_stride,
-                             uint64_t* lists, uint32_t max_lists,
+                             uint32_t k, const float* init_score, uint64_t* lists,
+                             uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
-// Top-k of per-workgroup candidate buffers cand[nwg][kMfmaQueries][cap] (4
-// quarters, counts cand_cnt[nwg][kMfmaQueries][4]) for queries 0 .. nq-1 ->
-// out[nq][k], sorted, 0-padded.
-hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st);
-// The same over the main pass's slab buffers (see launch_mfma_cand); the
-// main pass leaves masked rows in its slabs, so the select applies the same
-// pre-mask `allow` (local rows = global - row_base).
+// Top-k of the main pass's slab buffers (see launch_mfma_cand) for queries
+// 0 .. nq-1 -> out[nq][k], sorted, 0-padded; the main pass leaves masked rows
+// in its slabs, so the select applies the same pre-mask `allow` (local rows =
+// global - row_base).
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,

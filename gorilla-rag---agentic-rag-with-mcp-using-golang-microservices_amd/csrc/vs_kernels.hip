@@ -932,16 +932,16 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 struct MfArgs {
   const void* X;            // corpus rows (bf16 or fp32), row-major, 32 rows of padding
   const void* Q;            // kMfmaQueries x D, the collection's dtype (zero-padded)
-  const uint64_t* init_th;  // nullable: per-query lower-bound keys at [q * init_stride]
-  uint64_t* lists;          // MODE 3 / 8: [nwg][kMfmaQueries][k] sorted keys
-  uint64_t* cand;           // MODE 3: [nwg][kMfmaQueries][cand_cap] unsorted keys; MODE 0:
-                            // [nwg][kMfmaQueries][cand_cap] slabs of 8 f32 scores (32 B);
-                            // quarter kq of a query's buffer belongs to its lane kq
+  const float* init_score;  // nullable: per-query lower bound on the k-th score (MODE 0 / 8)
+  uint64_t* lists;          // MODE 8: [nwg][kMfmaQueries][k] sorted keys
+  float* tmax;              // MODE 3: [kMfmaQueries][nwg * max_tiles] tile maxima
+  uint64_t* cand;           // MODE 0: [nwg][kMfmaQueries][cand_cap] slabs of 8 f32 scores
+                            // (32 B); quarter kq of a query's buffer belongs to its lane kq
   uint32_t* cand_tile;      // MODE 0: first global row of each slab's tile
   float* cand_max;          // MODE 0: each slab's (masked) maximum score
-  uint32_t* cand_cnt;       // MODE 0 / 3: [nwg][kMfmaQueries][4] keys / slabs per quarter
+  uint32_t* cand_cnt;       // MODE 0: [nwg][kMfmaQueries][4] slabs per quarter
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
-  uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, init_stride, cand_cap;
+  uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, cand_cap;
   const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
 };
 
@@ -1163,12 +1163,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // candidate passes keep each lane's per-group append counters in LDS (a
   // register each would push the kernel past 256 VGPRs, and the compiler
   // then drops the A-fragment prefetch of the streaming loop: r01)
-  constexpr int kCntBytes = (MODE == 0 || MODE == 3) ? 64 * WAVES * G * 4 : 0;
+  constexpr int kCntBytes = MODE == 0 ? 64 * WAVES * G * 4 : 0;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
                     MODE == 8 ? kMfListBytes : 16 + kCntBytes, WAVES, kCsx, EB>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
   constexpr bool kLists = MODE == 8;
-  constexpr bool kCand = MODE == 0 || MODE == 3;
   constexpr int PPW = S::PPW;
   constexpr int kPD0 = (VAR & 64) ? 3 : ((VAR & 32) ? 2 : 1);
   constexpr int kPD = ((S::CPT * S::CT) % (kPD0 + 1) == 0) ? kPD0 : 1;
@@ -1202,6 +1201,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   uint32_t ntiles = (wr1 - wr0 + 31) / 32;
   if (a.max_tiles && ntiles > a.max_tiles) ntiles = a.max_tiles;
   const uint32_t nchunks = ntiles * S::CPT;
+  const uint32_t tstride = gridDim.x * a.max_tiles;  // MODE 3: tile maxima per query
 
   if constexpr (kLists)
     for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += THREADS) lists[i] = 0;
@@ -1234,8 +1234,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     const uint4* qrow = (const uint4*)((const unsigned char*)a.Q + (size_t)ql[g] * RBY);
 #pragma unroll
     for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
-    const uint64_t it = (a.init_th && qvalid[g]) ? a.init_th[(size_t)ql[g] * a.init_stride] : 0;
-    th_s[g] = it ? key_score(it) : -INFINITY;
+    th_s[g] = (a.init_score && qvalid[g]) ? a.init_score[ql[g]] : -INFINITY;
   }
 
   // LDS-DMA source mapping: piece (s4l, rg) of a chunk holds rows rg*8 ..
@@ -1245,6 +1244,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // is a scalar base advanced chunk by chunk (the chunk issued at step c is
   // c + AHEAD). Tiles past the last row read the collection's 32 rows of
   // allocation padding (vs_engine.cpp grow()) and are masked in the epilogue.
+  // VAR 8192: the prologue's loads drained and timed (ablation only)
+  uint64_t tclk1 = 0, tclk2 = 0;
+  if constexpr (kClock) {
+    __builtin_amdgcn_s_waitcnt(0);
+    tclk1 = wall_clock64();
+  }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
   uint32_t loff[PPW];
 #pragma unroll
@@ -1584,17 +1589,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         }
         continue;
       }
-      // sample pass: one candidate per (tile, query), the tile maximum
-      float lvl = th_s[g];
+      // sample pass: the tile maximum per query (the 4 lane quarters'
+      // maxima), one float per (query, tile): no keys, ballots or counters
       if constexpr (MODE == 3) {
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        lvl = mx > lvl ? mx : lvl;
+        if (kq == 0 && qvalid[g])
+          a.tmax[(size_t)ql[g] * tstride + (size_t)blockIdx.x * a.max_tiles + t] = mx;
+        continue;
       }
       if constexpr (MODE == 6) {
         asm volatile("" ::"v"(mx));
         continue;
       }
+      const float lvl = th_s[g];
       if (__any(qvalid[g] && mx >= lvl)) {
         uint32_t m = 0;
 #pragma unroll
@@ -1613,33 +1621,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           const uint32_t row = trow0 + 16 * (b >> 2) + 4 * kq + (b & 3);
           return make_key(sc, a.row_base + row);
         };
-        if constexpr (kCand) {
-          // lane-private quarter of the buffer: no atomics, fire-and-forget stores
-          const uint32_t n = (uint32_t)__popc(m);
-          const uint32_t sub = a.cand_cap >> 2;
-          const uint32_t cg = n ? cntl[g * THREADS + threadIdx.x] : 0u;
-          if (n) {
-            // a full quarter drops tile maxima: that only lowers the sample
-            // bound, which stays valid
-            if (cg + n <= sub) {
-              // the address is rebuilt here from an opaque thread id, so none
-              // of it is hoisted out of the tile loop (its register budget)
-              uint32_t tid = threadIdx.x;
-              asm volatile("" : "+v"(tid));
-              const uint32_t qo = (tid >> 6) * QPW + g * 16 + (tid & 15);
-              uint64_t* dst = a.cand + ((size_t)blockIdx.x * kMfmaQueries + qo) * a.cand_cap +
-                              ((tid & 63) >> 4) * sub + cg;
-              cntl[g * THREADS + threadIdx.x] = cg + n;
-              while (m) {
-                const int b = __builtin_ctz(m);
-                m &= m - 1;
-                *dst++ = key_of(b);
-              }
-            }
-          }
-        } else {
-          mf_insert(m, key_of, lists + (size_t)ql[g] * kMfListLen, k, lane, col, kq, th_s[g]);
-        }
+        mf_insert(m, key_of, lists + (size_t)ql[g] * kMfListLen, k, lane, col, kq, th_s[g]);
       }
     }
   };
@@ -1662,17 +1644,18 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     run_tiles(MfFull<false>{});
   }
   if constexpr (kDma && kBF) wait_vmcnt<0>();  // no LDS-DMA outlives the workgroup
-  if constexpr (kClock)
-    if (threadIdx.x == 0) {
-      a.lists[2 * blockIdx.x] = tclk0;
-      a.lists[2 * blockIdx.x + 1] = wall_clock64();
-    }
+  if constexpr (kClock) tclk2 = wall_clock64();
   // each wave owns its queries' lists / counters: no barrier before the write-out
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    if constexpr (kCand) {
+    if constexpr (MODE == 0) {
       a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
           kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
+    } else if constexpr (MODE == 3) {
+      // a workgroup with fewer tiles than max_tiles: the rest are empty
+      for (uint32_t t = ntiles + kq; t < a.max_tiles; t += 4)
+        if (qvalid[g]) a.tmax[(size_t)ql[g] * tstride + (size_t)blockIdx.x * a.max_tiles + t] =
+            -INFINITY;
     } else if constexpr (kLists) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1683,6 +1666,13 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       }
     }
   }
+  if constexpr (kClock)
+    if (threadIdx.x == 0) {  // [start, prologue done, tiles done, end] per workgroup
+      a.lists[4 * blockIdx.x] = tclk0;
+      a.lists[4 * blockIdx.x + 1] = tclk1;
+      a.lists[4 * blockIdx.x + 2] = tclk2;
+      a.lists[4 * blockIdx.x + 3] = wall_clock64();
+    }
 }
 
 bool mfma_supported(uint32_t dim, bool f32) {
@@ -1762,16 +1752,13 @@ static bool mfma_args_ok(uint32_t dim, bool f32, uint32_t n_rows, uint32_t nq_va
 
 hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const void* Q, uint32_t nq_valid,
-                              uint32_t k, uint32_t max_tiles, uint64_t* cand, uint32_t* cand_cnt,
-                              uint32_t max_lists, uint32_t* nlists, hipStream_t st,
-                              const uint64_t* allow) {
-  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || max_tiles == 0 ||
-      max_tiles > kMfmaMaxCandCap)
-    return hipErrorInvalidValue;
+                              uint32_t k, uint32_t max_tiles, float* tmax, uint32_t max_lists,
+                              uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
+  if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || max_tiles == 0) return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.cand = cand, a.cand_cnt = cand_cnt, a.cand_cap = 4 * max_tiles;
+  a.X = X, a.Q = Q, a.tmax = tmax;
   a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
   a.k = k, a.allow = allow;
   return mfma_launch_mode<3>(dim, f32, *nlists, a, st);
@@ -1779,15 +1766,15 @@ hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_
 
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
-                             uint32_t k, const uint64_t* init_th, uint32_t init_stride,
-                             uint64_t* lists, uint32_t max_lists,
+                             uint32_t k, const float* init_score, uint64_t* lists,
+                             uint32_t max_lists,
                              uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || k > kMfmaListMaxK)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.lists = lists;
+  a.X = X, a.Q = Q, a.init_score = init_score, a.lists = lists;
   a.n_rows = n_rows, a.row_base = row_base, a.nq_valid = nq_valid, a.k = k;
   a.allow = allow;
   return mfma_launch_mode<8>(dim, f32, *nlists, a, st);
@@ -1795,7 +1782,7 @@ hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_r
 
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
-                            const uint64_t* init_th, uint32_t init_stride, float* slabs,
+                            const float* init_score, float* slabs,
                             uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow) {
@@ -1805,7 +1792,7 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
-  a.X = X, a.Q = Q, a.init_th = init_th, a.init_stride = init_stride, a.cand = (uint64_t*)slabs;
+  a.X = X, a.Q = Q, a.init_score = init_score, a.cand = (uint64_t*)slabs;
   a.cand_tile = slab_tile, a.cand_max = slab_max, a.cand_cnt = cand_cnt;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
@@ -1909,30 +1896,6 @@ __device__ __forceinline__ void sel_finish_wave(const uint64_t* buf, uint32_t c,
   for (uint32_t j = (uint32_t)lane; j < k; j += 64) out[j] = j < 64 ? x : 0ull;
 }
 
-// max (or filtered append) over one quarter list, 4 loads in flight
-template <bool APPEND>
-__device__ __forceinline__ uint64_t sel_scan_quarter(const uint64_t* __restrict__ p, uint32_t c,
-                                                     uint64_t thr, uint64_t* buf,
-                                                     uint32_t* fill, uint32_t* spill) {
-  uint64_t m = 0;
-  for (uint32_t j = 0; j < c; j += 4) {
-    uint64_t x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = j + u < c ? p[j + u] : 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if constexpr (APPEND) {
-        if (x[u] > thr) {
-          const uint32_t pos = atomicAdd(fill, 1u);
-          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = x[u]; else *spill = 1u;
-        }
-      } else {
-        m = x[u] > m ? x[u] : m;
-      }
-    }
-  }
-  return m;
-}
 
 // Main-pass slabs: slab j of quarter list l holds the scores of rows
 // tile + 16 (b / 4) + 4 kq + b % 4, b = 0..7 (the MFMA accumulator layout; kq
@@ -1949,132 +1912,6 @@ __device__ __forceinline__ uint32_t slab_bits(SlabMask fm, uint32_t tile, uint32
   const uint32_t r = tile - fm.row_base;
   const uint32_t tw = (uint32_t)(fm.allow[r >> 6] >> (r & 32)) >> (4 * kq);
   return (tw & 0xFu) | ((tw >> 12) & 0xF0u);
-}
-
-// The sample pass's key buffers (select_slab_kernel below takes the main
-// pass's slabs).
-// SV (ablation builds only, tools/ablate_mfma.hip): 1 = stop after the
-// first pass, 2 = after the bound, 3 = after the append pass.
-template <int SV = 0>
-__global__ __launch_bounds__(kSelThreads) void select_cand_kernel(
-    const uint64_t* __restrict__ cand, const uint32_t* __restrict__ cnt, uint32_t nwg,
-    uint32_t cap, uint32_t k, uint64_t* __restrict__ out) {
-  __shared__ uint64_t buf[kMfmaSelBuf];
-  __shared__ uint64_t lmax[kMfmaMaxLists];
-  __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
-  __shared__ uint32_t fill, spill;
-  __shared__ uint64_t thr_sh;
-  static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two quarters per thread");
-  const uint32_t q = blockIdx.x;
-  const uint32_t sub = cap >> 2, nl = 4 * nwg;  // a buffer = 4 lane quarters
-  // first key of quarter list l: [wg][query][cap], a quarter = sub keys
-  auto qoff = [&](uint32_t l) -> size_t {
-    return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub;
-  };
-  uint32_t qc[2];
-  {
-    uint32_t craw[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {  // both counts in flight (index clamped, masked)
-      const uint32_t l = threadIdx.x + r * kSelThreads;
-      const uint32_t lc = l < nl ? l : 0u;
-      craw[r] = cnt[((size_t)(lc >> 2) * kMfmaQueries + q) * 4 + (lc & 3)];
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const uint32_t l = threadIdx.x + r * kSelThreads;
-      const uint32_t c = l < nl ? craw[r] : 0u;
-      qc[r] = c < sub ? c : sub;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const uint32_t l = threadIdx.x + r * kSelThreads;
-    uint64_t m = sel_scan_quarter<false>(cand + qoff(l < nl ? l : 0u), qc[r], 0, buf, &fill,
-                                         &spill);
-#pragma unroll
-    for (int s = 1; s <= 2; s <<= 1) {  // the 4 quarters of a buffer are 4 adjacent lanes
-      const uint64_t o = __shfl_xor(m, s, 64);
-      m = o > m ? o : m;
-    }
-    if ((l & 3) == 0) lmax[l >> 2] = m;
-  }
-  if (threadIdx.x == 0) fill = 0, spill = 0;
-  __syncthreads();
-  if constexpr (SV == 1) return;
-  // admit keys > thr (0 marks an empty slot)
-  uint64_t thr;
-  if (k <= 64) {
-    if (threadIdx.x < 64) {
-      const uint64_t b = sel_bound_wave(lmax, k, (int)threadIdx.x);
-      if (threadIdx.x == 0) thr_sh = b ? b - 1 : 0;
-    }
-    __syncthreads();
-    thr = thr_sh;
-  } else {
-    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
-    thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
-  }
-  if constexpr (SV == 2) return;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const uint32_t l = threadIdx.x + r * kSelThreads;
-    sel_scan_quarter<true>(cand + qoff(l < nl ? l : 0u), qc[r], thr, buf, &fill, &spill);
-  }
-  __syncthreads();
-  if constexpr (SV == 3) return;
-  uint32_t nR = 0;  // running top-k in buf[0, nR)
-  if (!spill && fill <= 64) {
-    if (threadIdx.x < 64) sel_finish_wave(buf, fill, k, (int)threadIdx.x, out + (size_t)q * k);
-    return;
-  }
-  if (!spill) {
-    const uint32_t c = fill;
-    if (c) {
-      int p2 = 1;
-      while ((uint32_t)p2 < c) p2 <<= 1;
-      for (uint32_t i = c + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
-      __syncthreads();
-      bitonic_sort_desc_n(buf, p2, kSelThreads);
-      nR = c < k ? c : k;
-    }
-  } else {
-    for (uint32_t l = threadIdx.x; l < nl; l += kSelThreads) pre[l + 1] = qc[l / kSelThreads];
-    if (threadIdx.x == 0) {
-      pre[0] = 0;
-      for (uint32_t l = 0; l < nl; ++l) pre[l + 1] += pre[l];
-    }
-    __syncthreads();
-    const uint32_t total = pre[nl];
-    const uint32_t chunk = kMfmaSelBuf - k;
-    for (uint32_t base = 0; base < total; base += chunk) {
-      if (threadIdx.x == 0) fill = nR;
-      __syncthreads();
-      const uint32_t end = base + chunk < total ? base + chunk : total;
-      for (uint32_t i = base + threadIdx.x; i < end; i += kSelThreads) {
-        uint32_t lo = 0, hi = nl;  // last quarter list with pre[lo] <= i
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (pre[mid] <= i) lo = mid; else hi = mid;
-        }
-        const uint64_t x = cand[qoff(lo) + (i - pre[lo])];
-        if (x > thr) buf[atomicAdd(&fill, 1u)] = x;
-      }
-      __syncthreads();
-      const uint32_t c = fill;
-      if (c > nR) {
-        int p2 = 1;
-        while ((uint32_t)p2 < c) p2 <<= 1;
-        for (uint32_t i = c + threadIdx.x; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
-        __syncthreads();
-        bitonic_sort_desc_n(buf, p2, kSelThreads);
-        nR = c < k ? c : k;
-        if (nR == k && buf[k - 1] > thr) thr = buf[k - 1];
-      }
-      __syncthreads();
-    }
-  }
-  for (uint32_t j = threadIdx.x; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
 }
 
 // Slab select, compacted (the main pass's buffers; one workgroup per query).
@@ -2286,18 +2123,84 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
   for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
 }
 
+// ---------------------------------------------------------------------------
+// sample bound: per query, a lower bound on the k-th largest of m tile maxima
+// (k maxima of k distinct tiles: k distinct rows score at least that much, so
+// it bounds the query's global k-th score from below). Radix select on the
+// order-preserving 32-bit image of the scores, 8 bits per pass, LDS histogram
+// + one block scan per pass; one workgroup per query. Two passes: the bound is
+// the lowest value of the 16-bit bucket holding the k-th largest (at least k
+// maxima reach it; it sits below the exact k-th by under 2^-7 relative, which
+// admits a few more rows than the exact value would, for half the passes).
+// Fewer than k maxima give -inf: every row is then admitted.
+// ---------------------------------------------------------------------------
+constexpr int kBoundThreads = 256;
+
+__device__ __forceinline__ uint32_t ord_f32(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+__global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
+    const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wsum[kBoundThreads / 64];
+  __shared__ uint32_t pick, above;
+  const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (m < k) {
+    if (tid == 0) bound[q] = -INFINITY;
+    return;
+  }
+  const float* v = tmax + (size_t)q * m;
+  uint32_t prefix = 0, kk = k;  // the kk-th largest of the values matching prefix
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    hist[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += kBoundThreads) {
+      const uint32_t u = ord_f32(v[i]);
+      if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    // inclusive scan over the digits in descending order (thread t: digit 255 - t)
+    const uint32_t c = hist[255 - tid];
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    for (uint32_t j = 0; j < w; ++j) x += wsum[j];
+    // exactly one digit has (count above) < kk <= (count above + its own)
+    if (x >= kk && x - c < kk) pick = tid, above = x - c;
+    __syncthreads();
+    prefix |= (uint32_t)(255 - pick) << shift;
+    kk -= above;
+    __syncthreads();  // pick / above / wsum / hist are rewritten by the next pass
+  }
+  // the bucket of -inf starts below ord(-inf), in the negative-NaN codes
+  if (tid == 0) bound[q] = prefix <= ord_f32(-INFINITY) ? -INFINITY : unord_f32(prefix);
+}
+
+hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
+                               float* bound, hipStream_t st) {
+  if (nq == 0 || nq > kMfmaQueries || k == 0 || k > kMfmaMaxK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_bound_kernel, dim3(nq), dim3(kBoundThreads), 0, st, tmax, m, k, bound);
+  return hipGetLastError();
+}
+
 static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) {
   return nwg != 0 && nwg <= kMfmaMaxLists && cap >= 4 && cap % 4 == 0 && k != 0 &&
          k <= kMfmaMaxK && nq != 0 && nq <= kMfmaQueries;
 }
 
-hipError_t launch_select(const uint64_t* cand, const uint32_t* cand_cnt, uint32_t nwg,
-                         uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out, hipStream_t st) {
-  if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_cand_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st, cand, cand_cnt,
-                     nwg, cap, k, out);
-  return hipGetLastError();
-}
 
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,

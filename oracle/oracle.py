@@ -29,6 +29,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB512_PATH = os.path.join(HERE, "liboracle_avx512.so")  # CPU baseline on AVX-512 hosts
 
 SEED_CORPUS = 0x5EED
 SEED_QUERY = 0xC0FFEE
@@ -39,7 +40,9 @@ _lib = None
 def build() -> str:
     """Compile liboracle.so (gcc, OpenMP) if missing or stale."""
     src = os.path.join(HERE, "vsearch_oracle.c")
-    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    stale = [p for p in (LIB_PATH, LIB512_PATH)
+             if not os.path.exists(p) or os.path.getmtime(p) < os.path.getmtime(src)]
+    if stale:
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -154,14 +157,52 @@ def rescore(X: np.ndarray, Q: np.ndarray, rows: np.ndarray, counts: np.ndarray,
     return out
 
 
+def cpu_info() -> dict:
+    """Host CPU model and whether it has AVX-512 (Linux /proc/cpuinfo)."""
+    model, flags = "unknown", set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") and model == "unknown":
+                    model = line.split(":", 1)[1].strip()
+                elif line.startswith("flags") and not flags:
+                    flags = set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return {"model": model, "avx512": "avx512f" in flags, "logical_cpus": os.cpu_count()}
+
+
+_scan_lib = None
+
+
+def scan_lib():
+    """The CPU-baseline build for this host: AVX-512 when the CPU has it."""
+    global _scan_lib
+    if _scan_lib is None:
+        build()
+        path = LIB512_PATH if cpu_info()["avx512"] and os.path.exists(LIB512_PATH) else LIB_PATH
+        L = ctypes.CDLL(path)
+        vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        L.oracle_cpu_scan.argtypes = [vp, i32, u64, u32, vp, u32, u32, i32, vp, vp]
+        L.oracle_cpu_scan.restype = i32
+        L.oracle_cpu_scan_lanes.restype = i32
+        _scan_lib = L
+    return _scan_lib
+
+
+def cpu_scan_isa() -> str:
+    return "avx512" if scan_lib().oracle_cpu_scan_lanes() == 16 else "avx2"
+
+
 def cpu_scan(X_raw: np.ndarray, bf16: bool, Q: np.ndarray, k: int, threads: int = 0):
-    """Qdrant-style fp32 exact scan (the CPU baseline). Returns (scores, rows, threads)."""
+    """Qdrant-style fp32 exact scan (the CPU baseline), one query at a time.
+    Returns (scores, rows, threads)."""
     Q = np.ascontiguousarray(Q, np.float32)
     nq, dim = Q.shape
     s = np.zeros((nq, k), np.float32)
     r = np.zeros((nq, k), np.uint64)
-    nth = lib().oracle_cpu_scan(_p(X_raw), int(bf16), X_raw.shape[0], dim, _p(Q), nq, k,
-                                threads, _p(s), _p(r))
+    nth = scan_lib().oracle_cpu_scan(_p(X_raw), int(bf16), X_raw.shape[0], dim, _p(Q), nq, k,
+                                     threads, _p(s), _p(r))
     return s, r, nth
 
 

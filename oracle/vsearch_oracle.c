@@ -369,30 +369,41 @@ void oracle_rescore_generated(uint64_t seed, uint32_t dim, int bf16, const float
 }
 
 /* ---- CPU baseline: restatement of Qdrant's plain exact scan ----
- * fp32 dot with 8 independent accumulators (Qdrant's AVX path keeps four
- * 8-wide accumulators), OpenMP over row blocks, per-thread fixed-length
- * top-k, then a merge. Values are read as stored (fp32, or bf16 widened).
- * Returns the number of threads used. */
+ * fp32 dot with O_LANES independent accumulators (one SIMD register's worth
+ * of lanes: 8 under AVX2 -- Qdrant's AVX path -- and 16 in the AVX-512
+ * build, liboracle_avx512.so), OpenMP over row blocks, per-thread
+ * fixed-length top-k, then a merge. Values are read as stored (fp32, or
+ * bf16 widened). Returns the number of threads used. */
+#ifdef __AVX512F__
+#define O_LANES 16
+#else
+#define O_LANES 8
+#endif
+static float o_hsum(float* acc) { /* pairwise tree: lanes j and j + w */
+  for (int w = O_LANES / 2; w >= 1; w /= 2)
+    for (int j = 0; j < w; ++j) acc[j] += acc[j + w];
+  return acc[0];
+}
 static float o_dot_f32(const float* x, const float* q, uint32_t dim) {
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[O_LANES] = {0};
   uint32_t d = 0;
-  for (; d + 8 <= dim; d += 8)
-    for (int j = 0; j < 8; ++j) acc[j] += x[d + j] * q[d + j];
-  float s = ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
+  for (; d + O_LANES <= dim; d += O_LANES)
+    for (int j = 0; j < O_LANES; ++j) acc[j] += x[d + j] * q[d + j];
+  float s = o_hsum(acc);
   for (; d < dim; ++d) s += x[d] * q[d];
   return s;
 }
 static float o_dot_bf16(const uint16_t* x, const float* q, uint32_t dim) {
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[O_LANES] = {0};
   uint32_t d = 0;
-  for (; d + 8 <= dim; d += 8)
-    for (int j = 0; j < 8; ++j) {
+  for (; d + O_LANES <= dim; d += O_LANES)
+    for (int j = 0; j < O_LANES; ++j) {
       uint32_t u = (uint32_t)x[d + j] << 16;
       float v;
       memcpy(&v, &u, 4);
       acc[j] += v * q[d + j];
     }
-  float s = ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
+  float s = o_hsum(acc);
   for (; d < dim; ++d) {
     uint32_t u = (uint32_t)x[d] << 16;
     float v;
@@ -401,6 +412,9 @@ static float o_dot_bf16(const uint16_t* x, const float* q, uint32_t dim) {
   }
   return s;
 }
+
+/* SIMD width the CPU baseline was built for (8 = AVX2, 16 = AVX-512). */
+int oracle_cpu_scan_lanes(void) { return O_LANES; }
 
 int oracle_cpu_scan(const void* X, int bf16, uint64_t n, uint32_t dim, const float* Q,
                     uint32_t nq, uint32_t k, int threads, float* out_scores,

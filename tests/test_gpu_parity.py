@@ -334,12 +334,15 @@ def test_bench_small_runs():
     for cfg in ("c3", "c2"):
         res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", cfg,
                               "--rows", "300000", "--steps", "3", "--warmup", "1",
-                              "--cpu-sample-rows", "20000", "--cpu-sample-queries", "2"],
+                              "--cpu-sample-rows", "20000", "--cpu-budget-s", "0.5"],
                              capture_output=True, text=True, timeout=300)
         assert res.returncode == 0, res.stderr[-3000:]
         line = json.loads(res.stdout.strip().splitlines()[-1])
         assert line["value"] > 0 and line["roofline"]["frac"] > 0
         assert line["cpu_baseline"]["value"] > 0
+        assert line["cpu_baseline"]["cpu_model"] and line["cpu_baseline"]["isa"] in ("avx2", "avx512")
+        if cfg == "c3":  # batched config: the BLAS secondary is reported too
+            assert line["cpu_baseline"]["batched"]["value"] > 0
 
 
 def test_large_properties(engine, orc):

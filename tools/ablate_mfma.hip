@@ -31,7 +31,7 @@ struct Ctx {
 template <int MODE, int VAR, int G = 2>
 static float run(const Ctx& c, bool bound) {
   MfArgs a = c.args;
-  if (!bound) a.init_th = nullptr;
+  if (!bound) a.init_score = nullptr;
   if (VAR & 65536) a.wg_tile = c.wgt;  // ablation: the weighted split
   // VS_ABL_BURST=B: B launches back to back per timing (sustained clocks, as
   // in a serving loop; the time per launch is returned). Default 1
@@ -62,8 +62,9 @@ int main(int argc, char** argv) {
   const uint32_t st_over = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;  // sample tiles override
   const uint32_t k = 10;
   uint16_t *X, *Q;
-  uint64_t *out, *skeys, *cand, *scand;
-  uint32_t *cnt, *scnt;
+  uint64_t *out, *cand;
+  float *tmax, *bnd;
+  uint32_t* cnt;
   CK(hipMalloc(&X, ((size_t)n + 32) * 768 * 2));
   CK(hipMemset(X, 0, ((size_t)n + 32) * 768 * 2));
   CK(hipMalloc(&Q, 256 * 768 * 2));
@@ -80,10 +81,9 @@ int main(int argc, char** argv) {
   float* cmax;
   CK(hipMalloc(&ctile, (size_t)c.nwg * 256 * cap * 4));
   CK(hipMalloc(&cmax, (size_t)c.nwg * 256 * cap * 4));
-  CK(hipMalloc(&scand, (size_t)c.nwg * 256 * 4 * st * 8));
-  CK(hipMalloc(&scnt, (size_t)c.nwg * 256 * 4 * 4));
+  CK(hipMalloc(&tmax, (size_t)c.nwg * 256 * st * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
-  CK(hipMalloc(&skeys, (size_t)256 * k * 8));
+  CK(hipMalloc(&bnd, 256 * 4));
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
@@ -93,8 +93,8 @@ int main(int argc, char** argv) {
   std::vector<float> ts;
   for (int r = 0; r < reps; ++r) {
     hipEventRecord(a, 0);
-    CK(launch_mfma_sample(X, false, 768, n, 0, Q, 256, k, st, scand, scnt, c.nwg, &L, 0));
-    CK(launch_select(scand, scnt, L, 4 * st, 256, k, skeys, 0));
+    CK(launch_mfma_sample(X, false, 768, n, 0, Q, 256, k, st, tmax, c.nwg, &L, 0));
+    CK(launch_sample_bound(tmax, L * st, 256, k, bnd, 0));
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms = 0;
@@ -103,7 +103,7 @@ int main(int argc, char** argv) {
   }
   CK(hipDeviceSynchronize());
   MfArgs& g = c.args;
-  g.X = X, g.Q = Q, g.init_th = skeys + (k - 1), g.init_stride = k, g.lists = out;
+  g.X = X, g.Q = Q, g.init_score = bnd, g.lists = out;
   g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.cand_max = cmax, g.cand_cap = cap;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const double bytes = (double)n * 768 * 2, flops = 2.0 * 256 * n * 768;
   std::sort(ts.begin(), ts.end());
-  printf("%-16s median %.3f ms  min %.3f ms\n", "sample+merge", ts[ts.size() / 2], ts[0]);
+  printf("%-16s median %.3f ms  min %.3f ms\n", "sample+bound", ts[ts.size() / 2], ts[0]);
   for (auto& arm : arms) {
     std::sort(arm.t.begin(), arm.t.end());
     const float med = arm.t[arm.t.size() / 2];
@@ -256,31 +256,44 @@ int main(int argc, char** argv) {
     printf("slabs/query %.1f; keys past the select's first bound: mean %.1f, max %u\n",
            slab_sum / 256, pass_sum / 256, pass_max);
   }
-  // per-workgroup start / end clocks of the main pass (VAR 8192; wall_clock64
-  // ticks at 100 MHz) in the last of `burst` back-to-back launches: how far
-  // the static row split leaves XCDs apart (blockIdx % 8 = XCD)
-  for (int burst : {1, 8}) {
+  // per-workgroup clocks [start, prologue done, tiles done, end] of the
+  // sample pass (MODE 3) and the main pass (MODE 0), VAR 8192: where the
+  // fixed costs go (dispatch spread, prologue, tiles, write-out)
+  auto clocks = [&](const char* name, auto kern, const MfArgs& args, int burst) -> int {
     for (int r = 0; r < 2; ++r) {
-      MfArgs m = c.args;
-      m.lists = out;
+      hipEventRecord(a, 0);
       for (int i = 0; i < burst; ++i)
-        hipLaunchKernelGGL((mfma_topk_kernel<768, 0, 8192, 2>), dim3(c.nwg), dim3(512), 0, 0, m);
+        hipLaunchKernelGGL(kern, dim3(c.nwg), dim3(512), 0, 0, args);
+      hipEventRecord(b, 0);
       CK(hipDeviceSynchronize());
-      std::vector<uint64_t> clk((size_t)2 * c.nwg);
+      float ms = 0;
+      hipEventElapsedTime(&ms, a, b);
+      std::vector<uint64_t> clk((size_t)4 * c.nwg);
       CK(hipMemcpy(clk.data(), out, clk.size() * 8, hipMemcpyDeviceToHost));
-      uint64_t s0 = ~0ull, e0 = ~0ull, e1 = 0;
-      double dsum = 0;
-      std::vector<double> xe(8, 0);
-      for (uint32_t i = 0; i < c.nwg; ++i) s0 = std::min(s0, clk[2 * i]);
-      for (uint32_t i = 0; i + 1 < c.nwg; ++i) {  // the last workgroup may hold fewer rows
-        e0 = std::min(e0, clk[2 * i + 1]), e1 = std::max(e1, clk[2 * i + 1]);
-        dsum += (double)(clk[2 * i + 1] - clk[2 * i]);
-        xe[i % 8] += (double)(clk[2 * i + 1] - s0);
+      uint64_t s0 = ~0ull, s1 = 0, e1 = 0;
+      double ph[3] = {0, 0, 0};
+      for (uint32_t i = 0; i < c.nwg; ++i) {
+        s0 = std::min(s0, clk[4 * i]), s1 = std::max(s1, clk[4 * i]);
+        e1 = std::max(e1, clk[4 * i + 3]);
+        for (int p = 0; p < 3; ++p) ph[p] += (double)(clk[4 * i + p + 1] - clk[4 * i + p]);
       }
-      printf("burst %d clocks: end spread %.1f us, mean dur %.1f us, last end %.1f; mean end by xcd:",
-             burst, (e1 - e0) / 100.0, dsum / (c.nwg - 1) / 100.0, (e1 - s0) / 100.0);
-      for (int x = 0; x < 8; ++x) printf(" %.0f", xe[x] / ((c.nwg - 1) / 8.0) / 100.0);
-      printf("\n");
+      printf("%s clocks (burst %d): event %.1f us/launch, start spread %.1f us, mean prologue %.1f / "
+             "tiles %.1f / write-out %.1f us, span %.1f us\n",
+             name, burst, 1e3 * ms / burst, (s1 - s0) / 100.0, ph[0] / c.nwg / 100.0,
+             ph[1] / c.nwg / 100.0, ph[2] / c.nwg / 100.0, (e1 - s0) / 100.0);
+    }
+    return 0;
+  };
+  {
+    MfArgs sa{};
+    sa.X = X, sa.Q = Q, sa.tmax = tmax;
+    sa.max_tiles = st, sa.n_rows = n, sa.rows_per_wg = rpw, sa.nq_valid = 256, sa.k = k;
+    sa.lists = out;
+    MfArgs ma = c.args;
+    ma.lists = out;
+    for (int burst : {1, 8}) {
+      if (clocks("sample", mfma_topk_kernel<768, 3, 8192, 2>, sa, burst)) return 1;
+      if (clocks("main", mfma_topk_kernel<768, 0, 8192, 2>, ma, burst)) return 1;
     }
   }
   std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
