@@ -1137,7 +1137,11 @@ struct MfShape {
 // threshold filter only (never keeps a row), 7 = 1 with one A-fragment read
 // per chunk, 10 = 1 reading only half the A fragments (the compiler then
 // merges the two row halves' MFMA chains: invalid as a timing), 11 = 1 with
-// 4-B LDS-DMA (a quarter of the bytes, same instructions). VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1;
+// 4-B LDS-DMA (a quarter of the bytes, same instructions), 13 = 1 with half
+// the A-fragment reads and every MFMA kept (r02: -5.5% against 1; a K-split
+// of query pairs that would halve the reads in the product needed 32
+// accumulator VGPRs and spilled, and its spill-free form needs a shorter
+// ring, which cost +2.4%: not kept). VAR 32 / 64: A fragments read 2 / 3 steps ahead instead of 1;
 // VAR 128: each step's reads and MFMAs pinned in program order; VAR 512:
 // the chunk's LDS-DMA pieces spread over its steps instead of at its head;
 // VAR 1024: flips the corpus stream's load policy (MODE 0 default: non-temporal
@@ -1399,7 +1403,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
         for (int p = 0; p < kPD; ++p)
 #pragma unroll
-          for (int hr = 0; hr < (MODE == 10 ? 1 : 2); ++hr) afr[p][hr] = lds_a(sb, p, hr);
+          for (int hr = 0; hr < (MODE == 10 || MODE == 13 ? 1 : 2); ++hr) afr[p][hr] = lds_a(sb, p, hr);
       }
       const bool refill = kDma && c + S::AHEAD < nchunks;
       auto sync_chunk = [&]() {
@@ -1432,7 +1436,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           if (MODE != 7 && sig + kPD < STEPS) {
             const int sp = s + kPD;
 #pragma unroll
-            for (int hr = 0; hr < (MODE == 10 ? 1 : 2); ++hr)
+            for (int hr = 0; hr < (MODE == 10 || MODE == 13 ? 1 : 2); ++hr)
               afr[(sig + kPD) % NB][hr] =
                   sp < S::CT ? lds_a(sb, sp, hr) : lds_a(sbn, sp - S::CT, hr);
           }
@@ -1455,11 +1459,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           } else {
 #pragma unroll
             for (int hr = 0; hr < 2; ++hr) {
-              const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][MODE == 10 ? 0 : hr];
+              const bf16x8_t av = afr[MODE == 7 ? 0 : sig % NB][MODE == 10 || MODE == 13 ? 0 : hr];
 #pragma unroll
-              for (int g = 0; g < G; ++g)
-                acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][u * S::CT + s],
-                                                                     acc[hr][g], 0, 0, 0);
+              for (int g = 0; g < G; ++g) {
+                // MODE 13 (ablation): half the A reads with every MFMA kept --
+                // row half 1 reuses half 0's fragment against the next step's
+                // query fragment (a distinct chain, so nothing merges)
+                const int qs = MODE == 13 && hr == 1 ? (sig + 1) % S::T : sig;
+                acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][qs], acc[hr][g], 0,
+                                                                     0, 0);
+              }
             }
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
@@ -1477,7 +1486,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       scur = snxt;
     }
     if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 7 || MODE == 10 ||
-                  MODE == 11) {
+                  MODE == 11 || MODE == 13) {
 #pragma unroll
       for (int hr = 0; hr < 2; ++hr)
 #pragma unroll

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace vsk;
@@ -157,7 +158,21 @@ int main(int argc, char** argv) {
       {"main v13", run<0, 131072 + 1024, 2>, true, {}},     // LDS counters, default policy
       {"main prio", run<0, 262144, 2>, true, {}},           // default + raised priority appends
   };
-  if (!getenv("VS_ABL_SHORT")) {
+  // VS_ABL_SET=lds: what the A-fragment LDS reads cost (no epilogue in the
+  // MODE 1 / 7 / 10 arms: all reads, hr 0 only = half the reads, one
+  // fragment set reused = almost none)
+  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "pd")) {
+    arms = {{"main bf", run<0, 0, 2>, true, {}},
+            {"PD2", run<0, 32, 2>, true, {}}};  // r02: 3.325 vs 3.340 ms, 0.426 vs 0.427 (noise)
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "lds")) {
+    arms = {{"main bf", run<0, 0, 2>, true, {}},
+            {"PD2", run<0, 32, 2>, true, {}},
+            {"no-epilogue", run<1, 0, 2>, false, {}},
+            {"half A reads (10)", run<10, 0, 2>, false, {}},
+            {"half A, all MFMA (13)", run<13, 0, 2>, false, {}},
+            {"no A reads (7)", run<7, 0, 2>, false, {}},
+            {"dma-only", run<2, 0, 2>, false, {}}};
+  } else if (!getenv("VS_ABL_SHORT")) {
     arms.push_back({"main weighted", run<0, 65536, 2>, true, {}});
     arms.push_back({"no-epilogue", run<1, 0, 2>, false, {}});
     arms.push_back({"max-only (6)", run<6, 0, 2>, true, {}});
