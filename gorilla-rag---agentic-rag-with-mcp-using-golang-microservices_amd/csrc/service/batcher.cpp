@@ -31,7 +31,8 @@ struct Batcher::Req {
 
 Batcher::Batcher(vs_engine* eng, Options opt) : eng_(eng), opt_(opt) {
   if (opt_.max_batch == 0) opt_.max_batch = 1;
-  worker_ = std::thread([this] { run(); });
+  if (opt_.workers == 0) opt_.workers = 1;
+  for (uint32_t i = 0; i < opt_.workers; ++i) workers_.emplace_back([this] { run(); });
 }
 
 Batcher::~Batcher() {
@@ -40,7 +41,7 @@ Batcher::~Batcher() {
     stop_ = true;
   }
   cv_.notify_all();
-  worker_.join();
+  for (auto& t : workers_) t.join();
 }
 
 int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint32_t k,

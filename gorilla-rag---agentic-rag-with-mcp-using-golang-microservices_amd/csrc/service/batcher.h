@@ -3,9 +3,9 @@
 //
 // rag/vector-service answers every /search with one Points.Search call for
 // one query (rag/vector-service/main.go:249-254); net/http runs the handlers
-// concurrently (main.go:77). Here concurrent handlers hand their query to one
-// worker thread per service, which coalesces whatever is queued into a few
-// vs_search(nq > 1) calls: a batch of bf16 queries then takes the MFMA path
+// concurrently (main.go:77). Here concurrent handlers hand their query to the
+// service's worker thread(s) (Options::workers), which coalesce whatever is
+// queued into a few vs_search(nq > 1) calls: a batch of bf16 queries then takes the MFMA path
 // (one pass over the corpus for up to 256 queries) instead of nq GEMV passes.
 //
 // Exactness: requests of one collection are searched together with
@@ -44,6 +44,10 @@ struct Options {
   bool enabled = true;
   uint32_t max_batch = 256;  // queries per engine call
   uint32_t max_wait_us = 0;  // linger for a non-full batch (0 = none)
+  // worker threads taking turns: with 2, the next call's batch assembly,
+  // query copy and launch wait on the engine while the current call runs,
+  // instead of following its return (and its results' hand-out)
+  uint32_t workers = 1;
 };
 
 struct Stats {
@@ -56,7 +60,7 @@ struct Stats {
 class Batcher {
  public:
   Batcher(vs_engine* eng, Options opt);
-  ~Batcher();  // drains the queue, then joins the worker
+  ~Batcher();  // drains the queue, then joins the workers
   Batcher(const Batcher&) = delete;
   Batcher& operator=(const Batcher&) = delete;
 
@@ -82,7 +86,7 @@ class Batcher {
   std::deque<Req*> queue_;
   bool stop_ = false;
   Stats stats_;
-  std::thread worker_;
+  std::vector<std::thread> workers_;
 };
 
 }  // namespace vsbatch

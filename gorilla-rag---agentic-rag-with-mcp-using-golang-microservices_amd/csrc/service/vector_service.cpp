@@ -669,7 +669,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
         return VS_ERR_INVALID_ARG;
       filter_match = fm->str == "match";
     }
-    // {"batching": {"enabled": bool, "max_batch": n, "max_wait_us": n}}
+    // {"batching": {"enabled": bool, "max_batch": n, "max_wait_us": n, "workers": n}}
     if (const Json* b = cfg.get("batching")) {
       if (b->kind != Json::Object) return VS_ERR_INVALID_ARG;
       if (const Json* e = b->get("enabled")) {
@@ -679,6 +679,10 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
       if (const Json* m = b->get("max_batch")) {
         if (m->kind != Json::Number || m->num < 1 || m->num > 4096) return VS_ERR_INVALID_ARG;
         bopt.max_batch = (uint32_t)m->num;
+      }
+      if (const Json* nw = b->get("workers")) {
+        if (nw->kind != Json::Number || nw->num < 1 || nw->num > 8) return VS_ERR_INVALID_ARG;
+        bopt.workers = (uint32_t)nw->num;
       }
       if (const Json* w = b->get("max_wait_us")) {
         if (w->kind != Json::Number || w->num < 0 || w->num > 1e6) return VS_ERR_INVALID_ARG;
@@ -899,6 +903,7 @@ int vsvc_stats(vsvc* svc, char** out) {
   b.obj.emplace_back("enabled", Json::boolean(svc->batcher != nullptr));
   b.obj.emplace_back("max_batch", Json::number(svc->batch_opt.max_batch));
   b.obj.emplace_back("max_wait_us", Json::number(svc->batch_opt.max_wait_us));
+  b.obj.emplace_back("workers", Json::number(svc->batch_opt.workers));
   o.obj.emplace_back("batching", std::move(b));
   o.obj.emplace_back("requests", Json::number((double)st.requests));
   o.obj.emplace_back("engine_calls", Json::number((double)st.engine_calls));

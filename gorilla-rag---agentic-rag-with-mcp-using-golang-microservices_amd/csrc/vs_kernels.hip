@@ -408,7 +408,7 @@ constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 // non-temporal loads: 75.5% -> 81-86% of 8 TB/s on 10M x 768 bf16 and
 // 1M x 768 fp32 (tools/ablate_gemv.hip). VAR 2 (DPP wave
 // sum) measured within noise of the shuffle sum.
-constexpr int kGemvVar = 1;
+constexpr int kGemvVar = 1 | 8;  // non-temporal loads, interleaved wave steps
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // Payload filter pre-mask: bit r of allow[] (local row r)
@@ -452,15 +452,18 @@ __device__ __forceinline__ float chunk_dot(const uint4& c, const float* qv) {
   }
 }
 
-// After the scan each wave holds its list; KPL == 1 lists are merged across
-// the workgroup in LDS (one list per workgroup), larger ones are written per
-// wave.
+// After the scan each wave holds its list; KPL <= 2 lists (k <= 128) are
+// merged across the workgroup in LDS (one list per workgroup), larger ones
+// are written per wave. r02: at k = 100 the per-wave lists (8 per workgroup,
+// 6144 per scan) made the merge kernel's work 8x larger than the scan's own
+// merge here: 0.9 ms of a 3.2 ms single-query step at 10M rows.
 template <int KPL>
 __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint32_t k,
                                           int lane, int w, uint64_t* __restrict__ out) {
-  if constexpr (KPL == 1) {
-    __shared__ uint64_t sm[kGemvWaves][64];
-    sm[w][lane] = L.e[0];
+  if constexpr (KPL <= 2) {
+    __shared__ uint64_t sm[kGemvWaves][64 * KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) sm[w][i * 64 + lane] = L.e[i];
     __syncthreads();
     if (w == 0) {
       for (int ow = 1; ow < kGemvWaves; ++ow) {
@@ -471,7 +474,11 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
           theta = L.kth(k);
         }
       }
-      if ((uint32_t)lane < k) out[(size_t)blockIdx.x * k + lane] = L.e[0];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const uint32_t idx = (uint32_t)(i * 64 + lane);
+        if (idx < k) out[(size_t)blockIdx.x * k + idx] = L.e[i];
+      }
     }
   } else {
     const size_t li = (size_t)blockIdx.x * kGemvWaves + w;
@@ -499,9 +506,18 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
-  const uint64_t lo64 = gw * rows_per_wave;
+  // VAR 8: waves interleave their RB-row steps over the whole range (wave gw
+  // reads steps gw, gw + waves, ...) instead of each streaming a contiguous
+  // slice: all waves then work inside a few MB of the corpus at a time, so
+  // the address translations they need stay cached (6144 slices of a 154 GB
+  // corpus ran at 79% of HBM peak against 84% for 15 GB).
+  constexpr bool kIlv = (VAR & 8) != 0;
+  const uint32_t nw = gridDim.x * kGemvWaves;
+  const uint32_t stride = kIlv ? nw * S::RB : S::RB;
+  const uint64_t lo64 = kIlv ? gw * S::RB : gw * rows_per_wave;
   const uint32_t lo = lo64 < n_rows ? (uint32_t)lo64 : n_rows;
-  const uint32_t hi = (uint64_t)lo + rows_per_wave < n_rows ? lo + rows_per_wave : n_rows;
+  const uint32_t hi = kIlv ? n_rows
+                           : ((uint64_t)lo + rows_per_wave < n_rows ? lo + rows_per_wave : n_rows);
 
   int rowsel[S::J];
   int coff[S::J];  // chunk index within its row
@@ -553,15 +569,15 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     };
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
-      const uint32_t r0 = lo + d * S::RB;
+      const uint32_t r0 = lo + d * stride;
       if constexpr (GATHER) fetch_ix(r0 < hi ? r0 : lo);
       load(buf[d], r0 < hi ? r0 : lo);
     }
-    if constexpr (GATHER) fetch_ix(lo + DEPTH * S::RB);
-    for (uint32_t r = lo; r < hi; r += S::RB) {
-      const uint32_t rn = r + DEPTH * S::RB;
+    if constexpr (GATHER) fetch_ix(lo + DEPTH * stride);
+    for (uint32_t r = lo; r < hi; r += stride) {
+      const uint32_t rn = r + DEPTH * stride;
       load(buf[DEPTH], rn < hi ? rn : r);
-      if constexpr (GATHER) fetch_ix(rn + S::RB);
+      if constexpr (GATHER) fetch_ix(rn + stride);
       float p[S::RB];
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) p[b] = 0.f;
@@ -672,7 +688,7 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k) {
   (void)bf16;
   GemvGrid g = gemv_grid(n_rows, 1);
   // rb > 1 only lowers the workgroup count; rb == 1 is the upper bound.
-  const uint32_t per = gemv_kpl(k) == 1 ? 1 : kGemvWaves;
+  const uint32_t per = gemv_kpl(k) <= 2 ? 1 : kGemvWaves;
   return g.nwg * per;
 }
 
@@ -700,7 +716,7 @@ static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row
   using S = GemvShape<D, BF16>;
   GemvGrid g = gemv_grid(n_rows, S::RB);
   const int kpl = gemv_kpl(k);
-  const uint32_t lists = g.nwg * (kpl == 1 ? 1 : kGemvWaves);
+  const uint32_t lists = g.nwg * (kpl <= 2 ? 1 : kGemvWaves);
   if (lists > max_lists) return hipErrorInvalidValue;
   *nlists = lists;
   dim3 grid(g.nwg), block(kGemvThreads);
@@ -736,7 +752,7 @@ static hipError_t gemv_generic(const void* X, uint32_t dim, uint32_t n_rows,
                                hipStream_t st, const uint32_t* rows) {
   GemvGrid g = gemv_grid(n_rows, 1);
   const int kpl = gemv_kpl(k);
-  const uint32_t lists = g.nwg * (kpl == 1 ? 1 : kGemvWaves);
+  const uint32_t lists = g.nwg * (kpl <= 2 ? 1 : kGemvWaves);
   if (lists > max_lists) return hipErrorInvalidValue;
   *nlists = lists;
   dim3 grid(g.nwg), block(kGemvThreads);
@@ -1825,12 +1841,15 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
 }
 
 uint32_t mfma_sample_tiles(uint32_t n_rows) {
-  // 1/64 of every workgroup's tiles, at least 4 when it has 64 or more: with
+  // 1/128 of every workgroup's tiles, at least 4 when it has 64 or more: with
   // the slab select, whose cost grows with the survivors, 4 instead of 2
-  // tiles at 1.25M rows (the N = 8 share) saved 2-3 us per batch (r01; the
-  // key-based select of earlier builds gained nothing from it).
+  // tiles at 1.25M rows (the N = 8 share) saved 2-3 us per batch (r01). With
+  // tile maxima stored as floats (r02) the sample pass costs ~5 us per tile
+  // and the select ~1.4 us per 100 survivors per query: at 10M rows 1/128
+  // (9 tiles: 61 + 24 us) beats 1/64 (19 tiles: 110 + 16 us;
+  // profiles/r02_sample_tiles_10m.txt).
   const uint32_t tpw = mfma_tiles_per_wg(n_rows);
-  uint32_t st = tpw / 64;
+  uint32_t st = tpw / 128;
   if (tpw >= 64 && st < 4) st = 4;
   if (st < 1) st = 1;
   if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;

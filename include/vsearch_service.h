@@ -36,7 +36,7 @@ typedef struct vsvc vsvc;
  * regulatory_docs, merchant_docs, kyc_docs, dim 768, Cosine, fp32) or
  * {"collections":[{"name":"..","dim":768,"metric":"Cosine"|"Dot",
  *  "dtype":"f32"|"bf16"}...],
- *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0},
+ *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0,"workers":1},
  *  "filter":"ignore"|"match"}.
  * "filter":"ignore" (default) keeps the reference's behaviour: the request's
  * `filter` is decoded and dropped (main.go:30 vs :249-254). "match" applies

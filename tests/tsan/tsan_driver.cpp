@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
   const char* cfg =
       "{\"collections\":[{\"name\":\"a\",\"dim\":16},{\"name\":\"b\",\"dim\":16,"
       "\"metric\":\"Dot\"}],\"batching\":{\"enabled\":true,\"max_batch\":16,"
-      "\"max_wait_us\":200},\"filter\":\"match\"}";
+      "\"max_wait_us\":200,\"workers\":2},\"filter\":\"match\"}";
   vsvc* svc = nullptr;
   if (vsvc_open(eng, cfg, &svc) != VS_OK) return 3;
   if (vsvc_bulk_generate(svc, "b", 500, 7) != VS_OK) return 4;

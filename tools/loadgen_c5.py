@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--clients", default="16,64,256")
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--unbatched-clients", type=int, default=64)
+    ap.add_argument("--workers", type=int, default=1, help="batcher worker threads")
     args = ap.parse_args()
     import torch  # noqa: F401  (binds torch's HIP runtime first, as bench.py does)
     import __graft_entry__ as ge
@@ -42,7 +43,8 @@ def main():
             continue
         eng = pkg.VectorEngine(device=0)
         svc = svcmod.VectorService(eng, {"collections": colls,
-                                         "batching": {"enabled": batching}})
+                                         "batching": {"enabled": batching,
+                                                      "workers": args.workers}})
         t0 = time.time()
         for i, n in enumerate(names):
             svc.bulk_generate(n, args.rows, 0x5EED + i)
@@ -58,7 +60,8 @@ def main():
             nreq = st["requests"] - before["requests"]
             line = {"workload": f"C5: 3 x {args.rows} x {args.dim} bf16, k in [3,50], "
                                 "closed loop, in-process clients",
-                    "clients": clients, "batching": batching, "qps": round(rep["qps"], 1),
+                    "clients": clients, "batching": batching, "workers": args.workers,
+                    "qps": round(rep["qps"], 1),
                     "requests": rep["requests"], "errors": rep["errors"],
                     "first_error": rep["first_error"][:200],
                     "lat_ms": {k: round(v, 3) for k, v in rep["lat_ms"].items()},
