@@ -1736,11 +1736,20 @@ uint32_t mfma_tiles_per_wg(uint32_t n_rows) {
   return (rpw + 31) / 32;
 }
 
+// bf16 rows of D = 768 stream in 24 KiB K-chunks (two per 32-row tile, so
+// two barriers per tile instead of three) through a 144 KiB ring (5 chunks in
+// flight): -0.75% / -1.7% main pass at 10M / 1.25M rows back to back
+// (profiles/r02_ablation_chunk_*.txt; VAR 2048 + 256 in the ablation set).
+template <int MODE, int D, bool F32>
+constexpr int mf_product_var() {
+  return (!F32 && D == 768 && (MODE == 0 || MODE == 3)) ? 2048 + 256 : 0;
+}
+
 template <int MODE, int D, bool F32>
 static void mfma_launch_d(uint32_t nwg, const MfArgs& a, hipStream_t st) {
   constexpr int G = mf_groups_b(D * (F32 ? 4 : 2));
-  hipLaunchKernelGGL((mfma_topk_kernel<D, MODE, 0, G, F32>), dim3(nwg), dim3(64 * mf_waves(G)),
-                     0, st, a);
+  hipLaunchKernelGGL((mfma_topk_kernel<D, MODE, mf_product_var<MODE, D, F32>(), G, F32>),
+                     dim3(nwg), dim3(64 * mf_waves(G)), 0, st, a);
 }
 
 template <int MODE>

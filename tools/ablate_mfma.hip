@@ -145,7 +145,8 @@ int main(int argc, char** argv) {
   }
   c.wgt = wgt;
   std::vector<Arm> arms = {
-      {"main bf", run<0, 0, 2>, true, {}},                  // default: branch-free stream
+      {"main (product)", run<0, 2048 + 256, 2>, true, {}},  // 24 KiB chunks, 144 KiB ring
+      {"main bf 16k", run<0, 0, 2>, true, {}},              // r02 build before: 16 KiB chunks
       {"main branchy", run<0, 524288, 2>, true, {}},        // r01 conditional stream
       {"bf no-replace", run<0, 2097152, 2>, true, {}},      // full quarter drops (inexact)
       {"bf no-max", run<0, 2097152 + 4194304, 2>, true, {}},  // + no slab max store (r02a)
@@ -161,7 +162,12 @@ int main(int argc, char** argv) {
   // VS_ABL_SET=lds: what the A-fragment LDS reads cost (no epilogue in the
   // MODE 1 / 7 / 10 arms: all reads, hr 0 only = half the reads, one
   // fragment set reused = almost none)
-  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "pd")) {
+  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "chunk")) {
+    arms = {{"main bf", run<0, 0, 2>, true, {}},
+            {"24k ring144", run<0, 2048 + 256, 2>, true, {}},
+            {"24k ring112", run<0, 2048, 2>, true, {}},
+            {"ring144", run<0, 256, 2>, true, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "pd")) {
     arms = {{"main bf", run<0, 0, 2>, true, {}},
             {"PD2", run<0, 32, 2>, true, {}}};  // r02: 3.325 vs 3.340 ms, 0.426 vs 0.427 (noise)
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "lds")) {
