@@ -165,7 +165,7 @@ int main(int argc, char** argv) {
   if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "chunk")) {
     arms = {{"main bf", run<0, 0, 2>, true, {}},
             {"24k ring144", run<0, 2048 + 256, 2>, true, {}},
-            {"24k ring112", run<0, 2048, 2>, true, {}},
+            {"48k ring144", run<0, 4096 + 256, 2>, true, {}},
             {"ring144", run<0, 256, 2>, true, {}}};
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "pd")) {
     arms = {{"main bf", run<0, 0, 2>, true, {}},
