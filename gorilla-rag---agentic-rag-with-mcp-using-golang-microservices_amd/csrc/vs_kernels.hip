@@ -1433,7 +1433,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           else
             wait_vmcnt<0>();
         }
-        if constexpr (MODE != 5) __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
+        // VAR 134217728 (timing ablation only: the ring is then unsynchronised
+        // and the results garbage): no barrier at all
+        if constexpr (MODE != 5 && (VAR & 134217728) == 0)
+          __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (kDma && kBF)
           issue_next_bf(refill);

@@ -162,7 +162,15 @@ int main(int argc, char** argv) {
   // VS_ABL_SET=lds: what the A-fragment LDS reads cost (no epilogue in the
   // MODE 1 / 7 / 10 arms: all reads, hr 0 only = half the reads, one
   // fragment set reused = almost none)
-  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "chunk")) {
+  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "barrier")) {
+    // timing only: without the barrier the ring is unsynchronised (wrong
+    // results, no hazard to the device: no waits depend on the data)
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
+            {"no-epi (product)", run<1, 2048 + 256, 2>, false, {}},
+            {"no-epi no-barrier", run<1, 2048 + 256 + 134217728, 2>, false, {}},
+            {"no-epi 16k", run<1, 0, 2>, false, {}},
+            {"no-epi 16k no-barrier", run<1, 134217728, 2>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "chunk")) {
     arms = {{"main bf", run<0, 0, 2>, true, {}},
             {"24k ring144", run<0, 2048 + 256, 2>, true, {}},
             {"48k ring144", run<0, 4096 + 256, 2>, true, {}},
