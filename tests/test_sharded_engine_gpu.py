@@ -272,3 +272,61 @@ def test_c4_100m_eight_shards(pkg, orc):
         _check(orc, s1, r1, c1, s64[:1], rr[:1], cc[:1], resc1)
     finally:
         eng.close()
+
+
+def test_sharded_concurrent_calls(sharded, orc):
+    """Many host threads on one sharded engine at once (ctypes releases the
+    GIL): searches of two collections at nq 1 / 5 / 64 (GEMV and MFMA paths,
+    each shard's scratch and the RCCL all-gather shared), while a third
+    collection is appended to and searched. Every answer must equal the one
+    computed before the threads started."""
+    import threading
+    dim, n = 256, 200_003
+    names = ["cc0", "cc1"]
+    for i, nm in enumerate(names):
+        sharded.create_collection(nm, dim, 1, 1, n)
+        sharded.generate(nm, n, orc.SEED_CORPUS + i)
+    sharded.create_collection("cc_up", dim, 0, 0)
+    try:
+        Q = orc.generate(orc.SEED_QUERY, 77, 64, dim)
+        want = {}
+        for nm in names:
+            for nq in (1, 5, 64):
+                want[(nm, nq)] = sharded.search(nm, Q[:nq], 10)
+        errors = []
+
+        def searcher(t):
+            try:
+                for it in range(6):
+                    nm = names[(t + it) % 2]
+                    nq = (1, 5, 64)[(t + it) % 3]
+                    s, r, c = sharded.search(nm, Q[:nq], 10)
+                    ws, wr, wc = want[(nm, nq)]
+                    if not (np.array_equal(r, wr) and np.array_equal(s, ws)):
+                        errors.append((t, it, nm, nq))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        def upserter():
+            try:
+                base = orc.generate(5, 0, 4000, dim)
+                for j in range(4):
+                    rows = np.arange(j * 1000, (j + 1) * 1000)
+                    sharded.upsert("cc_up", rows, base[j * 1000:(j + 1) * 1000])
+                    s, r, c = sharded.search("cc_up", base[j * 1000:j * 1000 + 3], 1)
+                    if r[:, 0].tolist() != [j * 1000, j * 1000 + 1, j * 1000 + 2]:
+                        errors.append(("upsert", j, r[:, 0].tolist()))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=searcher, args=(t,)) for t in range(6)]
+        th.append(threading.Thread(target=upserter))
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors[:5]
+        assert sharded.collection_info("cc_up")["rows"] == 4000
+    finally:
+        for nm in names + ["cc_up"]:
+            sharded.drop_collection(nm)
