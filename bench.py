@@ -249,7 +249,10 @@ def main():
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist_on = world > 1
+    # VS_BENCH_FORCE_DIST=1 (tests): the process group and the all-gather run
+    # even with one rank, so the RCCL path is exercised on a one-GPU box
+    force_dist = os.environ.get("VS_BENCH_FORCE_DIST") == "1"
+    dist_on = world > 1 or force_dist
     if dist_on:
         import torch.distributed as dist
         if backend == "gloo":
@@ -281,7 +284,7 @@ def main():
 
     stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True)
-    sharded = shard.ShardedSearch(ls, mg)
+    sharded = shard.ShardedSearch(ls, mg, always_gather=force_dist)
 
     el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
                             stream_fn, 0)

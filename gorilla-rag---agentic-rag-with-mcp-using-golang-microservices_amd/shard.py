@@ -39,6 +39,8 @@ class ShardedSearch:
     local_search: Callable
     merge: Callable
     group: Optional[object] = None
+    # gather even with one rank (tests: the collective path on a one-GPU box)
+    always_gather: bool = False
     _gather_bufs: Optional[dict] = None  # all-gather outputs, reused per shape
 
     def search(self, queries, k: int):
@@ -46,7 +48,9 @@ class ShardedSearch:
         import torch.distributed as dist
 
         local = self.local_search(queries, k)
-        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        if not dist.is_available() or not dist.is_initialized():
+            return local
+        if dist.get_world_size(self.group) == 1 and not self.always_gather:
             return local
         P = dist.get_world_size(self.group)
         local = local.contiguous()
