@@ -285,6 +285,18 @@ def main():
     stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True)
     sharded = shard.ShardedSearch(ls, mg, always_gather=force_dist)
+    # the data-path exchange: the engine's own RCCL communicator (all-gather +
+    # merge on the search's stream) unless VS_COLLECTIVE=torch; gloo runs
+    # (tests) always use torch.distributed
+    collective = None
+    if dist_on:
+        collective = "gloo" if backend == "gloo" else os.environ.get("VS_COLLECTIVE", "engine")
+        if collective == "engine":
+            uid = [pkg.VectorEngine.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            eng.comm_init(world, rank, uid[0])
+            sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True)
+            sharded.world_size = world
 
     el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
                             stream_fn, 0)
@@ -311,7 +323,7 @@ def main():
         "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
-                   "rows_per_gpu": hi - lo},
+                   "rows_per_gpu": hi - lo, "collective": collective},
         "roofline": roof,
     }
 

@@ -86,6 +86,11 @@ struct vs_engine {
     hipEvent_t qev = nullptr;  // dev 0: the caller's queries are ready
   };
   std::vector<Scratch> scr;
+  // one process per GPU (vs_comm_init): the ranks' communicator and the
+  // all-gather output of vs_gather_merge_keys (guarded by dev[0]->work_mu)
+  ncclComm_t pcomm = nullptr;
+  uint32_t pranks = 0, prank = 0;
+  DevBuf pgather;
   uint32_t shards() const { return (uint32_t)shard_dev.size(); }
 };
 
@@ -647,6 +652,12 @@ void destroy(vs_engine* E) {
     }
     if (d < E->comm.size() && E->comm[d]) (void)ncclCommDestroy(E->comm[d]);
   }
+  if (!E->dev.empty() && E->dev[0]) {
+    (void)hipSetDevice(E->dev[0]->device);
+    (void)hipStreamSynchronize(E->dev[0]->stream);
+    E->pgather.release();
+    if (E->pcomm) (void)ncclCommDestroy(E->pcomm);
+  }
   E->colls.clear();
   for (DevEngine* d : E->dev) vsd::close(d);
   delete E;
@@ -884,6 +895,65 @@ int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uin
                   uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   return vsd::merge_keys(eng->dev[0], d_lists, n_lists, nq, k_in, k, d_out_keys, stream);
+}
+
+int vs_comm_unique_id(unsigned char id[VS_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == VS_COMM_ID_BYTES, "RCCL unique id size");
+  if (!id) return fail(VS_ERR_INVALID_ARG, "id is NULL");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+  std::memcpy(id, &u, sizeof(u));
+  return VS_OK;
+}
+
+int vs_comm_init(vs_engine* eng, uint32_t n_ranks, uint32_t rank,
+                 const unsigned char id[VS_COMM_ID_BYTES]) {
+  if (!eng || !id) return fail(VS_ERR_INVALID_ARG, "engine and id are required");
+  if (eng->sharded)
+    return fail(VS_ERR_INVALID_ARG, "a vs_open_multi engine holds its own communicator");
+  if (n_ranks == 0 || rank >= n_ranks) return fail(VS_ERR_INVALID_ARG, "rank out of range");
+  DevEngine* d0 = eng->dev[0];
+  std::lock_guard<std::mutex> g(d0->work_mu);
+  if (eng->pcomm) return fail(VS_ERR_EXISTS, "vs_comm_init was called already");
+  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, (int)n_ranks, u, (int)rank);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclCommInitRank");
+  eng->pcomm = c;
+  eng->pranks = n_ranks;
+  eng->prank = rank;
+  return VS_OK;
+}
+
+int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, uint32_t k_in,
+                         uint32_t k, uint64_t* d_out_keys, void* stream) {
+  if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (!eng->pcomm) return fail(VS_ERR_INVALID_ARG, "vs_comm_init has not been called");
+  if (k == 0 || k > vsk::kMaxK || k_in == 0 || k_in > vsk::kMaxK)
+    return fail(VS_ERR_INVALID_ARG, "bad merge shape");
+  if (nq == 0) return VS_OK;
+  if (!d_local || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
+  DevEngine* d0 = eng->dev[0];
+  std::lock_guard<std::mutex> g(d0->work_mu);
+  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+  hipStream_t cs = (hipStream_t)stream;
+  // the gather buffer is reused: order this call after the last one that read it
+  VS_HIP(vsd::use_stream(d0, cs), "stream order");
+  const size_t lbytes = (size_t)nq * k_in * 8;
+  if (eng->pgather.bytes < lbytes * eng->pranks) {
+    VS_HIP(hipStreamSynchronize(cs), "sync");
+    VS_HIP(eng->pgather.ensure(lbytes * eng->pranks), "alloc gathered keys");
+  }
+  const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
+                                       eng->pcomm, cs);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
+  VS_HIP(vsk::launch_merge(eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in, nq,
+                           k_in, k, d_out_keys, cs),
+         "rank merge");
+  return VS_OK;
 }
 
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,

@@ -46,8 +46,9 @@ EXPORTS = (
     "vs_decode_keys", "vs_health", "vs_last_error", "vs_timing",
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
     "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
-    "vs_engine_layout",
+    "vs_engine_layout", "vs_comm_unique_id", "vs_comm_init", "vs_gather_merge_keys",
 )
+COMM_ID_BYTES = 128
 
 
 class VSError(RuntimeError):
@@ -96,6 +97,9 @@ def load_library(path: str = LIB_PATH):
         "vs_search": ([vp, cp, vp, u32, u32, u32, vp, vp, vp], i32),
         "vs_search_keys": ([vp, cp, vp, u32, u32, u32, vp, vp], i32),
         "vs_merge_keys": ([vp, vp, u32, u32, u32, u32, vp, vp], i32),
+        "vs_comm_unique_id": ([vp], i32),
+        "vs_comm_init": ([vp, u32, u32, vp], i32),
+        "vs_gather_merge_keys": ([vp, vp, u32, u32, u32, vp, vp], i32),
         "vs_decode_keys": ([vp, vp, u32, u32, vp, vp, vp, vp], i32),
         "vs_health": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "vs_last_error": ([], ctypes.c_char_p),
@@ -326,6 +330,27 @@ class VectorEngine:
                    d_out: int, stream: int = 0):
         _check(self._L.vs_merge_keys(self._h, ctypes.c_void_p(d_lists), n_lists, nq, k_in, k,
                                      ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
+
+    # one process per GPU (include/vsearch.h "one process per GPU") -------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """A fresh RCCL unique id (made on one rank, handed to all)."""
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        _check(load_library().vs_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, n_ranks: int, rank: int, uid: bytes):
+        """Joins the ranks' communicator (collective: every rank calls it)."""
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"the unique id is {COMM_ID_BYTES} bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _check(self._L.vs_comm_init(self._h, n_ranks, rank, buf))
+
+    def gather_merge_keys(self, d_local: int, nq: int, k_in: int, k: int, d_out: int,
+                          stream: int = 0):
+        """All-gather of every rank's [nq][k_in] keys + merge to [nq][k], on `stream`."""
+        _check(self._L.vs_gather_merge_keys(self._h, ctypes.c_void_p(d_local), nq, k_in, k,
+                                            ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
 
     def decode_keys(self, d_keys: int, nq: int, k: int, stream: int = 0):
         scores = np.zeros((nq, k), np.float32)

@@ -4,10 +4,16 @@ A collection of N rows is cut into contiguous shards: rank p of P owns global
 rows [p*ceil(N/P), min(N, (p+1)*ceil(N/P))). Every rank scans its shard for the
 whole query batch and produces a local top-k key list per query (64-bit keys
 that carry the global row, include/vsearch.h "Result key layout"). The only
-exchange is an all-gather of those lists (RCCL over xGMI via
-``torch.distributed``'s nccl backend); each rank then merges the P lists on its
-own device (vs_merge_keys). Messages are tiny (P x B x k x 8 bytes), so the
-step is latency-bound, not link-bandwidth-bound.
+exchange is an all-gather of those lists over RCCL / xGMI; each rank then
+merges the P lists on its own device. Messages are tiny (P x B x k x 8 bytes),
+so the step is latency-bound, not link-bandwidth-bound. Two forms:
+
+* ``gather_merge`` given (the product on GPUs): the engine's own communicator
+  (vs_comm_init) runs the all-gather and the merge back to back on the
+  search's stream (vs_gather_merge_keys), with no cross-stream wait;
+* otherwise ``torch.distributed``'s all-gather (the nccl backend runs it on
+  its internal stream, which the caller's stream then waits for) and
+  vs_merge_keys; the gloo tests use this form.
 
 The orchestration below is written against two callables so the CPU tests can
 drive it with gloo and the oracle; the product passes the HIP engine.
@@ -41,6 +47,10 @@ class ShardedSearch:
     group: Optional[object] = None
     # gather even with one rank (tests: the collective path on a one-GPU box)
     always_gather: bool = False
+    # gather_merge(local [nq, k], k) -> keys [nq, k]: the engine's all-gather +
+    # merge (engine_gather_merge); replaces the torch all-gather and `merge`
+    gather_merge: Optional[Callable] = None
+    world_size: int = 1  # ranks of gather_merge's communicator
     _gather_bufs: Optional[dict] = None  # all-gather outputs, reused per shape
 
     def search(self, queries, k: int):
@@ -48,6 +58,10 @@ class ShardedSearch:
         import torch.distributed as dist
 
         local = self.local_search(queries, k)
+        if self.gather_merge is not None:
+            if self.world_size == 1 and not self.always_gather:
+                return local
+            return self.gather_merge(local, k)
         if not dist.is_available() or not dist.is_initialized():
             return local
         if dist.get_world_size(self.group) == 1 and not self.always_gather:
@@ -107,3 +121,26 @@ def engine_callables(engine, collection: str, dim: int, stream_fn: Callable[[], 
         return out
 
     return local_search, merge
+
+
+def engine_gather_merge(engine, stream_fn: Callable[[], int], reuse: bool = False):
+    """ShardedSearch.gather_merge over the engine's communicator (the caller
+    ran engine.comm_init on every rank): vs_gather_merge_keys on the search's
+    stream."""
+    import torch
+
+    cache = {}
+
+    def gather_merge(local, k):
+        local = local.contiguous()
+        nq, kin = local.shape
+        key = (nq, k, str(local.device))
+        out = cache.get(key) if reuse else None
+        if out is None:
+            out = torch.empty((nq, k), dtype=torch.int64, device=local.device)
+            if reuse:
+                cache[key] = out
+        engine.gather_merge_keys(local.data_ptr(), nq, kin, k, out.data_ptr(), stream_fn())
+        return out
+
+    return gather_merge

@@ -230,6 +230,30 @@ int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists,
                   uint32_t nq, uint32_t k_in, uint32_t k, uint64_t* d_out_keys,
                   void* stream);
 
+/* ---- one process per GPU (row shards across processes) --------------------
+ *
+ * Each process opens its own single-device engine (vs_open) over its shard
+ * of rows (vs_collection_create with row_base = the shard's first global
+ * row). One rank makes an RCCL unique id; every rank receives those bytes
+ * over any host transport (the launcher's store, a socket, an env var) and
+ * calls vs_comm_init with the same id, its rank and the rank count (a
+ * collective call: it returns once all ranks joined). vs_gather_merge_keys
+ * then turns each rank's vs_search_keys output into the global top-k on
+ * every rank: ONE RCCL all-gather of the ranks' [nq][k_in] lists over xGMI
+ * and the vs_merge_keys merge, both on `stream`, with nothing between them
+ * (no event or cross-stream wait; every rank must make the same sequence of
+ * calls with the same nq / k_in / k). Replaces a framework all-gather +
+ * vs_merge_keys pair (the form shard.py uses with gloo). Not available on a
+ * vs_open_multi engine, which holds its own communicator. */
+#define VS_COMM_ID_BYTES 128
+int vs_comm_unique_id(unsigned char id[VS_COMM_ID_BYTES]);
+int vs_comm_init(vs_engine* eng, uint32_t n_ranks, uint32_t rank,
+                 const unsigned char id[VS_COMM_ID_BYTES]);
+/* d_local [nq][k_in] and d_out_keys [nq][k] on this engine's device. */
+int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq,
+                         uint32_t k_in, uint32_t k, uint64_t* d_out_keys,
+                         void* stream);
+
 /* Decodes device keys into host scores/rows/counts (blocking D2H). */
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq,
                    uint32_t k, float* out_scores, uint64_t* out_rows,

@@ -52,23 +52,27 @@ def test_two_ranks_equal_one_rank(tmp_path, config, rows):
 
 
 @pytest.mark.gpu
-def test_rccl_one_rank_gather_equals_plain(tmp_path):
+@pytest.mark.parametrize("collective", ["engine", "torch"])
+def test_rccl_one_rank_gather_equals_plain(tmp_path, collective):
     """The driver's N>1 runs initialise RCCL and all-gather every step; a
     one-GPU box cannot host two RCCL ranks, so this forces the process group,
     the barrier / MAX all-reduce of the timing and the all-gather + on-device
     merge at world size 1 (VS_BENCH_FORCE_DIST) under torch.distributed.run
-    with the nccl backend, and checks the keys against the plain run."""
+    with the nccl backend, and checks the keys against the plain run. Both
+    exchanges: the engine's communicator (vs_gather_merge_keys, the default)
+    and torch.distributed's all-gather + vs_merge_keys."""
     extra = ["--config", "c3", "--rows", "200000"]
     r1, k1 = _bench(tmp_path, "plain", 1, extra)
-    out = str(tmp_path / "rccl.npy")
+    out = str(tmp_path / f"rccl_{collective}.npy")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-secondary",
            "--dump-keys", out] + extra
     env = dict(os.environ, VS_DIST_BACKEND="nccl", VS_BENCH_FORCE_DIST="1",
-               MASTER_ADDR="127.0.0.1")
+               VS_COLLECTIVE=collective, MASTER_ADDR="127.0.0.1")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     r2 = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert r2["n_gpus"] == 1 and r2["config"]["rows_per_gpu"] == 200_000
+    assert r2["config"]["collective"] == collective
     np.testing.assert_array_equal(k1, np.load(out))
