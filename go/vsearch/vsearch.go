@@ -310,3 +310,31 @@ func (e *Engine) Health() (string, error) {
 	err := check(C.vs_health(e.h, buf, 4096))
 	return C.GoString(buf), err
 }
+
+// CommUniqueID makes the RCCL id of a one-process-per-GPU deployment: call it
+// on one rank and hand the bytes to every rank (any host transport).
+func CommUniqueID() ([]byte, error) {
+	id := make([]byte, C.VS_COMM_ID_BYTES)
+	err := check(C.vs_comm_unique_id((*C.uchar)(unsafe.Pointer(&id[0]))))
+	return id, err
+}
+
+// CommInit joins this engine (one GPU, one row shard opened with a row_base)
+// to the ranks' communicator; every rank calls it with the same id.
+func (e *Engine) CommInit(nRanks, rank int, id []byte) error {
+	if len(id) != int(C.VS_COMM_ID_BYTES) {
+		return fmt.Errorf("vsearch: comm id must be %d bytes: %w", int(C.VS_COMM_ID_BYTES), ErrInvalidArg)
+	}
+	return check(C.vs_comm_init(e.h, C.uint32_t(nRanks), C.uint32_t(rank),
+		(*C.uchar)(unsafe.Pointer(&id[0]))))
+}
+
+// GatherMergeKeys exchanges every rank's [nq][kIn] device keys (the output of
+// vs_search_keys) with one RCCL all-gather and merges them into the global
+// [nq][k] keys, both on `stream` (a hipStream_t; nil = the null stream).
+// dLocal and dOut are device pointers, which cgo passes as plain addresses.
+func (e *Engine) GatherMergeKeys(dLocal, dOut unsafe.Pointer, nq, kIn, k uint32,
+	stream unsafe.Pointer) error {
+	return check(C.vs_gather_merge_keys(e.h, (*C.uint64_t)(dLocal), C.uint32_t(nq),
+		C.uint32_t(kIn), C.uint32_t(k), (*C.uint64_t)(dOut), stream))
+}
