@@ -47,6 +47,10 @@ CONFIGS = {
     "c2b256": (1_000_000, 768, "f32", "cosine", 256, 10,
                "C2 corpus batched: {rows} x 768 fp32, 256-query batches, exact top-10, cosine "
                "(f32 MFMA)"),
+    # one C5 collection's scan at a full batch (C5 itself is a service load:
+    # tools/loadgen_c5.py); 1024-d rows: 128 queries per MFMA launch
+    "c5b256": (5_000_000, 1024, "bf16", "cosine", 256, 50,
+               "C5 collection: {rows} x 1024 bf16, 256-query batches, exact top-50, cosine"),
     # C4 is quoted on 8 GPUs (12.5M rows each); on fewer GPUs each holds more
     # (100M x 768 bf16 = 153.6 GB fits one MI355X's 288 GB)
     "c4": (100_000_000, 768, "bf16", "dot", 256, 100,
