@@ -24,7 +24,7 @@ def _keys(scores, rows):
     return (o << np.uint64(32)) | (np.uint64(0xFFFFFFFF) - rows.astype(np.uint64))
 
 
-def _worker(rank, world, port, n, dim, nq, k, q):
+def _worker(rank, world, port, n, dim, nq, k, q, form="torch"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -47,7 +47,22 @@ def _worker(rank, world, port, n, dim, nq, k, q):
         out = np.sort(np.concatenate(list(g), axis=1), axis=1)[:, ::-1][:, :kk]
         return torch.from_numpy(np.ascontiguousarray(out).view(np.int64))
 
-    ss = shard.ShardedSearch(local_search, merge)
+    if form == "torch":
+        ss = shard.ShardedSearch(local_search, merge)
+    else:
+        # the engine form's dispatch (engine_gather_merge binds
+        # vs_gather_merge_keys): one callable exchanges and merges, and the
+        # torch all-gather + `merge` pair must not run
+        def gather_merge(local, kk):
+            flat = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype)
+            dist.all_gather_into_tensor(flat, local.contiguous())
+            return merge(flat.view(world, local.shape[0], local.shape[1]), kk)
+
+        def no_merge(gathered, kk):
+            raise AssertionError("torch exchange used with gather_merge set")
+
+        ss = shard.ShardedSearch(local_search, no_merge, gather_merge=gather_merge,
+                                 world_size=world)
     res = ss.search(torch.from_numpy(Q), k).numpy().view(np.uint64)
     q.put((rank, res))
     dist.destroy_process_group()
@@ -66,13 +81,14 @@ def test_shard_ranges_cover_exactly():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_merge_equals_unsharded(orc):
+@pytest.mark.parametrize("form", ["torch", "gather_merge"])
+def test_two_rank_gloo_merge_equals_unsharded(orc, form):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     n, dim, nq, k, world = 6001, 128, 5, 10, 2
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, dim, nq, k, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, dim, nq, k, q, form)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
