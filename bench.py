@@ -296,11 +296,30 @@ def main():
     if dist_on:
         collective = "gloo" if backend == "gloo" else os.environ.get("VS_COLLECTIVE", "engine")
         if collective == "engine":
-            uid = [pkg.VectorEngine.comm_unique_id() if rank == 0 else None]
+            # every rank reaches each collective below whatever failed before
+            # it; if any rank could not join, all keep torch's exchange
+            uid = [None]
+            if rank == 0:
+                try:
+                    uid = [pkg.VectorEngine.comm_unique_id()]
+                except Exception as e:  # noqa: BLE001
+                    log(f"[bench] rank 0: no RCCL unique id ({e})")
             dist.broadcast_object_list(uid, src=0)
-            eng.comm_init(world, rank, uid[0])
-            sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True)
-            sharded.world_size = world
+            ok = 0
+            if uid[0] is not None:
+                try:
+                    eng.comm_init(world, rank, uid[0])
+                    ok = 1
+                except Exception as e:  # noqa: BLE001
+                    log(f"[bench] rank {rank}: engine communicator failed ({e})")
+            flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 1:
+                sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True)
+                sharded.world_size = world
+            else:
+                log("[bench] torch.distributed exchange instead of the engine communicator")
+                collective = "torch"
 
     el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
                             stream_fn, 0)
