@@ -47,6 +47,13 @@ CONFIGS = {
     "c2b256": (1_000_000, 768, "f32", "cosine", 256, 10,
                "C2 corpus batched: {rows} x 768 fp32, 256-query batches, exact top-10, cosine "
                "(f32 MFMA)"),
+    # the metric sweep's fp32 arm (N = 10M, D = 768, bf16 and
+    # fp32, B in {1, 256}): the reference's collection dtype at the C3 size
+    "c3f32": (10_000_000, 768, "f32", "dot", 256, 10,
+              "{rows} x 768 fp32 corpus, 256-query batches, exact top-10, inner product "
+              "(f32 MFMA)"),
+    "c3f32b1": (10_000_000, 768, "f32", "dot", 1, 10,
+                "{rows} x 768 fp32 corpus, single query, exact top-10, inner product (GEMV)"),
     # one C5 collection's scan at a full batch (C5 itself is a service load:
     # tools/loadgen_c5.py); 1024-d rows: 128 queries per MFMA launch
     "c5b256": (5_000_000, 1024, "bf16", "cosine", 256, 50,
