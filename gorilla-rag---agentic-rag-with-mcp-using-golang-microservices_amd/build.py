@@ -14,7 +14,10 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "lib", "libvsearch.so")
 SVC_LIB = os.path.join(HERE, "lib", "libvsearch_service.so")
 SVC_SOURCES = ["service/json.cpp", "service/vector_service.cpp", "service/batcher.cpp",
-               "service/loadgen.cpp"]
+               "service/loadgen.cpp", "service/http.cpp"]
+SVC_HEADERS = ["service/json.h", "service/batcher.h", "service/http.h"]
+# the vector-service process (PORT, VS_DEVICES, ...; csrc/service/server_main.cpp)
+SERVER = os.path.join(HERE, "lib", "vsearch_server")
 ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
@@ -56,12 +59,20 @@ def build(verbose: bool = False, force: bool = False) -> str:
         subprocess.run(cmd, check=True)
     # host-only service layer (the rag/vector-service handler mirror) over the C-ABI
     svc_srcs = [os.path.join(CSRC, x) for x in SVC_SOURCES]
-    svc_hdrs = [os.path.join(CSRC, "service", "json.h"), os.path.join(CSRC, "service", "batcher.h"),
-                os.path.join(ROOT, "include", "vsearch_service.h")]
+    svc_hdrs = [os.path.join(CSRC, x) for x in SVC_HEADERS] + [
+        os.path.join(ROOT, "include", "vsearch_service.h")]
     if force or _mtime(SVC_LIB) < max(_mtime(x) for x in svc_srcs + svc_hdrs + [LIB]):
         cmd = [os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-fPIC", "-Wall", "-shared",
                "-o", SVC_LIB, *svc_srcs, "-L" + os.path.dirname(LIB), "-lvsearch",
                "-pthread", "-Wl,-rpath,$ORIGIN", "-Wl,-soname,libvsearch_service.so"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    main_src = os.path.join(CSRC, "service", "server_main.cpp")
+    if force or _mtime(SERVER) < max(_mtime(main_src), _mtime(SVC_LIB)):
+        cmd = [os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-Wall", "-o", SERVER, main_src,
+               "-L" + os.path.dirname(LIB), "-lvsearch_service", "-lvsearch", "-pthread",
+               "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

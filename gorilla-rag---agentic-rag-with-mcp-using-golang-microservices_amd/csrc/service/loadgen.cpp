@@ -10,6 +10,15 @@
 // random unit vectors, one pool per run, floats printed with 9 significant
 // digits, which round-trip through Go's decimal -> float32 parse), so the
 // loop measures the service: decode, batcher, engine, reply encode.
+//
+// With "http":"host:port" the same bodies go over TCP as HTTP/1.1 POSTs
+// (http.Post in retrieval-service, main.go:229-233) to a listener
+// (vsvc_http_start, or any server with the reference's routes): each client
+// keeps one keep-alive connection (Go's Transport reuses idle connections),
+// or opens one per request with "keepalive":false; a keep-alive connection
+// the server closed is re-dialled once.
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -24,6 +33,7 @@
 #include <vector>
 
 #include "../../../include/vsearch_service.h"
+#include "http.h"
 #include "json.h"
 
 using vsjson::Json;
@@ -41,10 +51,72 @@ double num_or(const Json& o, const char* key, double dflt) {
   return v && v->kind == Json::Number ? v->num : dflt;
 }
 
+// One client's HTTP/1.1 connection to the listener.
+struct HttpClient {
+  std::string host, host_hdr;
+  int port = 0;
+  bool keepalive = true;
+  int fd = -1;
+  std::string buf;
+
+  ~HttpClient() { drop(); }
+  void drop() {
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+    buf.clear();
+  }
+  // POST path body -> *r; false on a transport error (*err says which)
+  bool post(const std::string& path, const std::string& body, vshttp::Response* r,
+            std::string* err) {
+    std::string req = "POST " + path + " HTTP/1.1\r\nHost: " + host_hdr +
+                      "\r\nUser-Agent: vsvc-loadgen\r\nContent-Type: application/json\r\n"
+                      "Content-Length: " + std::to_string(body.size()) + "\r\n";
+    if (!keepalive) req += "Connection: close\r\n";
+    req += "\r\n";
+    req += body;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const bool fresh = fd < 0;
+      if (fresh) {
+        fd = vshttp::connect_tcp(host, port);
+        if (fd < 0) {
+          *err = "connect failed";
+          return false;
+        }
+      }
+      if (!vshttp::send_all(fd, req.data(), req.size())) {
+        drop();
+        if (fresh) break;
+        continue;  // a reused connection the server had closed
+      }
+      for (;;) {
+        size_t used = 0;
+        const vshttp::Frame f = vshttp::parse_response(buf.data(), buf.size(), r, &used);
+        if (f == vshttp::Frame::kBad) {
+          *err = "malformed response";
+          drop();
+          return false;
+        }
+        if (f == vshttp::Frame::kDone) {
+          buf.erase(0, used);
+          if (r->status >= 100 && r->status < 200) continue;  // 100 Continue
+          if (!r->keep_alive || !keepalive) drop();
+          return true;
+        }
+        if (!vshttp::recv_some(fd, &buf)) break;
+      }
+      const bool got_nothing = buf.empty();
+      drop();
+      if (fresh || !got_nothing) break;  // re-dial only an idle connection that was closed
+    }
+    *err = "connection closed";
+    return false;
+  }
+};
+
 }  // namespace
 
 extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
-  if (!svc || !spec_json || !report) return VS_ERR_INVALID_ARG;
+  if (!spec_json || !report) return VS_ERR_INVALID_ARG;
   *report = nullptr;
   Json spec;
   std::string perr;
@@ -62,6 +134,16 @@ extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
   const int k_min = (int)num_or(spec, "k_min", 3), k_max = (int)num_or(spec, "k_max", 50);
   const int nqueries = (int)num_or(spec, "queries", 256);
   const uint64_t seed = (uint64_t)num_or(spec, "seed", 1);
+  // TCP mode: "http":"host:port"
+  std::string http_host;
+  int http_port = 0;
+  const Json* hv = spec.get("http");
+  const bool use_http = hv && hv->kind == Json::String;
+  if (hv && !use_http && hv->kind != Json::Null) return VS_ERR_INVALID_ARG;
+  if (use_http && !vshttp::split_addr(hv->str, &http_host, &http_port)) return VS_ERR_INVALID_ARG;
+  if (!use_http && !svc) return VS_ERR_INVALID_ARG;
+  const Json* kav = spec.get("keepalive");
+  const bool keepalive = !(kav && kav->kind == Json::Bool && !kav->b);
   if (dim < 1 || dim > 65536 || clients < 1 || clients > 4096 || !(seconds > 0) ||
       seconds > 3600 || k_min < 1 || k_max < k_min || nqueries < 1 || nqueries > 1 << 16)
     return VS_ERR_INVALID_ARG;
@@ -99,6 +181,15 @@ extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
     th.emplace_back([&, c] {
       std::mt19937_64 rng(seed * 7919 + (uint64_t)c + 1);
       std::string body;
+      HttpClient hc;
+      if (use_http) {
+        hc.host = http_host.empty() ? std::string("127.0.0.1") : http_host;
+        hc.port = http_port;
+        hc.host_hdr = hc.host + ":" + std::to_string(http_port);
+        hc.keepalive = keepalive;
+      }
+      vshttp::Response hr;
+      std::string terr;
       auto& my = lat[c];
       while (std::chrono::steady_clock::now() < deadline) {
         const std::string& coll = colls[rng() % colls.size()];
@@ -116,8 +207,16 @@ extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
         size_t n = 0;
         const char* ct = nullptr;
         const auto a = std::chrono::steady_clock::now();
-        const int rc = vsvc_handle(svc, "POST", "/search", body.data(), body.size(), &status,
-                                   &resp, &n, &ct);
+        int rc;
+        if (use_http) {
+          rc = hc.post("/search", body, &hr, &terr) ? VS_OK : VS_ERR_IO;
+          status = rc == VS_OK ? hr.status : 0;
+          resp = rc == VS_OK ? (char*)hr.body.data() : nullptr;
+          n = rc == VS_OK ? hr.body.size() : 0;
+        } else {
+          rc = vsvc_handle(svc, "POST", "/search", body.data(), body.size(), &status, &resp, &n,
+                           &ct);
+        }
         const auto b = std::chrono::steady_clock::now();
         bool ok = rc == VS_OK && status == 200 && resp;
         if (ok) {  // the caller decodes results[] (main.go:244-257)
@@ -131,10 +230,12 @@ extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
           errors.fetch_add(1);
           std::lock_guard<std::mutex> g(mu);
           if (first_error.empty())
-            first_error = "status " + std::to_string(status) + ": " +
-                          (resp ? std::string(resp, std::min<size_t>(n, 300)) : "");
+            first_error = rc != VS_OK && use_http
+                              ? "transport: " + terr
+                              : "status " + std::to_string(status) + ": " +
+                                    (resp ? std::string(resp, std::min<size_t>(n, 300)) : "");
         }
-        vsvc_free(resp);
+        if (!use_http) vsvc_free(resp);
         requests.fetch_add(1);
         my.push_back(std::chrono::duration<float, std::milli>(b - a).count());
       }
@@ -163,6 +264,7 @@ extern "C" int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report) {
   l.obj.emplace_back("max", Json::number(all.empty() ? 0.0 : all.back()));
   o.obj.emplace_back("lat_ms", std::move(l));
   o.obj.emplace_back("first_error", Json::string(first_error));
+  o.obj.emplace_back("transport", Json::string(use_http ? "http" : "inproc"));
   std::string s;
   vsjson::encode(o, &s, false);
   *report = dup_str(s);

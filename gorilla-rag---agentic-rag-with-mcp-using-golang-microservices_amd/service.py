@@ -52,6 +52,12 @@ def load_service_library(path: str = SVC_LIB_PATH):
     L.vsvc_stats.restype = ctypes.c_int
     L.vsvc_loadgen.argtypes = [vp, cp, ctypes.POINTER(vp)]
     L.vsvc_loadgen.restype = ctypes.c_int
+    L.vsvc_http_start.argtypes = [vp, cp, ctypes.POINTER(vp)]
+    L.vsvc_http_start.restype = ctypes.c_int
+    L.vsvc_http_port.argtypes = [vp]
+    L.vsvc_http_port.restype = ctypes.c_int
+    L.vsvc_http_stop.argtypes = [vp]
+    L.vsvc_http_stop.restype = None
     _svc = L
     return L
 
@@ -139,12 +145,41 @@ class VectorService:
         return json.loads(_take(self._L, out))
 
     def loadgen(self, collections, dim: int, clients: int = 16, seconds: float = 5.0,
-                k_min: int = 3, k_max: int = 50, queries: int = 256, seed: int = 1) -> dict:
+                k_min: int = 3, k_max: int = 50, queries: int = 256, seed: int = 1,
+                http: Optional[str] = None, keepalive: bool = True) -> dict:
         """Closed-loop /search load (vsvc_loadgen): retrieval-service-shaped
-        requests from `clients` threads for `seconds`; returns QPS + latency."""
-        spec = json.dumps({"collections": list(collections), "dim": dim, "clients": clients,
-                           "seconds": seconds, "k_min": k_min, "k_max": k_max,
-                           "queries": queries, "seed": seed}).encode()
+        requests from `clients` threads for `seconds`; returns QPS + latency.
+        `http="host:port"` posts them over TCP to a listener instead."""
+        spec = {"collections": list(collections), "dim": dim, "clients": clients,
+                "seconds": seconds, "k_min": k_min, "k_max": k_max, "queries": queries,
+                "seed": seed}
+        if http is not None:
+            spec.update(http=http, keepalive=keepalive)
         out = ctypes.c_void_p()
-        _check(self._L.vsvc_loadgen(self._h, spec, ctypes.byref(out)))
+        _check(self._L.vsvc_loadgen(self._h, json.dumps(spec).encode(), ctypes.byref(out)))
         return json.loads(_take(self._L, out))
+
+    def serve(self, addr: str = "127.0.0.1:0") -> "HttpListener":
+        """HTTP/1.1 listener on `addr` in front of the handlers (vsvc_http_start)."""
+        h = ctypes.c_void_p()
+        _check(self._L.vsvc_http_start(self._h, addr.encode(), ctypes.byref(h)))
+        return HttpListener(self._L, h)
+
+
+class HttpListener:
+    """A running vsvc_http listener; stop() before closing the service."""
+
+    def __init__(self, L, h):
+        self._L, self._h = L, h
+        self.port = L.vsvc_http_port(h)
+
+    def stop(self):
+        if self._h:
+            self._L.vsvc_http_stop(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()

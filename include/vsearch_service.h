@@ -11,6 +11,9 @@
  *   POST /upsert       upsertHandler       main.go:149-225
  *   POST /search       searchHandler       main.go:227-278
  *
+ * served in-process by vsvc_handle, or over TCP by vsvc_http_start (the
+ * reference's http.ListenAndServe, main.go:75-77).
+ *
  * Point UUIDs and payloads live here (a UUID -> row map and a row-indexed
  * payload store per collection); the engine sees dense rows only. A Go
  * deployment binds the same engine C-ABI through cgo and
@@ -76,13 +79,37 @@ int vsvc_stats(vsvc* svc, char** out);
 
 /* Closed-loop load generator: `clients` threads each send
  * /search bodies shaped like rag/retrieval-service's searchVectorDB
- * (main.go:221-226: {"collection","filter","query","top_k"}) through
- * vsvc_handle, back to back, for `seconds`. spec_json:
- * {"collections":["..",..],"dim":768,"clients":64,"seconds":5,"k_min":3,
- *  "k_max":50,"queries":256,"seed":1}. *report (malloc'd) gets
+ * (main.go:221-226: {"collection","filter","query","top_k"}) back to back,
+ * for `seconds`: through vsvc_handle in-process, or, with "http":"host:port",
+ * as HTTP/1.1 POSTs over TCP to a listener (vsvc_http_start or any server
+ * with the reference's routes; `svc` may then be NULL), each client on its
+ * own keep-alive connection ("keepalive":false opens one per request).
+ * spec_json: {"collections":["..",..],"dim":768,"clients":64,"seconds":5,
+ * "k_min":3,"k_max":50,"queries":256,"seed":1,"http":"127.0.0.1:8082",
+ * "keepalive":true}. *report (malloc'd) gets
  * {"requests","errors","seconds","qps","lat_ms":{"p50","p90","p99","max"},
- *  "first_error"}. Returns VS_OK or VS_ERR_INVALID_ARG for a bad spec. */
+ *  "first_error","transport":"inproc"|"http"}. Returns VS_OK or
+ * VS_ERR_INVALID_ARG for a bad spec. */
 int vsvc_loadgen(vsvc* svc, const char* spec_json, char** report);
+
+/* The reference's http.ListenAndServe(":"+PORT, mux) (main.go:70-77): an
+ * HTTP/1.1 listener on `addr` ("host:port", ":port" for every IPv4
+ * address; port 0 picks a free one, see vsvc_http_port) that hands every
+ * request to vsvc_handle and answers as net/http does: keep-alive and
+ * pipelining, Content-Length or chunked request bodies, Expect:
+ * 100-continue, HEAD, routing on the URL path without its query, 400 for a
+ * malformed request or a missing Host header, 431 past 1 MiB of headers,
+ * 501 for a transfer coding other than chunked, 505 for HTTP/2+ request
+ * lines. One thread per connection (net/http: one goroutine); concurrent
+ * /search requests meet in the batcher. Returns VS_OK, VS_ERR_INVALID_ARG
+ * (bad address) or VS_ERR_IO (socket / bind / listen failed). */
+typedef struct vsvc_http vsvc_http;
+int vsvc_http_start(vsvc* svc, const char* addr, vsvc_http** out);
+/* The bound TCP port. */
+int vsvc_http_port(const vsvc_http* h);
+/* Stops accepting, closes every connection after its in-flight request and
+ * joins the threads. Call before vsvc_close. */
+void vsvc_http_stop(vsvc_http* h);
 
 /* Serves one HTTP request. Sets *status, *body (malloc'd, NUL-terminated;
  * free with vsvc_free) and *content_type (static string). Safe to call from

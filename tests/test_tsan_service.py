@@ -27,7 +27,7 @@ SVC = os.path.join(ROOT, "gorilla-rag---agentic-rag-with-mcp-using-golang-micros
 def test_service_under_tsan(tmp_path):
     exe = str(tmp_path / "tsan_driver")
     srcs = [os.path.join(SVC, f) for f in ("json.cpp", "vector_service.cpp", "batcher.cpp",
-                                           "loadgen.cpp")]
+                                           "loadgen.cpp", "http.cpp")]
     srcs += [os.path.join(ROOT, "tests", "tsan", f) for f in ("fake_engine.cpp",
                                                              "tsan_driver.cpp")]
     subprocess.run([CLANG, "-std=c++17", "-g", "-O1", "-fsanitize=thread", "-pthread", *srcs,

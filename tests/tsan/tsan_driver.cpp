@@ -142,6 +142,36 @@ int main(int argc, char** argv) {
     vsvc_close(svc2);
     vs_close(eng2);
   }
+  // the HTTP listener under concurrent keep-alive and per-request connections,
+  // with in-process searches beside it; stopped while idle connections remain
+  {
+    vsvc_http* http = nullptr;
+    if (vsvc_http_start(svc, "127.0.0.1:0", &http) != VS_OK) return 10;
+    const std::string addr = "127.0.0.1:" + std::to_string(vsvc_http_port(http));
+    std::vector<std::thread> lg;
+    std::atomic<int> lg_bad{0};
+    for (int ka = 0; ka < 2; ++ka)
+      lg.emplace_back([&, ka] {
+        const std::string spec = "{\"collections\":[\"a\",\"b\"],\"dim\":" + std::to_string(dim) +
+                                 ",\"clients\":6,\"seconds\":0.5,\"http\":\"" + addr +
+                                 "\",\"keepalive\":" + (ka ? "true" : "false") + "}";
+        char* rep = nullptr;
+        if (vsvc_loadgen(nullptr, spec.c_str(), &rep) != VS_OK || !rep ||
+            std::strstr(rep, "\"errors\":0,") == nullptr) {
+          std::fprintf(stderr, "http loadgen: %s\n", rep ? rep : "(none)");
+          lg_bad++;
+        }
+        vsvc_free(rep);
+      });
+    std::mt19937 rng(7);
+    for (int i = 0; i < 50; ++i)
+      if (call(svc, "POST", "/search",
+               "{\"collection\":\"a\",\"query\":" + vec_json(rng, dim) + ",\"top_k\":4}") != 200)
+        g_bad++;
+    for (auto& t : lg) t.join();
+    if (lg_bad.load()) return 11;
+    vsvc_http_stop(http);
+  }
   char* st = nullptr;
   if (vsvc_stats(svc, &st) == VS_OK) {
     std::printf("stats %s\n", st);

@@ -2,11 +2,14 @@
 vector-service mirror, 3 collections x 5M x 1024 bf16, k uniform in [3, 50].
 
     python tools/loadgen_c5.py [--rows 5000000] [--clients 16,64,256] [--seconds 5]
+                               [--transport inproc|http|both]
 
 Each client count runs once with the dynamic batcher (csrc/service/batcher.h)
-and, for comparison, once with batching off. Clients are in-process threads
-calling vsvc_handle with retrieval-service-shaped JSON bodies
-(csrc/service/loadgen.cpp); no sockets are involved. One JSON line per run.
+and, for comparison, once with batching off. Clients are threads sending
+retrieval-service-shaped JSON bodies (csrc/service/loadgen.cpp): in-process
+through vsvc_handle, or (--transport http) as HTTP/1.1 POSTs over TCP to the
+service's listener (vsvc_http_start on 127.0.0.1), each client on its own
+keep-alive connection. One JSON line per run.
 """
 import argparse
 import json
@@ -26,6 +29,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--unbatched-clients", type=int, default=64)
     ap.add_argument("--workers", type=int, default=1, help="batcher worker threads")
+    ap.add_argument("--transport", default="inproc", choices=["inproc", "http", "both"])
     args = ap.parse_args()
     import torch  # noqa: F401  (binds torch's HIP runtime first, as bench.py does)
     import __graft_entry__ as ge
@@ -50,17 +54,20 @@ def main():
             svc.bulk_generate(n, args.rows, 0x5EED + i)
         print(f"[c5] {len(names)} x {args.rows} x {args.dim} bf16 generated in "
               f"{time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-        for clients in todo:
-            svc.loadgen(names, args.dim, clients=clients, seconds=0.5)  # warm-up
+        lis = svc.serve("127.0.0.1:0") if args.transport != "inproc" else None
+        transports = ["inproc", "http"] if args.transport == "both" else [args.transport]
+        for clients, transport in [(c, t) for c in todo for t in transports]:
+            addr = "127.0.0.1:%d" % lis.port if transport == "http" else None
+            svc.loadgen(names, args.dim, clients=clients, seconds=0.5, http=addr)  # warm-up
             before = svc.stats()
             rep = svc.loadgen(names, args.dim, clients=clients, seconds=args.seconds,
-                              seed=clients)
+                              seed=clients, http=addr)
             st = svc.stats()
             calls = st["engine_calls"] - before["engine_calls"]
             nreq = st["requests"] - before["requests"]
             line = {"workload": f"C5: 3 x {args.rows} x {args.dim} bf16, k in [3,50], "
-                                "closed loop, in-process clients",
-                    "clients": clients, "batching": batching, "workers": args.workers,
+                                f"closed loop, {transport} clients",
+                    "transport": transport, "clients": clients, "batching": batching, "workers": args.workers,
                     "qps": round(rep["qps"], 1),
                     "requests": rep["requests"], "errors": rep["errors"],
                     "first_error": rep["first_error"][:200],
@@ -69,6 +76,8 @@ def main():
                     "mean_batch": round(nreq / calls, 2) if calls else None,
                     "largest_call": st["largest_call"]}
             print(json.dumps(line), flush=True)
+        if lis is not None:
+            lis.stop()
         svc.close()
         eng.close()
 
