@@ -244,8 +244,8 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
 
 // Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
 // queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
-//  1. sample pass over 1/64 of every workgroup's tiles -> top-k of the tile
-//     maxima -> per-query lower bound on the global k-th key;
+//  1. sample pass over 1/128 of every workgroup's tiles -> tile maxima ->
+//     sample_bound_kernel: per-query lower bound on the global k-th score;
 //  2. main pass: rows reaching the bound -> candidate buffers -> select. A
 //     full buffer quarter keeps its best slabs (exact, vs_kernels.h), so no
 //     pass is ever re-run and nothing here waits on the device.

@@ -10,8 +10,8 @@ namespace vsk {
 // 8 waves x 32 at dim <= 768, 8 x 16 at dim 1024 / 1536; mfma_queries()).
 constexpr uint32_t kMfmaQueries = 256;
 // Largest k of the batched MFMA scan (candidate path); larger k uses the
-// GEMV scan per query. The sorted-list pass (overflow fallback) keeps
-// kMfmaListMaxK keys per query in LDS.
+// GEMV scan per query. The sorted-list pass (small collections, k <= 16)
+// keeps kMfmaListMaxK keys per query in LDS.
 constexpr uint32_t kMfmaMaxK = 128;
 constexpr uint32_t kMfmaListMaxK = 16;
 // Largest k any scan supports (GEMV register lists: 16 entries per lane).

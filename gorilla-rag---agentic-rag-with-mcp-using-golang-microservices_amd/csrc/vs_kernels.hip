@@ -6,10 +6,13 @@
 //   * gemv_topk_kernel  — one query, HBM-bound stream of the resident matrix
 //                         (16-B coalesced loads, wave reduction, per-wave
 //                         register top-k list), fp32 or bf16 rows;
-//   * mfma_topk_kernel  — up to 256 queries per launch, bf16 rows streamed
-//                         once through an LDS ring by LDS-DMA, scores on
-//                         v_mfma_f32_32x32x16_bf16 with the query block
-//                         resident in registers, fused per-query top-k in LDS;
+//   * mfma_topk_kernel  — up to 256 queries per launch, bf16 / fp32 rows
+//                         streamed once through an LDS ring by LDS-DMA,
+//                         scores on v_mfma_f32_16x16x32_bf16 (fp32:
+//                         16x16x4_f32) with the query block resident in
+//                         registers; a sample pass bounds each query's k-th
+//                         score and the main pass keeps only 8-row slabs
+//                         that reach it (select_slab_kernel picks the top k);
 //   * merge_keys_kernel — global top-k over per-workgroup / per-shard lists.
 // Store side (upsert, Qdrant cosine preprocess) and the synthetic generator
 // are here too. Numerics contract: include/vsearch.h and DESIGN.md.
@@ -911,20 +914,23 @@ hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t*
 // per 2 LDS reads. Scores never reach HBM.
 //
 // Top-k, main pass (MODE 0). Every query starts from a lower bound on its
-// global k-th score (init_th, the sample pass below). The tile epilogue tests
-// each lane's 8 scores per group against it (one v_max3 chain + one ballot);
-// the rare survivors are appended, unsorted, to the query's candidate buffer
-// in global memory (slot from an LDS counter, fire-and-forget stores), and
-// select_cand_kernel picks the top k of all workgroups' candidates. No wave
-// ever waits on a list in the loop, so no stall reaches the other seven
-// waves through the per-chunk barrier. A full buffer quarter (many
-// near-equal rows) keeps its best slabs in place (mf_replace_min): exact,
-// so no batch is ever re-run and the host never waits on the device.
+// global k-th score (init_score, the sample pass below). The tile epilogue
+// tests each lane's 8 scores per group against it (one v_max3 chain); a lane
+// whose maximum reaches it appends its 8-score slab, unsorted, to its own
+// quarter of the query's candidate buffer in global memory (count and slot
+// in registers, fire-and-forget stores), and select_slab_kernel picks the
+// top k of all workgroups' slabs. No wave ever waits on a list in the loop,
+// so no stall reaches the other seven waves through the per-chunk barrier.
+// A full buffer quarter (many near-equal rows) keeps its best slabs in place
+// (mf_replace_min): exact, so no batch is ever re-run and the host never
+// waits on the device.
 //
-// Sample pass (MODE 3): the same scan over the first 1/64 of every
-// workgroup's tiles, keeping per query the top k of the TILE MAXIMA (mf_insert
-// lists). Those are k distinct rows with scores >= the merged k-th key, so it
-// lower-bounds the global k-th key: rows under it can never enter the result.
+// Sample pass (MODE 3): the same scan over the first 1/128 of every
+// workgroup's tiles, writing per (query, tile) only the TILE MAXIMUM;
+// sample_bound_kernel takes the k-th largest of them (k distinct rows reach
+// it), a lower bound on the global k-th score: rows under it can never enter
+// the result. MODE 8 (sorted per-query lists in LDS, mf_insert) serves
+// small collections (fewer than 8 tiles per workgroup, k <= 16).
 // Query groups (16 queries each) per wave: G = 2 -> 8 waves of 32 queries
 // (two per SIMD, 256 queries per launch; D <= 768); G = 1 -> 8 waves of 16
 // queries (128 per launch: the B fragments of D = 1024 / 1536 then fit the
