@@ -80,6 +80,47 @@ struct EventPair {
   hipEvent_t a, b;
 };
 
+// Pinned staging of one host search call (search_host): the queries go H2D
+// and the keys D2H asynchronously through it, so a call holds work_mu only
+// while it enqueues and waits for the device outside it; a call arriving
+// meanwhile (another batcher worker, another collection) enqueues behind it
+// on the same stream, and the device runs the two back to back.
+struct HostSlot {
+  void* in = nullptr;
+  void* out = nullptr;
+  size_t in_bytes = 0, out_bytes = 0;
+  hipEvent_t done = nullptr;
+  bool busy = false;  // between its enqueue and the end of its decode
+  HostSlot() = default;
+  HostSlot(const HostSlot&) = delete;
+  HostSlot& operator=(const HostSlot&) = delete;
+  ~HostSlot() {
+    if (in) (void)hipHostFree(in);
+    if (out) (void)hipHostFree(out);
+    if (done) (void)hipEventDestroy(done);
+  }
+  // grows the pinned buffers (the slot is idle: nothing in flight uses them)
+  hipError_t ensure(size_t in_b, size_t out_b) {
+    hipError_t e = hipSuccess;
+    if (!done) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (e == hipSuccess && in_b > in_bytes) {
+      if (in) (void)hipHostFree(in);
+      in = nullptr;
+      in_bytes = 0;
+      e = hipHostMalloc(&in, in_b, hipHostMallocDefault);
+      if (e == hipSuccess) in_bytes = in_b;
+    }
+    if (e == hipSuccess && out_b > out_bytes) {
+      if (out) (void)hipHostFree(out);
+      out = nullptr;
+      out_bytes = 0;
+      e = hipHostMalloc(&out, out_b, hipHostMallocDefault);
+      if (e == hipSuccess) out_bytes = out_b;
+    }
+    return e;
+  }
+};
+
 
 struct DevEngine {
   int device = 0;
@@ -107,6 +148,7 @@ struct DevEngine {
   std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
   uint64_t next_filter = 1;
   std::vector<uint64_t> h_keys;
+  std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing
   std::vector<EventPair> scan_ev, merge_ev;
   std::vector<hipEvent_t> ev_pool;  // recycled timing events (none created on the hot path)

@@ -803,7 +803,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
                                         " words, the collection needs " +
                                         std::to_string((c->rows + 63) / 64));
-  std::lock_guard<std::mutex> g(eng->work_mu);
+  std::unique_lock<std::mutex> g(eng->work_mu);
   const DevEngine::DevFilter* df = nullptr;
   if (filter_id) {
     auto it = eng->filters.find(filter_id);
@@ -825,9 +825,22 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     VS_HIP(eng->keys.ensure(kbytes), "alloc keys");
     VS_HIP(eng->allow.ensure(abytes), "alloc filter bitmap");
   }
-  VS_HIP(hipMemcpyAsync(eng->q_in.p, queries, qbytes, hipMemcpyHostToDevice, eng->stream),
+  // an idle pinned staging slot (one per call in flight)
+  HostSlot* hs = nullptr;
+  for (auto& x : eng->host_slots)
+    if (!x->busy) {
+      hs = x.get();
+      break;
+    }
+  if (!hs) {
+    eng->host_slots.push_back(std::make_unique<HostSlot>());
+    hs = eng->host_slots.back().get();
+  }
+  VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
+  std::memcpy(hs->in, queries, qbytes);
+  VS_HIP(hipMemcpyAsync(eng->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, eng->stream),
          "query H2D");
-  if (abytes)
+  if (abytes)  // pageable: HIP stages it (a shipped-bitmap call, not the batcher's path)
     VS_HIP(hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream),
            "filter bitmap H2D");
   int rc;
@@ -840,12 +853,18 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
                      abytes ? eng->allow.as<uint64_t>() : nullptr,
                      abytes ? popcount_rows(allow, c->rows) : 0);
   if (rc != VS_OK) return rc;
-  eng->h_keys.resize((size_t)nq * k);
-  VS_HIP(hipMemcpyAsync(eng->h_keys.data(), eng->keys.p, kbytes, hipMemcpyDeviceToHost,
-                        eng->stream),
+  VS_HIP(hipMemcpyAsync(hs->out, eng->keys.p, kbytes, hipMemcpyDeviceToHost, eng->stream),
          "keys D2H");
-  VS_HIP(hipStreamSynchronize(eng->stream), "search sync");
-  decode_host(eng->h_keys.data(), nq, k, out_scores, out_rows, out_count);
+  VS_HIP(hipEventRecord(hs->done, eng->stream), "search event");
+  hs->busy = true;
+  // wait for the device outside work_mu: the next call (q_in, keys and every
+  // scratch buffer are ordered on the same stream) enqueues behind this one
+  g.unlock();
+  const hipError_t we = hipEventSynchronize(hs->done);
+  if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+  g.lock();
+  hs->busy = false;
+  VS_HIP(we, "search sync");
   return VS_OK;
 }
 
