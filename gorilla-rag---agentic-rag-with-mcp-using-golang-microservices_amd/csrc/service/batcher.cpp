@@ -67,14 +67,42 @@ Stats Batcher::stats() {
   return stats_;
 }
 
+namespace {
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+std::chrono::steady_clock::time_point deadline_in(int64_t us) {
+  return std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+}
+}  // namespace
+
 void Batcher::run() {
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
     cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
     if (queue_.empty()) break;  // stop_ and drained
-    if (opt_.max_wait_us && queue_.size() < opt_.max_batch && !stop_)
-      cv_.wait_for(lk, std::chrono::microseconds(opt_.max_wait_us),
-                   [&] { return stop_ || queue_.size() >= opt_.max_batch; });
+    if (opt_.max_wait_us && queue_.size() < opt_.max_batch && !stop_) {
+      cv_.wait_until(lk, deadline_in(opt_.max_wait_us),
+                     [&] { return stop_ || queue_.size() >= opt_.max_batch; });
+      // another worker may have taken the whole queue while this one lingered
+      if (queue_.empty()) continue;
+    }
+    // Another call in flight: form this batch late, lead_us before the
+    // earliest in-flight call is expected to end (or at once when it ends
+    // earlier), so requests arriving in the meantime still join it.
+    if (opt_.lead_us && !inflight_end_.empty() && !stop_) {
+      const int64_t wake = *std::min_element(inflight_end_.begin(), inflight_end_.end()) -
+                           (int64_t)opt_.lead_us;
+      const size_t n0 = inflight_end_.size();
+      const int64_t t = now_us();
+      if (wake > t)
+        cv_.wait_until(lk, deadline_in(wake - t), [&] {
+          return stop_ || inflight_end_.size() < n0 || queue_.size() >= opt_.max_batch;
+        });
+      if (queue_.empty()) continue;  // another worker took it
+    }
     // One engine call per turn, for the group (collection, dim, k class) of
     // the oldest queued request: all of that group's queued requests, up to
     // max_batch, go together; other groups keep queueing meanwhile, so the
@@ -92,13 +120,33 @@ void Batcher::run() {
         ++it;
       }
     }
+    // expected end of this call: the device runs the calls in flight one
+    // after another, so it starts when the ones ahead of it are expected to
+    // end, and takes its collection's recent service time
+    const std::string coll = *first->coll;
+    const int64_t t0 = now_us();
+    auto est = call_us_.find(coll);
+    gpu_free_at_ = std::max(gpu_free_at_, t0) +
+                   (int64_t)(est == call_us_.end() ? 0.0 : est->second);
+    const int64_t end = gpu_free_at_;
+    inflight_end_.push_back(end);
     lk.unlock();
     execute(batch);
     lk.lock();
+    // service time: from its start, or from the previous call's end when it
+    // was queued behind one
+    const int64_t t1 = now_us();
+    const double took = (double)(t1 - std::max(t0, last_done_));
+    last_done_ = t1;
+    double& avg = call_us_[coll];
+    avg = avg == 0.0 ? took : 0.8 * avg + 0.2 * took;
+    inflight_end_.erase(std::find(inflight_end_.begin(), inflight_end_.end(), end));
+    if (inflight_end_.empty()) gpu_free_at_ = 0;
     for (Req* r : batch) {
       r->done = true;
       r->cv->notify_one();
     }
+    cv_.notify_all();  // a worker waiting to form its batch late
   }
 }
 

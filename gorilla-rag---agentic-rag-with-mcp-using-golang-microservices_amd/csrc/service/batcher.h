@@ -31,6 +31,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -46,8 +47,14 @@ struct Options {
   uint32_t max_wait_us = 0;  // linger for a non-full batch (0 = none)
   // worker threads taking turns: with 2, the next call's batch assembly,
   // query copy and launch wait on the engine while the current call runs,
-  // instead of following its return (and its results' hand-out)
-  uint32_t workers = 1;
+  // instead of following its return (and its results' hand-out); the engine
+  // waits for the device outside its lock, so the two calls run back to back
+  uint32_t workers = 2;
+  // with a call in flight, a second worker forms its batch only lead_us
+  // before that call is expected to end (its collection's recent call time),
+  // not at once: requests arriving meanwhile still join, so pipelining the
+  // calls does not shrink the batches (0 = form at once)
+  uint32_t lead_us = 300;
 };
 
 struct Stats {
@@ -85,6 +92,12 @@ class Batcher {
   std::condition_variable cv_;
   std::deque<Req*> queue_;
   bool stop_ = false;
+  // calls in flight: expected end (steady clock, us) of each, and of the
+  // last one; end of the last call that completed; recent service time per
+  // collection (exponential average, us)
+  std::vector<int64_t> inflight_end_;
+  int64_t gpu_free_at_ = 0, last_done_ = 0;
+  std::map<std::string, double> call_us_;
   Stats stats_;
   std::vector<std::thread> workers_;
 };

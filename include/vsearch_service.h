@@ -39,7 +39,8 @@ typedef struct vsvc vsvc;
  * regulatory_docs, merchant_docs, kyc_docs, dim 768, Cosine, fp32) or
  * {"collections":[{"name":"..","dim":768,"metric":"Cosine"|"Dot",
  *  "dtype":"f32"|"bf16"}...],
- *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0,"workers":1},
+ *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0,"workers":2,
+ *              "lead_us":300},
  *  "filter":"ignore"|"match"}.
  * "filter":"ignore" (default) keeps the reference's behaviour: the request's
  * `filter` is decoded and dropped (main.go:30 vs :249-254). "match" applies
@@ -49,7 +50,9 @@ typedef struct vsvc vsvc;
  * searched with vs_search_filter_id. Existing collections are reused.
  * Batching (on by default) coalesces concurrent /search requests into one
  * engine call per collection (and per filter, for filtered requests)
- * (csrc/service/batcher.h); each request still gets exactly its own top k. */
+ * (csrc/service/batcher.h); each request still gets exactly its own top k.
+ * With 2 workers two calls are in flight (the second enqueued while the
+ * first runs, its batch formed lead_us before the first is expected to end). */
 int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out);
 void vsvc_close(vsvc* svc);
 

@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--clients", default="16,64,256")
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--unbatched-clients", type=int, default=64)
-    ap.add_argument("--workers", type=int, default=1, help="batcher worker threads")
+    ap.add_argument("--workers", type=int, default=2, help="batcher worker threads")
+    ap.add_argument("--lead-us", type=int, default=300,
+                    help="late batch formation with a call in flight (batcher.h)")
     ap.add_argument("--transport", default="inproc", choices=["inproc", "http", "both"])
     args = ap.parse_args()
     import torch  # noqa: F401  (binds torch's HIP runtime first, as bench.py does)
@@ -48,7 +50,8 @@ def main():
         eng = pkg.VectorEngine(device=0)
         svc = svcmod.VectorService(eng, {"collections": colls,
                                          "batching": {"enabled": batching,
-                                                      "workers": args.workers}})
+                                                      "workers": args.workers,
+                                                      "lead_us": args.lead_us}})
         t0 = time.time()
         for i, n in enumerate(names):
             svc.bulk_generate(n, args.rows, 0x5EED + i)
@@ -67,7 +70,7 @@ def main():
             nreq = st["requests"] - before["requests"]
             line = {"workload": f"C5: 3 x {args.rows} x {args.dim} bf16, k in [3,50], "
                                 f"closed loop, {transport} clients",
-                    "transport": transport, "clients": clients, "batching": batching, "workers": args.workers,
+                    "transport": transport, "clients": clients, "batching": batching, "workers": args.workers, "lead_us": args.lead_us,
                     "qps": round(rep["qps"], 1),
                     "requests": rep["requests"], "errors": rep["errors"],
                     "first_error": rep["first_error"][:200],
