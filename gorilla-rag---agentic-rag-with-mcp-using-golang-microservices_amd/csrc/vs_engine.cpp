@@ -264,13 +264,13 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
   const bool fast = tpw >= 8;
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
-  const uint32_t st = vsk::mfma_sample_tiles(n_rows);
+  const uint32_t st = vsk::mfma_sample_tiles(n_rows, dim, f32);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds
-  // main pass slabs: 32 B of scores + a 4-B tile row + a 4-B maximum per slot
+  // main pass slabs: 32 B of scores + a 4-B tile row per slot
   const size_t slots = (size_t)maxl * PS * cap;
-  const size_t cbytes = slots * 40;
+  const size_t cbytes = slots * 36;
   const size_t scbytes = (size_t)maxl * st * PS * 4;  // tile maxima, [query][wg * st]
   const size_t nbytes = (size_t)maxl * PS * 4 * 4;
   if (eng->lists.bytes < lbytes || eng->sample_bound.bytes < sbytes || eng->cand.bytes < cbytes ||
@@ -286,7 +286,6 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   uint64_t* lists = eng->lists.as<uint64_t>();
   float* slabs = eng->cand.as<float>();
   uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + slots * 32);
-  float* slab_max = (float*)((char*)eng->cand.p + slots * 36);
   for (uint32_t p = 0; p < npass; ++p) {
     const uint32_t q0 = p * P;
     const uint32_t nv = std::min(P, nq - q0);
@@ -318,7 +317,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
-                                 slab_tile, slab_max, cap, eng->cand_cnt.as<uint32_t>(), maxl,
+                                 slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl,
                                  &L, eng->stream, allow),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");

@@ -78,10 +78,10 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //    per-query lower bound init_score[q] appends them as one slab
 //    (8 f32, the accumulator layout) and the tile's first global row to the
 //    query's buffer: slabs[nlists][kMfmaQueries][cap][8],
-//    slab_tile[nlists][kMfmaQueries][cap] and each slab's masked maximum
-//    slab_max[..][cap] (cap % 4 == 0, cap >= 4 k: quarter j of a buffer is
-//    lane j's, counts in slabs cand_cnt[nlists][256][4]); a full quarter
-//    keeps its cap / 4 best slabs (exact for k <= cap / 4, never overflows);
+//    slab_tile[nlists][kMfmaQueries][cap] (cap % 4 == 0, cap >= 4 k:
+//    quarter j of a buffer is lane j's, counts in slabs
+//    cand_cnt[nlists][256][4]); a full quarter keeps its cap / 4 best slabs
+//    (exact for k <= cap / 4, never overflows);
 //    launch_select_slabs picks the top k;
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
 //    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; collections
@@ -101,7 +101,7 @@ hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint3
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const float* init_score, float* slabs,
-                            uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
+                            uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow = nullptr);
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
@@ -119,7 +119,7 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint64_t* allow = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
-uint32_t mfma_sample_tiles(uint32_t n_rows);
+uint32_t mfma_sample_tiles(uint32_t n_rows, uint32_t dim = 768, bool f32 = false);
 uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles);
 uint32_t mfma_max_lists(uint32_t n_rows);
 uint32_t mfma_tiles_per_wg(uint32_t n_rows);

@@ -960,7 +960,6 @@ struct MfArgs {
   uint64_t* cand;           // MODE 0: [nwg][kMfmaQueries][cand_cap] slabs of 8 f32 scores
                             // (32 B); quarter kq of a query's buffer belongs to its lane kq
   uint32_t* cand_tile;      // MODE 0: first global row of each slab's tile
-  float* cand_max;          // MODE 0: each slab's (masked) maximum score
   uint32_t* cand_cnt;       // MODE 0: [nwg][kMfmaQueries][4] slabs per quarter
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, cand_cap;
@@ -1082,26 +1081,43 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
   }
 }
 
-// A full quarter of a main-pass candidate buffer (slots [base, base + sub),
-// their masked maximum scores in cand_max): the new slab (scores v0, v1 of
-// global tile row tile, masked maximum mx) replaces the slot whose maximum is
-// smallest -- among equal maxima the latest tile (highest rows) -- if mx is
-// larger. Exact for k <= sub: every slab dropped this way (or never stored)
-// is beaten by sub >= k keys of distinct rows, one per slot kept (a larger
-// score, or an equal score of an earlier, lower-row tile of this
-// workgroup's ascending scan). Rare path; reads back this lane's own stores.
+// A full quarter of a main-pass candidate buffer (slots [base, base + sub)):
+// the new slab (scores v0, v1 of global tile row tile, masked maximum mx)
+// replaces the slot whose masked maximum is smallest -- among equal maxima
+// the latest tile (highest rows) -- if mx is larger. Exact for k <= sub:
+// every slab dropped this way (or never stored) is beaten by sub >= k keys of
+// distinct rows, one per slot kept (a larger score, or an equal score of an
+// earlier, lower-row tile of this workgroup's ascending scan). Rare path: the
+// slots' maxima are recomputed from the stored slabs (8 scores, the filter
+// bits of their rows applied), so the append path stores no maximum.
 template <typename Args>
 __device__ __forceinline__ void mf_replace_min(const Args& a, uint32_t base, uint32_t sub,
                                                f32x4_t v0, f32x4_t v1, uint32_t tile, float mx) {
   // opaque: no address built from it is hoisted out of this rare path into
   // the tile loop (whose registers are all taken)
   asm volatile("" : "+v"(base));
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const uint32_t kq = (tid & 63u) >> 4;  // this lane's rows 4kq+i and 16+4kq+i of a tile
   float msel = INFINITY;
   uint32_t tsel = 0, jsel = 0;
   for (uint32_t j = 0; j < sub; ++j) {
-    const float m = a.cand_max[base + j];
+    const f32x4_t* sl = (const f32x4_t*)a.cand + 2 * (size_t)(base + j);
+    const f32x4_t s0 = sl[0], s1 = sl[1];
     const uint32_t t = a.cand_tile[base + j];
-    // selects, not branches: both loads are consumed on every path
+    uint32_t am = 0xFFu;
+    if (a.allow) {
+      const uint32_t lr = t - a.row_base;  // local first row of the slot's tile
+      const uint32_t tw = (uint32_t)(a.allow[lr >> 6] >> (lr & 32)) >> (4 * kq);
+      am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      m = ((am >> i) & 1u) && s0[i] > m ? s0[i] : m;
+      m = ((am >> (4 + i)) & 1u) && s1[i] > m ? s1[i] : m;
+    }
+    // selects, not branches: every load is consumed on every path
     const bool lt = m < msel || (m == msel && t > tsel);
     msel = lt ? m : msel;
     tsel = lt ? t : tsel;
@@ -1113,7 +1129,6 @@ __device__ __forceinline__ void mf_replace_min(const Args& a, uint32_t base, uin
     sl[0] = v0;
     sl[1] = v1;
     a.cand_tile[e] = tile;
-    a.cand_max[e] = mx;
   }
   // Leave no load of this path outstanding: the compiler's wait analysis
   // merges this path into the tile loop, and a pending load here became an
@@ -1600,7 +1615,6 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             sp[0] = acc[0][g];
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
-            if constexpr ((VAR & 4194304) == 0) a.cand_max[slot] = mx;
             cnt_r[g] = cg + 1;
             if constexpr ((VAR & 262144) != 0) __builtin_amdgcn_s_setprio(0);
           } else {
@@ -1826,7 +1840,7 @@ hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_r
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const float* init_score, float* slabs,
-                            uint32_t* slab_tile, float* slab_max, uint32_t cand_cap,
+                            uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 * k || cand_cap % 4 ||
@@ -1836,7 +1850,7 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_score = init_score, a.cand = (uint64_t*)slabs;
-  a.cand_tile = slab_tile, a.cand_max = slab_max, a.cand_cnt = cand_cnt;
+  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
   return mfma_launch_mode<0>(dim, f32, *nlists, a, st);
@@ -1858,16 +1872,20 @@ uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
   return cap;
 }
 
-uint32_t mfma_sample_tiles(uint32_t n_rows) {
+uint32_t mfma_sample_tiles(uint32_t n_rows, uint32_t dim, bool f32) {
   // 1/128 of every workgroup's tiles, at least 4 when it has 64 or more: with
   // the slab select, whose cost grows with the survivors, 4 instead of 2
   // tiles at 1.25M rows (the N = 8 share) saved 2-3 us per batch (r01). With
   // tile maxima stored as floats (r02) the sample pass costs ~5 us per tile
   // and the select ~1.4 us per 100 survivors per query: at 10M rows 1/128
   // (9 tiles: 61 + 24 us) beats 1/64 (19 tiles: 110 + 16 us;
-  // profiles/r02_sample_tiles_10m.txt).
+  // profiles/r02_sample_tiles_10m.txt). bf16 rows of 1024 / 1536 (128-query
+  // launches, HBM-bound): 1/64, since there every candidate append slows the
+  // stream (5M x 1024: sample + main 1.776 -> 1.735 ms at k = 50 and 1.631
+  // -> 1.603 at k = 10 for 4 -> 8 tiles; profiles/r02_sample_tiles_d1024_*).
   const uint32_t tpw = mfma_tiles_per_wg(n_rows);
-  uint32_t st = tpw / 128;
+  const bool hbm_bound = !f32 && mf_groups_b((int)dim * 2) == 1;
+  uint32_t st = tpw / (hbm_bound ? 64 : 128);
   if (tpw >= 64 && st < 4) st = 4;
   if (st < 1) st = 1;
   if (st > kMfmaMaxSampleTiles) st = kMfmaMaxSampleTiles;

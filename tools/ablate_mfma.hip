@@ -79,9 +79,7 @@ int main(int argc, char** argv) {
   const uint32_t st = st_over ? st_over : mfma_sample_tiles(n), cap = mfma_cand_cap(n, k, st);
   CK(hipMalloc(&cand, (size_t)c.nwg * 256 * cap * 32));  // main-pass slabs
   uint32_t* ctile;
-  float* cmax;
   CK(hipMalloc(&ctile, (size_t)c.nwg * 256 * cap * 4));
-  CK(hipMalloc(&cmax, (size_t)c.nwg * 256 * cap * 4));
   CK(hipMalloc(&tmax, (size_t)c.nwg * 256 * st * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
   CK(hipMalloc(&bnd, 256 * 4));
@@ -105,7 +103,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   MfArgs& g = c.args;
   g.X = X, g.Q = Q, g.init_score = bnd, g.lists = out;
-  g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.cand_max = cmax, g.cand_cap = cap;
+  g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.cand_cap = cap;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
@@ -149,7 +147,6 @@ int main(int argc, char** argv) {
       {"main bf 16k", run<0, 0, 2>, true, {}},              // r02 build before: 16 KiB chunks
       {"main branchy", run<0, 524288, 2>, true, {}},        // r01 conditional stream
       {"bf no-replace", run<0, 2097152, 2>, true, {}},      // full quarter drops (inexact)
-      {"bf no-max", run<0, 2097152 + 4194304, 2>, true, {}},  // + no slab max store (r02a)
       {"main bf stag", run<0, 1048576, 2>, true, {}},       // + waves 4-7 half a chunk ahead
       {"bf ring144", run<0, 256, 2>, true, {}},             // 8 chunks in flight
       {"bf 24k ring144", run<0, 2048 + 256, 2>, true, {}},  // 2 barriers / tile
