@@ -15,14 +15,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCAN = {"c3": "mfma_topk_kernel<768, 0,", "c3b1": "gemv_topk_kernel<768, true, 1",
         "c2": "gemv_topk_kernel<768, false, 1", "c4": "mfma_topk_kernel<768, 0,",
-        "c4b1": "gemv_topk_kernel<768, true, 16"}
+        "c4b1": "gemv_topk_kernel<768, true, 16", "c5b256": "mfma_topk_kernel<1024, 0,"}
 
 
 def main():
     tag, specs = sys.argv[1], sys.argv[2:]
-    out = {"_doc": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (KB, x1024, x2 gfx950 "
+    # entries for configs not re-measured this time are kept
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = json.load(open(p)) if os.path.exists(p) else {}
+    out["_doc"] = ("HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (KB, x1024, x2 gfx950 "
                    "correction: MI355X_MICROARCH.md HBM section), averaged over the scan launches "
-                   "of `python bench.py --config <cfg> --steps 5 --warmup 1`; build " + tag}
+                   "of `python bench.py --config <cfg> --steps 5 --warmup 2`; each entry names "
+                   "its build")
     for spec in specs:
         cfg, path = spec.split("=", 1)
         vals, name = [], None
@@ -34,7 +38,7 @@ def main():
             raise SystemExit(f"no FETCH_SIZE rows for {SCAN[cfg]} in {path}")
         kb = sum(vals) / len(vals)
         out[cfg] = {"kernel": name, "launches": len(vals), "fetch_size_kb_avg": round(kb, 1),
-                    "hbm_bytes_per_launch": int(kb * 1024 * 2)}
+                    "hbm_bytes_per_launch": int(kb * 1024 * 2), "build": tag}
     json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
