@@ -238,7 +238,7 @@ Frame parse_request_head(const char* buf, size_t len, Request* req, size_t* head
 }
 
 Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_length,
-                 std::string* body, size_t* consumed) {
+                 std::string* body, size_t* consumed, ChunkScan* scan) {
   if (!chunked) {
     const size_t cl = content_length > 0 ? (size_t)content_length : 0;
     if (len < cl) return Frame::kNeedMore;
@@ -246,10 +246,11 @@ Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_leng
     *consumed = cl;
     return Frame::kDone;
   }
-  // first pass: framing only (jumps over chunk data, so a retry after more
-  // bytes arrive costs O(chunks)); second pass copies the data
-  size_t pos = 0, total = 0;
-  std::list<std::pair<size_t, size_t>> parts;
+  // framing first (chunks already framed by an earlier call are skipped,
+  // and chunk data is jumped over), then one copy of the data
+  ChunkScan local;
+  ChunkScan& st = scan ? *scan : local;
+  size_t pos = st.pos;
   for (;;) {
     const void* nl = std::memchr(buf + pos, '\n', len - pos);
     if (!nl) return len - pos > 4096 ? Frame::kBad : Frame::kNeedMore;
@@ -269,37 +270,41 @@ Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_leng
     // chunk extensions (";name=value") and the CR are ignored
     if (x < e && buf[x] != ';' && buf[x] != '\r' && buf[x] != ' ' && buf[x] != '\t')
       return Frame::kBad;
-    pos = e + 1;
+    size_t p = e + 1;
     if (sz == 0) {
       // trailer section: header lines up to a blank line
       for (;;) {
-        const void* tl = std::memchr(buf + pos, '\n', len - pos);
+        const void* tl = std::memchr(buf + p, '\n', len - p);
         if (!tl) return Frame::kNeedMore;
         const size_t te = (const char*)tl - buf;
-        const bool blank = te == pos || (te == pos + 1 && buf[pos] == '\r');
-        pos = te + 1;
+        const bool blank = te == p || (te == p + 1 && buf[p] == '\r');
+        p = te + 1;
         if (blank) break;
       }
+      pos = p;
       break;
     }
-    if ((int64_t)(total + sz) > kMaxBodyBytes) return Frame::kBad;
-    if (len - pos < sz + 1) return Frame::kNeedMore;
-    parts.emplace_back(pos, (size_t)sz);
-    total += sz;
-    pos += sz;
-    if (buf[pos] == '\r') {
-      if (len - pos < 2) return Frame::kNeedMore;
-      if (buf[pos + 1] != '\n') return Frame::kBad;
-      pos += 2;
-    } else if (buf[pos] == '\n') {
-      pos += 1;
+    if ((int64_t)(st.total + sz) > kMaxBodyBytes) return Frame::kBad;
+    if (len - p < sz + 1) return Frame::kNeedMore;
+    const size_t data = p;
+    p += sz;
+    if (buf[p] == '\r') {
+      if (len - p < 2) return Frame::kNeedMore;
+      if (buf[p + 1] != '\n') return Frame::kBad;
+      p += 2;
+    } else if (buf[p] == '\n') {
+      p += 1;
     } else {
       return Frame::kBad;
     }
+    // this chunk is complete: record it and resume after it next time
+    st.parts.emplace_back(data, (size_t)sz);
+    st.total += sz;
+    st.pos = pos = p;
   }
   body->clear();
-  body->reserve(total);
-  for (const auto& pr : parts) body->append(buf + pr.first, pr.second);
+  body->reserve(st.total);
+  for (const auto& pr : st.parts) body->append(buf + pr.first, pr.second);
   *consumed = pos;
   return Frame::kDone;
 }
@@ -494,12 +499,16 @@ void serve_conn(vsvc* svc, ConnSlot* cs, const std::atomic<bool>* stop) {
       break;
     }
     off += hl;
-    if (req.content_length > 0) buf.reserve(off + (size_t)req.content_length);
+    // room for the announced body, up to 64 MiB ahead (a larger one grows as
+    // it arrives: a header alone never commits gigabytes)
+    if (req.content_length > 0)
+      buf.reserve(off + std::min<size_t>((size_t)req.content_length, size_t(64) << 20));
     bool sent_continue = false, ok = true;
     size_t used = 0;
+    vshttp::ChunkScan cscan;
     for (;;) {
       const Frame b = vshttp::body_frame(buf.data() + off, buf.size() - off, req.chunked,
-                                         req.content_length, &req.body, &used);
+                                         req.content_length, &req.body, &used, &cscan);
       if (b == Frame::kDone) break;
       if (b == Frame::kBad) {
         send_error_close(fd, 400);

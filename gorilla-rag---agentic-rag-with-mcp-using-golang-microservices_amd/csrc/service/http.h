@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <utility>
+#include <vector>
 
 namespace vshttp {
 
@@ -41,11 +43,21 @@ constexpr int64_t kMaxBodyBytes = int64_t(1) << 32;
 Frame parse_request_head(const char* buf, size_t len, Request* req, size_t* head_len,
                          int* bad_status);
 
+// Progress of framing one chunked body across calls (bytes arrive in
+// pieces): the chunks already framed are not scanned again.
+struct ChunkScan {
+  size_t pos = 0;    // offset of the next chunk-size line
+  size_t total = 0;  // data bytes framed so far
+  std::vector<std::pair<size_t, size_t>> parts;  // (offset, length) of each chunk's data
+};
+
 // Frames a body that starts at buf[0]: Content-Length or chunked (trailers
 // skipped). On kDone, *consumed is the byte count of the framed body and
-// *body the decoded bytes. kBad: malformed chunk framing.
+// *body the decoded bytes. kBad: malformed chunk framing. `scan` (chunked
+// only; nullable) carries the progress between calls on a growing buffer;
+// reset it for every new body.
 Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_length,
-                 std::string* body, size_t* consumed);
+                 std::string* body, size_t* consumed, ChunkScan* scan = nullptr);
 
 // Parses a response head + body (Content-Length, chunked, or none for 1xx /
 // 204 / 304). On kDone, *consumed is the byte count of the whole message.

@@ -144,6 +144,39 @@ def _post(port, body):
     return out
 
 
+def test_vsearch_server_sharded(tmp_path, orc):
+    """VS_DEVICES=0,0: the server's multi-device mode (vs_open_multi, two
+    row-striped shards, here both on the box's one GPU, RCCL with a
+    1-device communicator) answers /search exactly like one device."""
+    assert os.path.exists(SERVER), "run __graft_entry__.build()"
+    cfgp = tmp_path / "cfg.json"
+    cfgp.write_text(json.dumps({"collections": [
+        {"name": "kyc_docs", "dim": 768, "metric": "Cosine", "dtype": "bf16"}]}))
+    n, seed = 30001, 99
+    env = dict(os.environ, PORT="0", VS_SERVICE_CONFIG=str(cfgp), VS_DEVICES="0,0",
+               VS_BULK="kyc_docs=%d:%d" % (n, seed))
+    env.pop("VS_DATA_DIR", None)
+    X = orc.generate(seed, 0, n, 768, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 501, 3, 768)
+    p, port = _start_server(env)
+    try:
+        for i in range(3):
+            for k in (1, 10, 50):
+                st, body = _post(port, {"collection": "kyc_docs", "query": Q[i].tolist(),
+                                        "top_k": k, "filter": None})
+                assert st == 200, body
+                _check_reply(orc, body, X, _bulk_row, Q[i], k, True)
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+        c.request("GET", "/health")
+        r = c.getresponse()
+        assert r.status == 200 and json.loads(r.read())["status"] == "healthy"
+        c.close()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=120)
+    assert p.returncode == 0, err[-2000:]
+
+
 def test_vsearch_server_process(tmp_path, orc):
     """lib/vsearch_server as the vector-service process: bulk rows from
     VS_BULK, /search over HTTP checked against the oracle, SIGTERM writes the

@@ -232,6 +232,23 @@ def test_chunked_body_and_expect_continue(lib, server):
     s.close()
 
 
+def test_chunked_body_in_pieces(lib, server):
+    """Many small chunks arriving in separate segments: the framing resumes
+    where it stopped (csrc/service/http.cpp ChunkScan) and decodes exactly."""
+    body = _search_body(91, "kyc", 12)
+    want = lib.handle("POST", "/search", body)[1]
+    enc = b"".join(b"%x\r\n%s\r\n" % (len(body[i:i + 7]), body[i:i + 7])
+                   for i in range(0, len(body), 7)) + b"0\r\n\r\n"
+    s = _raw(server)
+    s.sendall(b"POST /search HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n")
+    for i in range(0, len(enc), 1000):
+        s.sendall(enc[i:i + 1000])
+        time.sleep(0.002)
+    st, hdr, got, _ = _read_response(s)
+    assert st == 200 and got == want
+    s.close()
+
+
 def test_head_and_connection_close(lib, server):
     s = _raw(server)
     s.sendall(b"HEAD /health HTTP/1.1\r\nHost: x\r\n\r\n")
