@@ -128,10 +128,15 @@ def _bulk_row(uid):
 def _start_server(env):
     p = subprocess.Popen([SERVER], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                          text=True)
-    line = p.stdout.readline()
+    seen = []
+    for _ in range(50):  # RCCL prints its version line first in the multi-device mode
+        line = p.stdout.readline()
+        seen.append(line)
+        if "starting on port" in line or not line:
+            break
     if "starting on port" not in line:
         p.kill()
-        raise AssertionError("server did not start: %r %s" % (line, p.stderr.read()[-2000:]))
+        raise AssertionError("server did not start: %r %s" % (seen, p.stderr.read()[-2000:]))
     return p, int(line.split()[-1])
 
 

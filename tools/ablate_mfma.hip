@@ -159,7 +159,10 @@ int main(int argc, char** argv) {
   // VS_ABL_SET=lds: what the A-fragment LDS reads cost (no epilogue in the
   // MODE 1 / 7 / 10 arms: all reads, hr 0 only = half the reads, one
   // fragment set reused = almost none)
-  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "barrier")) {
+  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "product")) {
+    // the product main pass alone (sample-tile sweeps: argv[3])
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "barrier")) {
     // timing only: without the barrier the ring is unsynchronised (wrong
     // results, no hazard to the device: no waits depend on the data)
     arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
