@@ -44,6 +44,17 @@ Batcher::~Batcher() {
   for (auto& t : workers_) t.join();
 }
 
+namespace {
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+std::chrono::steady_clock::time_point deadline_in(int64_t us) {
+  return std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+}
+}  // namespace
+
 int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint32_t k,
                     float* scores, uint64_t* rows, uint32_t* count, std::string* err,
                     uint64_t filter_id) {
@@ -55,11 +66,49 @@ int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint3
     if (err) *err = "service is closing";
     return VS_ERR_INVALID_ARG;
   }
-  queue_.push_back(&r);
-  cv_.notify_all();
-  done_cv.wait(lk, [&] { return r.done; });
+  if (opt_.caller_runs && !opt_.max_wait_us && queue_.empty() && inflight_end_.empty()) {
+    // Nothing queued and nothing in flight: run this request on the calling
+    // thread (no hand-off to a worker and back: two thread wake-ups less on
+    // an idle service). Requests arriving meanwhile queue as usual and the
+    // workers treat this call as one in flight.
+    std::vector<Req*> batch{&r};
+    const int64_t t0 = now_us(), end = begin_call(coll, t0);
+    lk.unlock();
+    execute(batch);
+    lk.lock();
+    end_call(coll, t0, end);
+    cv_.notify_all();
+  } else {
+    queue_.push_back(&r);
+    cv_.notify_all();
+    done_cv.wait(lk, [&] { return r.done; });
+  }
   if (r.rc != VS_OK && err) *err = r.err;
   return r.rc;
+}
+
+// (mu_ held) registers a call of `coll` starting at t0: the device runs the
+// calls in flight one after another, so it starts when the ones ahead of it
+// are expected to end, and takes its collection's recent service time.
+// Returns its expected end.
+int64_t Batcher::begin_call(const std::string& coll, int64_t t0) {
+  auto est = call_us_.find(coll);
+  gpu_free_at_ = std::max(gpu_free_at_, t0) + (int64_t)(est == call_us_.end() ? 0.0 : est->second);
+  inflight_end_.push_back(gpu_free_at_);
+  return gpu_free_at_;
+}
+
+// (mu_ held) the call registered as (t0, end) returned: its service time
+// (from its start, or from the previous call's end when it queued behind
+// one) updates the collection's average.
+void Batcher::end_call(const std::string& coll, int64_t t0, int64_t end) {
+  const int64_t t1 = now_us();
+  const double took = (double)(t1 - std::max(t0, last_done_));
+  last_done_ = t1;
+  double& avg = call_us_[coll];
+  avg = avg == 0.0 ? took : 0.8 * avg + 0.2 * took;
+  inflight_end_.erase(std::find(inflight_end_.begin(), inflight_end_.end(), end));
+  if (inflight_end_.empty()) gpu_free_at_ = 0;
 }
 
 Stats Batcher::stats() {
@@ -67,16 +116,6 @@ Stats Batcher::stats() {
   return stats_;
 }
 
-namespace {
-int64_t now_us() {
-  return std::chrono::duration_cast<std::chrono::microseconds>(
-             std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-std::chrono::steady_clock::time_point deadline_in(int64_t us) {
-  return std::chrono::steady_clock::now() + std::chrono::microseconds(us);
-}
-}  // namespace
 
 void Batcher::run() {
   std::unique_lock<std::mutex> lk(mu_);
@@ -120,28 +159,12 @@ void Batcher::run() {
         ++it;
       }
     }
-    // expected end of this call: the device runs the calls in flight one
-    // after another, so it starts when the ones ahead of it are expected to
-    // end, and takes its collection's recent service time
     const std::string coll = *first->coll;
-    const int64_t t0 = now_us();
-    auto est = call_us_.find(coll);
-    gpu_free_at_ = std::max(gpu_free_at_, t0) +
-                   (int64_t)(est == call_us_.end() ? 0.0 : est->second);
-    const int64_t end = gpu_free_at_;
-    inflight_end_.push_back(end);
+    const int64_t t0 = now_us(), end = begin_call(coll, t0);
     lk.unlock();
     execute(batch);
     lk.lock();
-    // service time: from its start, or from the previous call's end when it
-    // was queued behind one
-    const int64_t t1 = now_us();
-    const double took = (double)(t1 - std::max(t0, last_done_));
-    last_done_ = t1;
-    double& avg = call_us_[coll];
-    avg = avg == 0.0 ? took : 0.8 * avg + 0.2 * took;
-    inflight_end_.erase(std::find(inflight_end_.begin(), inflight_end_.end(), end));
-    if (inflight_end_.empty()) gpu_free_at_ = 0;
+    end_call(coll, t0, end);
     for (Req* r : batch) {
       r->done = true;
       r->cv->notify_one();

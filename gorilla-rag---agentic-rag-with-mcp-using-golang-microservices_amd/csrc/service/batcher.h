@@ -55,6 +55,10 @@ struct Options {
   // not at once: requests arriving meanwhile still join, so pipelining the
   // calls does not shrink the batches (0 = form at once)
   uint32_t lead_us = 300;
+  // a request that finds nothing queued and nothing in flight runs on the
+  // calling thread instead of being handed to a worker (not with a linger:
+  // max_wait_us asks for batches to be waited for)
+  bool caller_runs = true;
 };
 
 struct Stats {
@@ -85,6 +89,8 @@ class Batcher {
   struct Req;
   void run();
   void execute(std::vector<Req*>& batch);
+  int64_t begin_call(const std::string& coll, int64_t t0);
+  void end_call(const std::string& coll, int64_t t0, int64_t end);
 
   vs_engine* eng_;
   Options opt_;

@@ -670,7 +670,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
       filter_match = fm->str == "match";
     }
     // {"batching": {"enabled": bool, "max_batch": n, "max_wait_us": n, "workers": n,
-    //               "lead_us": n}}
+    //               "lead_us": n, "caller_runs": bool}}
     if (const Json* b = cfg.get("batching")) {
       if (b->kind != Json::Object) return VS_ERR_INVALID_ARG;
       if (const Json* e = b->get("enabled")) {
@@ -688,6 +688,10 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
       if (const Json* w = b->get("max_wait_us")) {
         if (w->kind != Json::Number || w->num < 0 || w->num > 1e6) return VS_ERR_INVALID_ARG;
         bopt.max_wait_us = (uint32_t)w->num;
+      }
+      if (const Json* cr = b->get("caller_runs")) {
+        if (cr->kind != Json::Bool) return VS_ERR_INVALID_ARG;
+        bopt.caller_runs = cr->b;
       }
       if (const Json* l = b->get("lead_us")) {
         if (l->kind != Json::Number || l->num < 0 || l->num > 1e6) return VS_ERR_INVALID_ARG;
@@ -910,6 +914,7 @@ int vsvc_stats(vsvc* svc, char** out) {
   b.obj.emplace_back("max_wait_us", Json::number(svc->batch_opt.max_wait_us));
   b.obj.emplace_back("workers", Json::number(svc->batch_opt.workers));
   b.obj.emplace_back("lead_us", Json::number(svc->batch_opt.lead_us));
+  b.obj.emplace_back("caller_runs", Json::boolean(svc->batch_opt.caller_runs));
   o.obj.emplace_back("batching", std::move(b));
   o.obj.emplace_back("requests", Json::number((double)st.requests));
   o.obj.emplace_back("engine_calls", Json::number((double)st.engine_calls));

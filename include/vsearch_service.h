@@ -40,7 +40,7 @@ typedef struct vsvc vsvc;
  * {"collections":[{"name":"..","dim":768,"metric":"Cosine"|"Dot",
  *  "dtype":"f32"|"bf16"}...],
  *  "batching":{"enabled":true,"max_batch":256,"max_wait_us":0,"workers":2,
- *              "lead_us":300},
+ *              "lead_us":300,"caller_runs":true},
  *  "filter":"ignore"|"match"}.
  * "filter":"ignore" (default) keeps the reference's behaviour: the request's
  * `filter` is decoded and dropped (main.go:30 vs :249-254). "match" applies
@@ -52,7 +52,8 @@ typedef struct vsvc vsvc;
  * engine call per collection (and per filter, for filtered requests)
  * (csrc/service/batcher.h); each request still gets exactly its own top k.
  * With 2 workers two calls are in flight (the second enqueued while the
- * first runs, its batch formed lead_us before the first is expected to end). */
+ * first runs, its batch formed lead_us before the first is expected to end);
+ * a request meeting an idle batcher runs on its own thread (caller_runs). */
 int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out);
 void vsvc_close(vsvc* svc);
 

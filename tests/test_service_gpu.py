@@ -266,7 +266,8 @@ def test_batcher_disabled(pkg, svcmod, orc):
         st, body, _ = _post(s, "/search", {"collection": "b16", "query": Xp[7].tolist(), "top_k": 3})
         assert st == 200 and json.loads(body)["results"][0]["id"] == ids[7]
         assert s.stats() == {"batching": {"enabled": False, "max_batch": 256, "max_wait_us": 0,
-                                          "workers": 2, "lead_us": 300},
+                                          "workers": 2, "lead_us": 300,
+                                          "caller_runs": True},
                              "requests": 0, "engine_calls": 0, "largest_call": 0,
                              "calls_by_log2_nq": [0] * 10}
     finally:
