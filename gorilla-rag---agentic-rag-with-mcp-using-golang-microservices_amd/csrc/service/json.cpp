@@ -168,7 +168,11 @@ struct Parser {
     }
     out->kind = Json::Number;
     out->str.assign(s + st, i - st);
-    out->num = std::strtod(out->str.c_str(), nullptr);
+    // correctly rounded either way; from_chars is ~4x faster than strtod
+    // (no locale), which matters for 768-number query bodies. Out of range
+    // (overflow to inf, underflow) keeps strtod's IEEE result.
+    const auto r = std::from_chars(s + st, s + i, out->num);
+    if (r.ec != std::errc() || r.ptr != s + i) out->num = std::strtod(out->str.c_str(), nullptr);
     return true;
   }
   bool value(Json* out) {
@@ -207,9 +211,8 @@ struct Parser {
         ws();
         if (i < n && s[i] == ']') { ++i; ok = true; break; }
         while (true) {
-          Json v;
-          if (!value(&v)) { ok = false; break; }
-          out->arr.push_back(std::move(v));
+          out->arr.emplace_back();  // parsed in place: no element copy per value
+          if (!value(&out->arr.back())) { ok = false; break; }
           ws();
           if (i < n && s[i] == ',') { ++i; continue; }
           if (i < n && s[i] == ']') { ++i; ok = true; break; }
@@ -369,6 +372,16 @@ void encode(const Json& v, std::string* o, bool sort_keys) {
 }
 
 bool parse_float32(const std::string& lit, float* out) {
+  // Go's ParseFloat(s, 32): the correctly rounded float32. Fast path
+  // from_chars; anything it does not take cleanly (out of range either way)
+  // goes through strtof, which tells overflow (an error in Go) from
+  // underflow (not one).
+  float f;
+  const auto r = std::from_chars(lit.data(), lit.data() + lit.size(), f);
+  if (r.ec == std::errc() && r.ptr == lit.data() + lit.size()) {
+    *out = f;
+    return true;
+  }
   errno = 0;
   char* end = nullptr;
   float v = std::strtof(lit.c_str(), &end);
