@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)atol(argv[1]) : 10000000u;
   const int reps = argc > 2 ? atoi(argv[2]) : 8;
   const uint32_t st_over = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;  // sample tiles override
-  const uint32_t k = 10;
+  const uint32_t k = getenv("VS_ABL_K") ? (uint32_t)atoi(getenv("VS_ABL_K")) : 10u;
   uint16_t *X, *Q;
   uint64_t *out, *cand;
   float *tmax, *bnd;
