@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -783,6 +784,21 @@ uint64_t popcount_rows(const uint64_t* allow, uint64_t rows) {
   return allowed + (uint64_t)__builtin_popcountll(w);
 }
 
+// Waits for a search's completion event: polled for up to kSpinUs (a small
+// collection's search completes within tens of microseconds, and a blocking
+// wait adds the thread's wake-up to its latency), then a blocking wait (a
+// long scan does not keep a host core busy).
+constexpr int64_t kSpinUs = 60;
+hipError_t wait_event(hipEvent_t ev) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q != hipErrorNotReady) return q;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
+  }
+  return hipEventSynchronize(ev);
+}
+
 int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t nq,
                 uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count,
@@ -859,7 +875,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   // wait for the device outside work_mu: the next call (q_in, keys and every
   // scratch buffer are ordered on the same stream) enqueues behind this one
   g.unlock();
-  const hipError_t we = hipEventSynchronize(hs->done);
+  const hipError_t we = wait_event(hs->done);
   if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
   g.lock();
   hs->busy = false;
