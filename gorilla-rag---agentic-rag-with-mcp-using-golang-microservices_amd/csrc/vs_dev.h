@@ -134,6 +134,7 @@ struct DevEngine {
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound, upsert_vecs, upsert_rows;
   DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
+  DevBuf merge_tmp;                 // first stage of a two-stage GEMV merge
   DevBuf scand;                     // MFMA sample pass tile maxima
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered

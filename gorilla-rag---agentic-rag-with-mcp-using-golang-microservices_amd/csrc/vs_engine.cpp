@@ -214,6 +214,18 @@ int device_checksum(DevEngine* eng, const Collection& c, uint64_t* out) {
 // -> keys d_keys[i * k], one scan + merge per query. For bf16 collections qp
 // already holds bf16-rounded values (search_core's query prep). With `gather`
 // (n_gather device row indices) only those rows are scanned.
+// Workgroups of the first stage of a two-stage merge of L lists of k keys
+// (1 = one stage). The one-workgroup merge's fast paths cover up to 8192
+// keys at k <= 32; past that (large k over many lists) a first stage of G
+// workgroups, each over L / G lists, runs the merge in parallel. G divides
+// L and leaves >= 8 lists per group.
+uint32_t merge_groups(uint32_t L, uint32_t k) {
+  if (k <= 32 || (uint64_t)L * k <= 8192) return 1;
+  for (uint32_t g = 64; g >= 4; --g)
+    if (L % g == 0 && L / g >= 8) return g;
+  return 1;
+}
+
 int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr,
                 const uint32_t* gather = nullptr, uint32_t n_gather = 0) {
@@ -223,9 +235,11 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
   const uint32_t row_base = (uint32_t)c.row_base;
   const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, n_rows, k);
   const size_t lbytes = (size_t)maxl * k * 8;
-  if (eng->lists.bytes < lbytes) {
+  const size_t mbytes = (size_t)64 * k * 8;  // two-stage merge: <= 64 groups
+  if (eng->lists.bytes < lbytes || eng->merge_tmp.bytes < mbytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
+    VS_HIP(eng->merge_tmp.ensure(mbytes), "alloc merge scratch");
   }
   for (uint32_t i = q0; i < q0 + n; ++i) {
     uint32_t L = 0;
@@ -235,9 +249,23 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
            "gemv scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-    VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
-                             d_keys + (size_t)(i - q0) * k, eng->stream),
-           "merge");
+    const uint32_t G = merge_groups(L, k);
+    if (G > 1) {
+      // two stages: G workgroups each take the top k of L / G lists, then
+      // one merges the G lists (exact: the global top k is among the groups'
+      // top k). One workgroup over 768 x 100 keys took 195 us (12.5M rows,
+      // k = 100: 6% of the step).
+      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L / G, k, (uint64_t)(L / G) * k, G, k,
+                               k, eng->merge_tmp.as<uint64_t>(), eng->stream),
+             "merge (groups)");
+      VS_HIP(vsk::launch_merge(eng->merge_tmp.as<uint64_t>(), G, k, 0, 1, k, k,
+                               d_keys + (size_t)(i - q0) * k, eng->stream),
+             "merge");
+    } else {
+      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
+                               d_keys + (size_t)(i - q0) * k, eng->stream),
+             "merge");
+    }
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
   }
   return VS_OK;
