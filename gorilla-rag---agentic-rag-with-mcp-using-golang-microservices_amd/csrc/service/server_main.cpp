@@ -15,7 +15,8 @@
 //   VS_DATA_DIR        restore every collection snapshotted there at start,
 //                      snapshot all of them there on SIGINT / SIGTERM (what
 //                      Qdrant's storage volume gives the reference,
-//                      docker-compose.yml)
+//                      docker-compose.yml); VS_SNAPSHOT_DIR is an alias (the
+//                      Go service's name, go/vector-service/main.go)
 //   VS_BULK            "coll=rows[:seed],..." synthetic bulk rows per
 //                      collection at start (benchmark corpora, vsvc_bulk_generate)
 // Prints "Vector Service starting on port <PORT>" (main.go:76) once listening.
@@ -95,7 +96,8 @@ int main() {
   rc = vsvc_open(eng, config.empty() ? nullptr : config.c_str(), &svc);
   if (rc != VS_OK) return fail("vsvc_open", rc);
 
-  const std::string data_dir = get_env("VS_DATA_DIR", "");
+  // VS_SNAPSHOT_DIR is the Go service's name for it (go/vector-service/main.go)
+  const std::string data_dir = get_env("VS_DATA_DIR", get_env("VS_SNAPSHOT_DIR", "").c_str());
   if (!data_dir.empty()) {
     ::mkdir(data_dir.c_str(), 0755);
     rc = vsvc_restore(svc, data_dir.c_str());
