@@ -212,6 +212,53 @@ int main(int argc, char** argv) {
     printf("%-16s median %.3f ms  min %.3f ms  HBM %.0f GB/s  MFMA %.0f TF/s\n", arm.name, med,
            arm.t[0], bytes / med / 1e6, flops / med / 1e9);
   }
+  // VS_ABL_OVERLAP=1: what pipelining batches would save -- B iterations of
+  // [main pass; sample pass + bound of the next batch] on one stream against
+  // the sample pass on a second stream, free to start on the CUs the main
+  // pass's workgroups leave early (tmax / bound of its own: no hazard)
+  if (getenv("VS_ABL_OVERLAP")) {
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    float* tmax2;
+    float* bnd2;
+    CK(hipMalloc(&tmax2, (size_t)c.nwg * 256 * st * 4));
+    CK(hipMalloc(&bnd2, 256 * 4));
+    hipEvent_t e_main;
+    CK(hipEventCreateWithFlags(&e_main, hipEventDisableTiming));
+    const int B = 16;
+    for (int rep = 0; rep < 4; ++rep) {
+      for (int mode = 0; mode < 2; ++mode) {
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < B; ++i) {
+          MfArgs m = c.args;
+          hipLaunchKernelGGL((mfma_topk_kernel<768, 0, 2048 + 256, 2>), dim3(c.nwg), dim3(512), 0, 0,
+                             m);
+          hipStream_t ss = mode ? s2 : (hipStream_t)0;
+          if (mode) {  // the next batch's sample may not pass this batch's main on s2's side
+            CK(hipEventRecord(e_main, 0));
+          }
+          uint32_t L2 = 0;
+          CK(launch_mfma_sample(X, false, 768, n, 0, Q, 256, k, st, tmax2, c.nwg, &L2, ss));
+          CK(launch_sample_bound(tmax2, L2 * st, 256, k, bnd2, ss));
+          if (mode) {
+            hipEvent_t e_s;
+            CK(hipEventCreateWithFlags(&e_s, hipEventDisableTiming));
+            CK(hipEventRecord(e_s, s2));
+            CK(hipStreamWaitEvent(0, e_s, 0));  // the next main pass waits for this bound
+            CK(hipEventDestroy(e_s));
+          }
+        }
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("overlap rep %d %-10s %.3f ms per [main + sample + bound]\n", rep,
+               mode ? "2 streams" : "1 stream", ms / B);
+      }
+    }
+    return 0;
+  }
   // the main pass once more, then its select (timed) and, on the host, how
   // many slab keys pass the select's first bound per query
   {
