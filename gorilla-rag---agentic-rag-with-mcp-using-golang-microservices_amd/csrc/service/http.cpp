@@ -356,7 +356,8 @@ Frame parse_response(const char* buf, size_t len, Response* resp, size_t* consum
   return f;
 }
 
-std::string response_head(int status, const char* content_type, size_t body_len, bool close) {
+std::string response_head(int status, const char* content_type, size_t body_len, bool close,
+                          bool keep_alive_10) {
   static const char* kDay[] = {"Sun", "Mon", "Tue", "Wed", "Thu", "Fri", "Sat"};
   static const char* kMon[] = {"Jan", "Feb", "Mar", "Apr", "May", "Jun",
                                "Jul", "Aug", "Sep", "Oct", "Nov", "Dec"};
@@ -386,6 +387,7 @@ std::string response_head(int status, const char* content_type, size_t body_len,
   h += std::to_string(body_len);
   h += "\r\n";
   if (close) h += "Connection: close\r\n";
+  if (keep_alive_10) h += "Connection: keep-alive\r\n";  // an HTTP/1.0 client asked for it
   h += "\r\n";
   return h;
 }
@@ -542,7 +544,8 @@ void serve_conn(vsvc* svc, ConnSlot* cs, const std::atomic<bool>* stop) {
       send_error_close(fd, 500);
       break;
     }
-    std::string out = vshttp::response_head(status, ct, rlen, !req.keep_alive);
+    std::string out = vshttp::response_head(status, ct, rlen, !req.keep_alive,
+                                            req.minor == 0 && req.keep_alive);
     if (!head) out.append(resp, rlen);
     vsvc_free(resp);
     req.body.clear();

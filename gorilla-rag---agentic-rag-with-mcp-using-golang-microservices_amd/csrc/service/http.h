@@ -68,7 +68,10 @@ const char* status_text(int status);
 
 // Serialises a response head: status line, Content-Type, Date, Content-Length
 // and, for text/plain bodies (http.Error), X-Content-Type-Options: nosniff.
-std::string response_head(int status, const char* content_type, size_t body_len, bool close);
+// keep_alive_10: an HTTP/1.0 request asked to keep the connection
+// ("Connection: keep-alive" is echoed, as net/http does).
+std::string response_head(int status, const char* content_type, size_t body_len, bool close,
+                          bool keep_alive_10 = false);
 
 // Blocking helpers over a connected socket. send_all uses MSG_NOSIGNAL.
 bool send_all(int fd, const char* p, size_t n);

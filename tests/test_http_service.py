@@ -274,6 +274,15 @@ def test_head_and_connection_close(lib, server):
     st, hdr, body, _ = _read_response(s)
     assert st == 200 and _closed(s)
     s.close()
+    # HTTP/1.0 with keep-alive: echoed, and the connection serves a second request
+    s = _raw(server)
+    s.sendall(b"GET /health HTTP/1.0\r\nConnection: keep-alive\r\n\r\n")
+    st, hdr, body, rest = _read_response(s)
+    assert st == 200 and hdr.get("connection") == "keep-alive"
+    s.sendall(b"GET /collections HTTP/1.0\r\n\r\n")
+    st, hdr, body, _ = _read_response(s, rest)
+    assert st == 200 and _closed(s)
+    s.close()
 
 
 @pytest.mark.parametrize("req,status", [
