@@ -120,6 +120,57 @@ def test_http_listener_gpu(pkg, svcmod, orc):
         eng.close()
 
 
+def test_c1_over_http(pkg, svcmod, orc):
+    """Config C1 end to end over HTTP with the reference's defaults (3 x 768
+    Cosine fp32 collections): ingest-service's /upsert bodies (2 documents x
+    110 chunks + 1, payload text / document_id / position) posted to the
+    listener, then retrieval-service's /search bodies (top_k 5, and top_k 0
+    -> 5) checked against the oracle; every HTTP reply equals the in-process
+    handler's bytes."""
+    eng = pkg.VectorEngine(device=0)
+    s = svcmod.VectorService(eng)
+    try:
+        n, dim = 221, 768
+        X = orc.generate(4040, 0, n, dim) * 3.0  # not unit: the upsert normalises
+        ids = _ids(n, 4040)
+        docs = [(0, 110, "doc-a"), (110, 220, "doc-b"), (220, 221, "test_doc")]
+        with s.serve("127.0.0.1:0") as lis:
+            c = http.client.HTTPConnection("127.0.0.1", lis.port, timeout=60)
+            for lo, hi, doc in docs:
+                body = json.dumps({"collection": "regulatory_docs", "points": [
+                    {"id": ids[i], "vector": [float(x) for x in X[i]],
+                     "payload": {"text": f"chunk {i} of {doc}", "document_id": doc,
+                                 "position": i - lo}} for i in range(lo, hi)]})
+                c.request("POST", "/upsert", body=body,
+                          headers={"Content-Type": "application/json"})
+                r = c.getresponse()
+                out = json.loads(r.read())
+                assert r.status == 200 and out == {"collection": "regulatory_docs",
+                                                   "points": hi - lo, "status": "success"}
+            Xp = orc.preprocess(X, True, False)
+            pos = {u: j for j, u in enumerate(ids)}
+            Q = orc.generate(orc.SEED_QUERY, 4041, 6, dim)
+            for i in range(6):
+                top_k = 0 if i == 5 else 5
+                body = json.dumps({"collection": "regulatory_docs", "filter": None,
+                                   "query": [float(x) for x in Q[i]], "top_k": top_k})
+                c.request("POST", "/search", body=body,
+                          headers={"Content-Type": "application/json"})
+                r = c.getresponse()
+                got = r.read()
+                assert r.status == 200
+                res = _check_reply(orc, got, Xp, pos.__getitem__, Q[i], 5, False)
+                for hit in res["results"]:
+                    j = pos[hit["id"]]
+                    doc = "doc-a" if j < 110 else ("doc-b" if j < 220 else "test_doc")
+                    assert hit["payload"]["document_id"] == doc
+                assert got == s.handle("POST", "/search", body.encode())[1]
+            c.close()
+    finally:
+        s.close()
+        eng.close()
+
+
 def _bulk_row(uid):
     g = uid.split("-")
     return ((int(g[3], 16) << 48) | int(g[4], 16)) & ((1 << 62) - 1)
