@@ -51,6 +51,7 @@ class _Lib:
         L.vsvc_http_port.argtypes = [vp]
         L.vsvc_http_stop.argtypes = [vp]
         L.vsvc_loadgen.argtypes = [vp, cp, ctypes.POINTER(vp)]
+        L.vsvc_stats.argtypes = [vp, ctypes.POINTER(vp)]
         self.L = L
         self.eng = vp()
         assert L.vs_open(None, ctypes.byref(self.eng)) == 0
@@ -65,6 +66,13 @@ class _Lib:
         data = ctypes.string_at(out.value, n.value)
         self.L.vsvc_free(out)
         return st.value, data, ct.value.decode()
+
+    def stats(self):
+        out = ctypes.c_void_p()
+        assert self.L.vsvc_stats(self.svc, ctypes.byref(out)) == 0
+        d = json.loads(ctypes.string_at(out.value))
+        self.L.vsvc_free(out)
+        return d
 
     def serve(self, addr=b"127.0.0.1:0"):
         h = ctypes.c_void_p()
@@ -376,3 +384,31 @@ def test_bad_address_and_stop_with_idle_connections(lib):
         s.close()
     with pytest.raises(OSError):
         socket.create_connection(("127.0.0.1", port), timeout=2).recv(1)
+
+
+def test_batcher_policies_over_http(lib, server):
+    """The batcher seen through the listener (csrc/service/batcher.h): a lone
+    request on an idle batcher runs as its own engine call (caller_runs);
+    concurrent keep-alive clients are coalesced into multi-query calls, two
+    in flight, each request still answered with exactly its own top k."""
+    st0 = lib.stats()
+    assert st0["batching"]["workers"] == 2 and st0["batching"]["caller_runs"]
+    c = http.client.HTTPConnection("127.0.0.1", server, timeout=30)
+    for i in range(10):
+        b = _search_body(5000 + i, "docs", 4)
+        c.request("POST", "/search", body=b)
+        r = c.getresponse()
+        assert r.status == 200 and r.read() == lib.handle("POST", "/search", b)[1]
+    c.close()
+    st1 = lib.stats()
+    # each sequential request (and each in-process check after it) was alone
+    assert st1["requests"] - st0["requests"] == 20
+    assert st1["engine_calls"] - st0["engine_calls"] == 20
+    rc, rep = lib.loadgen({"collections": ["docs", "kyc"], "dim": DIM, "clients": 32,
+                           "seconds": 0.6, "k_min": 1, "k_max": 60,
+                           "http": "127.0.0.1:%d" % server}, svc=False)
+    assert rc == 0 and rep["errors"] == 0, rep
+    st2 = lib.stats()
+    calls = st2["engine_calls"] - st1["engine_calls"]
+    reqs = st2["requests"] - st1["requests"]
+    assert reqs == rep["requests"] and calls < reqs and st2["largest_call"] >= 2, (st2, rep)
