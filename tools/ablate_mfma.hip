@@ -159,7 +159,14 @@ int main(int argc, char** argv) {
   // VS_ABL_SET=lds: what the A-fragment LDS reads cost (no epilogue in the
   // MODE 1 / 7 / 10 arms: all reads, hr 0 only = half the reads, one
   // fragment set reused = almost none)
-  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "product")) {
+  if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "g4")) {
+    // one wave per SIMD, 64 queries each (half the A-fragment LDS reads), on
+    // the product's 24 KiB chunks / 144 KiB ring, against the product layout
+    arms = {{"no-epi (product)", run<1, 2048 + 256, 2>, false, {}},
+            {"no-epi G4 pd1", run<1, 2048 + 256, 4>, false, {}},
+            {"no-epi G4 pd3 pin", run<1, 2048 + 256 + 64 + 128, 4>, false, {}},
+            {"no-epi G4 pd2 pin", run<1, 2048 + 256 + 32 + 128, 4>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "product")) {
     // the product main pass alone (sample-tile sweeps: argv[3])
     arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}}};
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "barrier")) {
