@@ -23,6 +23,14 @@
 // with several collections each call finds its collection's whole backlog.
 // max_wait_us > 0 adds a linger before a non-full batch.
 //
+// Two calls in flight (Options::workers = 2, lead_us): the engine waits for
+// the device outside its lock, so a second worker's call runs on the device
+// right behind the first; that worker forms its batch only lead_us before
+// the first call is expected to end (each collection's recent service
+// time), so the batches stay as large as with one worker. A request meeting
+// an idle batcher (nothing queued or in flight) runs on its own thread
+// (caller_runs): no hand-off to a worker and back.
+//
 // Filtered requests ("filter":"match") carry the id of their device-resident
 // filter (vs_filter_create) and are grouped by it too: requests sharing a
 // filter become one vs_search_filter_id call (the MFMA pass with the bitmap
