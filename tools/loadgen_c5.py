@@ -32,7 +32,11 @@ def main():
     ap.add_argument("--lead-us", type=int, default=300,
                     help="late batch formation with a call in flight (batcher.h)")
     ap.add_argument("--transport", default="inproc", choices=["inproc", "http", "both"])
+    ap.add_argument("--server", action="store_true",
+                    help="serve from a separate lib/vsearch_server process (HTTP only)")
     args = ap.parse_args()
+    if args.server:
+        return run_server(args)
     import torch  # noqa: F401  (binds torch's HIP runtime first, as bench.py does)
     import __graft_entry__ as ge
     from importlib import import_module
@@ -83,6 +87,71 @@ def main():
             lis.stop()
         svc.close()
         eng.close()
+
+
+def run_server(args):
+    """C5 against the vector-service process: lib/vsearch_server holds the
+    three collections (VS_BULK) and serves them on a port; this process only
+    drives retrieval-service-shaped HTTP load at it (vsvc_loadgen's client,
+    no engine here)."""
+    import ctypes
+    import json as js
+    import signal
+    import subprocess
+    import tempfile
+    import __graft_entry__ as ge
+    from importlib import import_module
+    pkg = ge.load_package()
+    svcmod = import_module(pkg.__name__ + ".service")
+    L = svcmod.load_service_library()
+    names = ["regulatory_docs", "merchant_docs", "kyc_docs"]
+    cfg = {"collections": [{"name": n, "dim": args.dim, "metric": "Cosine", "dtype": "bf16"}
+                           for n in names],
+           "batching": {"workers": args.workers, "lead_us": args.lead_us}}
+    d = tempfile.mkdtemp(prefix="c5srv")
+    cfgp = os.path.join(d, "cfg.json")
+    open(cfgp, "w").write(js.dumps(cfg))
+    env = dict(os.environ, PORT="0", VS_SERVICE_CONFIG=cfgp,
+               VS_BULK=",".join(f"{n}={args.rows}:{0x5EED + i}" for i, n in enumerate(names)))
+    server = os.path.join(os.path.dirname(svcmod.SVC_LIB_PATH), "vsearch_server")
+    t0 = time.time()
+    p = subprocess.Popen([server], env=env, stdout=subprocess.PIPE, text=True)
+    port = None
+    for _ in range(50):
+        line = p.stdout.readline()
+        if "starting on port" in line:
+            port = int(line.split()[-1])
+            break
+        if not line:
+            break
+    if port is None:
+        p.kill()
+        raise SystemExit("vsearch_server did not start")
+    print(f"[c5] vsearch_server on port {port}, {len(names)} x {args.rows} x {args.dim} bf16 "
+          f"in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    try:
+        for clients in [int(c) for c in args.clients.split(",")]:
+            for secs, seed in ((0.5, 1), (args.seconds, clients)):
+                spec = {"collections": names, "dim": args.dim, "clients": clients,
+                        "seconds": secs, "k_min": 3, "k_max": 50, "seed": seed,
+                        "http": f"127.0.0.1:{port}"}
+                out = ctypes.c_void_p()
+                rc = L.vsvc_loadgen(None, js.dumps(spec).encode(), ctypes.byref(out))
+                if rc != 0:
+                    raise SystemExit(f"loadgen failed: {rc}")
+                rep = js.loads(ctypes.string_at(out.value))
+                L.vsvc_free(out)
+            line = {"workload": f"C5: 3 x {args.rows} x {args.dim} bf16, k in [3,50], closed "
+                                "loop, HTTP clients -> vsearch_server process",
+                    "transport": "http (separate server process)", "clients": clients,
+                    "workers": args.workers, "lead_us": args.lead_us,
+                    "qps": round(rep["qps"], 1), "requests": rep["requests"],
+                    "errors": rep["errors"], "first_error": rep["first_error"][:200],
+                    "lat_ms": {k: round(v, 3) for k, v in rep["lat_ms"].items()}}
+            print(js.dumps(line), flush=True)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.wait(timeout=120)
 
 
 if __name__ == "__main__":
