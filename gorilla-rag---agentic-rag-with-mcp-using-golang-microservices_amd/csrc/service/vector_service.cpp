@@ -8,6 +8,7 @@
 // gRPC error shape ("rpc error: code = ... desc = ...") is kept in the
 // messages, as the Go service surfaces err.Error() verbatim.
 #include <algorithm>
+#include <charconv>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -202,8 +203,138 @@ struct SearchRequest {  // main.go:26-31
   Json filter;  // Filter map[string]interface{}: decoded; the reference never uses it
 };
 
-// Returns "" on success, else the decode error.
-std::string decode_search(const char* body, size_t len, SearchRequest* req) {
+// A JSON number literal at b[i..) (the grammar json.Decoder accepts):
+// -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?. Returns its end, or 0 when
+// there is none; *integer is whether it has neither fraction nor exponent.
+size_t json_number_end(const char* b, size_t n, size_t i, bool* integer) {
+  auto digit = [&](size_t j) { return j < n && b[j] >= '0' && b[j] <= '9'; };
+  *integer = true;
+  if (i < n && b[i] == '-') ++i;
+  if (!digit(i)) return 0;
+  if (b[i] == '0') ++i;
+  else
+    while (digit(i)) ++i;
+  if (i < n && b[i] == '.') {
+    *integer = false;
+    if (!digit(++i)) return 0;
+    while (digit(i)) ++i;
+  }
+  if (i < n && (b[i] == 'e' || b[i] == 'E')) {
+    *integer = false;
+    ++i;
+    if (i < n && (b[i] == '+' || b[i] == '-')) ++i;
+    if (!digit(i)) return 0;
+    while (digit(i)) ++i;
+  }
+  return i;
+}
+
+// Fast path for the body retrieval-service sends (main.go:221-226): one
+// object whose keys are exactly "collection", "query", "top_k" and "filter",
+// each at most once, in any order; collection a string of printable ASCII
+// without escapes, query an array of numbers, top_k an integer literal,
+// filter null. The query's float32s come straight from the literals
+// (from_chars: the correctly rounded float32, as Go's ParseFloat(s, 32)),
+// with no JSON tree. Anything else -- other keys, case-folded keys,
+// duplicates, escapes, nulls inside the query, a filter object, a number out
+// of range, a syntax error -- returns false and the generic decoder below
+// answers it (with Go's semantics and errors). A 768-number body decodes
+// ~3x faster this way. Trailing bytes after the object are ignored, as
+// json.Decoder.Decode ignores them.
+bool decode_search_fast(const char* b, size_t n, SearchRequest* req) {
+  size_t i = 0;
+  auto ws = [&] {
+    while (i < n && (b[i] == ' ' || b[i] == '\t' || b[i] == '\n' || b[i] == '\r')) ++i;
+  };
+  ws();
+  if (i >= n || b[i] != '{') return false;
+  ++i;
+  bool seen_c = false, seen_q = false, seen_k = false, seen_f = false;
+  for (;;) {
+    ws();
+    if (i >= n || b[i] != '"') return false;  // also the empty object: generic path
+    const size_t ks = ++i;
+    while (i < n && b[i] != '"' && b[i] != '\\') ++i;
+    if (i >= n || b[i] != '"') return false;
+    const std::string key(b + ks, i - ks);
+    ++i;
+    ws();
+    if (i >= n || b[i] != ':') return false;
+    ++i;
+    ws();
+    if (i >= n) return false;
+    if (key == "collection") {
+      if (seen_c || b[i] != '"') return false;
+      seen_c = true;
+      const size_t s0 = ++i;
+      while (i < n && b[i] != '"' && b[i] != '\\' && (unsigned char)b[i] >= 0x20 &&
+             (unsigned char)b[i] < 0x80)
+        ++i;
+      if (i >= n || b[i] != '"') return false;
+      req->collection.assign(b + s0, i - s0);
+      ++i;
+    } else if (key == "query") {
+      if (seen_q || b[i] != '[') return false;
+      seen_q = true;
+      ++i;
+      req->query.clear();
+      ws();
+      if (i < n && b[i] == ']') {
+        ++i;
+      } else {
+        for (;;) {
+          ws();
+          bool integer;
+          const size_t e = json_number_end(b, n, i, &integer);
+          if (!e) return false;
+          float f;
+          const auto r = std::from_chars(b + i, b + e, f);
+          if (r.ec != std::errc() || r.ptr != b + e) return false;  // out of range: generic
+          req->query.push_back(f);
+          i = e;
+          ws();
+          if (i < n && b[i] == ',') {
+            ++i;
+            continue;
+          }
+          if (i < n && b[i] == ']') {
+            ++i;
+            break;
+          }
+          return false;
+        }
+      }
+    } else if (key == "top_k") {
+      if (seen_k) return false;
+      seen_k = true;
+      bool integer;
+      const size_t e = json_number_end(b, n, i, &integer);
+      if (!e || !integer) return false;
+      int64_t v;
+      const auto r = std::from_chars(b + i, b + e, v);
+      if (r.ec != std::errc() || r.ptr != b + e) return false;
+      req->top_k = v;
+      i = e;
+    } else if (key == "filter") {
+      if (seen_f || n - i < 4 || std::memcmp(b + i, "null", 4) != 0) return false;
+      seen_f = true;
+      i += 4;
+    } else {
+      return false;
+    }
+    ws();
+    if (i < n && b[i] == ',') {
+      ++i;
+      continue;
+    }
+    if (i < n && b[i] == '}') return true;
+    return false;
+  }
+}
+
+// The generic decode (a JSON tree, then Go's field rules). Returns "" on
+// success, else the decode error.
+std::string decode_search_generic(const char* body, size_t len, SearchRequest* req) {
   Json root;
   std::string err;
   if (!vsjson::parse(body, len, &root, &err)) return err;
@@ -257,6 +388,18 @@ std::string decode_search(const char* body, size_t len, SearchRequest* req) {
     }
   }
   return first;
+}
+
+// Returns "" on success, else the decode error.
+std::string decode_search(const char* body, size_t len, SearchRequest* req) {
+  {
+    SearchRequest fast;
+    if (decode_search_fast(body, len, &fast)) {
+      *req = std::move(fast);
+      return "";
+    }
+  }
+  return decode_search_generic(body, len, req);
 }
 
 struct UpsertRequest {  // main.go:21-24
@@ -961,6 +1104,39 @@ int vsvc_reencode(const char* json, size_t len, char** out) {
   s.push_back('\n');
   *out = dup_bytes(s);
   return 0;
+}
+
+// Test hook (not in the public header): the /search decode through the fast
+// path only (path 1: "declined" when it falls back) or the generic decoder
+// only (path 0), as JSON {"collection","query":[float32 bits],"top_k"} or
+// {"error"}, so the tests can hold the two decoders equal.
+int vsvc_debug_decode_search(const char* body, size_t len, int path, char** out) {
+  if (!out) return VS_ERR_INVALID_ARG;
+  SearchRequest r;
+  std::string err;
+  if (path == 1) {
+    if (!decode_search_fast(body ? body : "", len, &r)) err = "declined";
+  } else {
+    err = decode_search_generic(body ? body : "", len, &r);
+  }
+  Json o = Json::object();
+  if (!err.empty()) {
+    o.obj.emplace_back("error", Json::string(err));
+  } else {
+    o.obj.emplace_back("collection", Json::string(r.collection));
+    Json q = Json::array();
+    for (float f : r.query) {
+      uint32_t u;
+      std::memcpy(&u, &f, 4);
+      q.arr.push_back(Json::number((double)u));
+    }
+    o.obj.emplace_back("query", std::move(q));
+    o.obj.emplace_back("top_k", Json::number((double)r.top_k));
+  }
+  std::string s;
+  vsjson::encode(o, &s, false);
+  *out = dup_bytes(s);
+  return *out ? VS_OK : VS_ERR_OOM;
 }
 
 int vsvc_validate(const char* path, const char* body, size_t len, char** msg) {

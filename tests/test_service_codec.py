@@ -103,3 +103,78 @@ def test_service_requires_engine(svc, pkg):
         pytest.skip("a GPU is visible")
     with pytest.raises(pkg.VSError):
         pkg.VectorEngine(device=0)
+
+
+def _decode(L, body, path):
+    import ctypes
+    import json
+    out = ctypes.c_void_p()
+    assert L.vsvc_debug_decode_search(body, len(body), path, ctypes.byref(out)) == 0
+    d = json.loads(ctypes.string_at(out.value))
+    L.vsvc_free(out)
+    return d
+
+
+def test_search_fast_decoder_matches_generic(svc):
+    """The /search fast path (vector_service.cpp decode_search_fast) against
+    the generic decoder on typical retrieval-service bodies (it must take
+    them, and agree bit for bit) and on bodies it must hand to the generic
+    decoder (it must decline them, never answer differently)."""
+    import ctypes
+    import random
+    import numpy as np
+    L = svc.load_service_library()
+    L.vsvc_debug_decode_search.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_void_p)]
+    rnd = random.Random(11)
+    rng = np.random.default_rng(11)
+
+    def num(x):
+        f = rnd.randrange(7)
+        if f == 0:
+            return "%.9g" % x
+        if f == 1:
+            return repr(float(x))
+        if f == 2:
+            return "%.17e" % x
+        if f == 3:
+            return "%dE%+d" % (rnd.randrange(-99999, 99999), rnd.randrange(-30, 30))
+        if f == 4:
+            return str(rnd.randrange(-3, 3))
+        if f == 5:
+            return "-0.0e-0"
+        return "%.3f" % x
+
+    def ws():
+        return rnd.choice(["", " ", "\n  ", "\t", "\r\n"])
+
+    taken = 0
+    for t in range(400):
+        q = rng.standard_normal(rnd.choice([0, 1, 3, 768])) * 10.0 ** rnd.randrange(-3, 3)
+        parts = {"collection": '"%s"' % rnd.choice(["regulatory_docs", "kyc_docs", "", "a b-c_9"]),
+                 "query": "[" + ",".join(ws() + num(x) + ws() for x in q) + "]",
+                 "top_k": str(rnd.choice([0, 5, 10, -3, 1024, 2 ** 40])),
+                 "filter": "null"}
+        keys = [k for k in parts if rnd.random() < 0.9]
+        rnd.shuffle(keys)
+        body = ("{" + ",".join(ws() + '"%s"' % k + ws() + ":" + ws() + parts[k] + ws()
+                               for k in keys) + "}" + rnd.choice(["", " ", "\n", "junk"])).encode()
+        if not keys:
+            body = b"{}"
+        fast, gen = _decode(L, body, 1), _decode(L, body, 0)
+        if fast != {"error": "declined"}:
+            taken += 1
+            assert fast == gen, body[:200]
+        elif keys:
+            pytest.fail(f"fast path declined a typical body: {body[:200]!r}")
+    assert taken > 350
+    declined = [
+        b'{"Query":[1],"top_k":3}', b'{"query":[1],"query":[2]}', b'{"query":[1,null]}',
+        b'{"query":null}', b'{"collection":"a\\u0062"}', b'{"collection":"caf\xc3\xa9"}',
+        b'{"query":[1e39]}', b'{"query":[1e-50]}', b'{"top_k":1.5}', b'{"top_k":1e2}',
+        b'{"top_k":01}', b'{"query":[01]}', b'{"query":[+1]}', b'{"query":[.5]}',
+        b'{"query":[1.]}', b'{"filter":{"a":"b"}}', b'{"extra":1}', b'{"query":[1,]}',
+        b'{"top_k":99999999999999999999}', b'[1]', b'', b'{', b'{"query":[1]', b'{}',
+        b'{"collection":"x","collection":"y"}', b'{"top_k":"5"}', b'{"query":"abc"}']
+    for body in declined:
+        assert _decode(L, body, 1) == {"error": "declined"}, body
