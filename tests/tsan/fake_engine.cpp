@@ -136,6 +136,29 @@ int vs_generate(vs_engine* e, const char* coll, uint64_t n, uint64_t seed) {
   return VS_OK;
 }
 
+// Qdrant-style f32 dot: 8-lane vector accumulators, then a fixed-order sum
+// (so the CPU backend of tools/c1_http.py is a fair SIMD scan, not a scalar
+// loop).
+static float dot(const float* x, const float* q, uint32_t dim) {
+  typedef float v8 __attribute__((vector_size(32)));
+  v8 a0 = {0, 0, 0, 0, 0, 0, 0, 0}, a1 = a0;
+  uint32_t d = 0;
+  for (; d + 16 <= dim; d += 16) {
+    v8 x0, x1, q0, q1;
+    std::memcpy(&x0, x + d, 32);
+    std::memcpy(&x1, x + d + 8, 32);
+    std::memcpy(&q0, q + d, 32);
+    std::memcpy(&q1, q + d + 8, 32);
+    a0 += x0 * q0;
+    a1 += x1 * q1;
+  }
+  a0 += a1;
+  float s = 0;
+  for (int j = 0; j < 8; ++j) s += a0[j];
+  for (; d < dim; ++d) s += x[d] * q[d];
+  return s;
+}
+
 static int search_impl(vs_engine* e, const char* coll, const float* q, uint32_t nq, uint32_t dim,
                        uint32_t k, const uint64_t* allow, float* os, uint64_t* orow,
                        uint32_t* ocnt) {
@@ -152,9 +175,7 @@ static int search_impl(vs_engine* e, const char* coll, const float* q, uint32_t 
     std::vector<std::pair<float, uint64_t>> hits;
     for (uint64_t r = 0; r < c.n(); ++r) {
       if (allow && !((allow[r / 64] >> (r % 64)) & 1)) continue;
-      float s = 0;
-      for (uint32_t d = 0; d < dim; ++d) s += c.rows[r * dim + d] * qq[d];
-      hits.push_back({s, r});
+      hits.push_back({dot(c.rows.data() + r * dim, qq.data(), dim), r});
     }
     const size_t m = std::min<size_t>(k, hits.size());
     std::partial_sort(hits.begin(), hits.begin() + m, hits.end(), [](auto& a, auto& b) {
