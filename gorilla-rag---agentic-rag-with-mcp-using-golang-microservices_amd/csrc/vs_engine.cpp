@@ -374,6 +374,16 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   }
   if (c.rows >= 0xFFFFFFFFull || c.row_base + c.rows >= 0xFFFFFFFFull)
     return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
+  // one query over a small collection (config C1): prep, scan and merge in
+  // one launch (the same keys as the three launches below, bit for bit)
+  if (nq == 1 && !allow && vsk::gemv_small_ok(dim, (uint32_t)c.rows, k)) {
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_gemv_small(c.data, bf16, dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q,
+                                  cosine, k, d_keys, eng->stream),
+           "small scan");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    return VS_OK;
+  }
 
   // 1. query preprocessing (cosine normalise) -> q_pre (fp32). The fp32
   // MFMA path reads q_pre directly, whole passes of kMfmaQueries rows: rows

@@ -61,6 +61,18 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 hipError_t launch_compact_rows(const uint64_t* allow, uint32_t n_rows, uint32_t* rows,
                                uint32_t* scratch, hipStream_t st);
 uint32_t compact_scratch_words(uint32_t n_rows);
+// One-launch search of a small collection for one raw (unpreprocessed)
+// query: query prep + scan + merge in one workgroup, writing the k final keys
+// to out[0, k). Bit-identical to launch_query_prep + launch_gemv +
+// launch_merge. Only where gemv_small_ok (dim in the GEMV table up to 1536,
+// rows <= kGemvSmallMaxRows, k <= kGemvSmallMaxK); unfiltered.
+constexpr uint32_t kGemvSmallMaxRows = 256;  // 32 rows per wave
+constexpr uint32_t kGemvSmallMaxK = 16;  // the workgroup merge is serial in k
+bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k);
+hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
+                             uint64_t* out, hipStream_t st);
+
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 

@@ -16,6 +16,7 @@
 //   * merge_keys_kernel — global top-k over per-workgroup / per-shard lists.
 // Store side (upsert, Qdrant cosine preprocess) and the synthetic generator
 // are here too. Numerics contract: include/vsearch.h and DESIGN.md.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -499,15 +500,48 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 // rows[] (a selective filter, compact_rows_kernel) instead of the rows
 // themselves; each gathered row is still one contiguous, coalesced read, and
 // the list entries are fetched one step ahead of the row data.
-template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar>
+// PREP (small collections, one workgroup, launch_gemv_small): q is the raw
+// query; wave 0 preprocesses it into LDS first, exactly as query_prep_kernel
+// does (prep bit 0: cosine, bit 1: round to bf16 values).
+template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar, bool PREP = false>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
     uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr) {
+    const uint32_t* __restrict__ rows = nullptr, int prep = 0) {
   using S = GemvShape<D, BF16>;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ float qs[PREP ? D : 1];
+  if constexpr (PREP) {
+    static_assert(D % 64 == 0 && D <= 64 * kQPrepMax, "query_prep_kernel's shapes only");
+    if (w == 0) {
+      constexpr int PJ = D / 64;
+      float v[PJ];
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) v[j] = q[lane + 64 * j];
+      bool keep = true;
+      double nrm = 1.0;
+      if (prep & 1) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+          const double t = (double)v[j];
+          s = s + t * t;
+        }
+        s = wave_sum_f64(s);
+        keep = vs::cosine_keep(s);
+        nrm = sqrt(s);
+      }
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        const float y = keep ? v[j] : (float)((double)v[j] / nrm);
+        qs[lane + 64 * j] = (prep & 2) ? vs::bf16_to_f32(vs::f32_to_bf16(y)) : y;
+      }
+    }
+    __syncthreads();
+  }
+  const float* qsrc = PREP ? qs : q;
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
   // VAR 8: waves interleave their RB-row steps over the whole range (wave gw
   // reads steps gw, gw + waves, ...) instead of each streaming a contiguous
@@ -531,7 +565,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
     coff[j] = c % S::CPR;
 #pragma unroll
-    for (int e = 0; e < S::EPC; ++e) qv[j][e] = q[coff[j] * S::EPC + e];
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qsrc[coff[j] * S::EPC + e];
   }
 
   WaveList<KPL> L;
@@ -664,7 +698,21 @@ int device_cu_count() {
 
 static int gemv_kpl(uint32_t k) { return k <= 64 ? 1 : (k <= 128 ? 2 : 16); }
 
-constexpr uint32_t kGemvMinRowsPerWave = 16;
+// Rows-per-wave floor of small scans: 2 since r02 (was 16). Swept over
+// 221 .. 200k rows x 768 fp32, k 5 and 100 (tools/tiny_sweep.py,
+// profiles/r02c_tiny_sweep.jsonl): fewer rows per wave shortens the serial
+// list inserts of a high-k scan (221 rows, k = 100: 73.6 -> 43.3 us; 20k rows:
+// 140 -> 112 us) and costs nothing at k = 5. VS_GEMV_MIN_RPW overrides it
+// (read once) for that sweep.
+static uint32_t gemv_min_rpw() {
+  static const uint32_t v = [] {
+    const char* e = getenv("VS_GEMV_MIN_RPW");
+    const int x = e ? atoi(e) : 2;
+    return (uint32_t)(x > 0 ? x : 2);
+  }();
+  return v;
+}
+#define kGemvMinRowsPerWave gemv_min_rpw()
 
 struct GemvGrid {
   uint32_t nwg, rows_per_wave;
@@ -797,6 +845,58 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                                         max_lists, nlists, st, rows);
   }
 #undef VS_GEMV_CASE
+}
+
+// Small collections, one query, k <= 16, no filter: query preprocessing,
+// scan and the workgroup merge in one launch of one workgroup, which writes
+// the final k keys (what query prep + gemv + merge produce, bit for bit: the
+// same per-row sums, the same exact top k). Saves two dependent launches of a
+// search that is all launch latency (221 rows).
+template <int D, bool BF16>
+static void gemv_small_launch(const void* X, uint32_t n_rows, uint32_t row_base,
+                              const float* q_raw, int prep, uint32_t k, uint64_t* out,
+                              hipStream_t st) {
+  using S = GemvShape<D, BF16>;
+  uint32_t rpw = (n_rows + kGemvWaves - 1) / kGemvWaves;
+  rpw = (rpw + S::RB - 1) / S::RB * S::RB;
+  hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1, false, kGemvVar, true>), dim3(1),
+                     dim3(kGemvThreads), 0, st, X, n_rows, row_base, q_raw, nullptr, k, rpw, out,
+                     nullptr, prep);
+}
+
+bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
+  if (n_rows == 0 || n_rows > kGemvSmallMaxRows || k == 0 || k > kGemvSmallMaxK) return false;
+  switch (dim) {
+    case 128: case 256: case 384: case 512: case 768: case 1024: case 1536: return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                             uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
+                             uint64_t* out, hipStream_t st) {
+  if (!gemv_small_ok(dim, n_rows, k)) return hipErrorInvalidValue;
+  const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
+#define VS_SMALL_CASE(DD)                                                                   \
+  case DD:                                                                                  \
+    if (bf16)                                                                               \
+      gemv_small_launch<DD, true>(X, n_rows, row_base, q_raw, prep, k, out, st);            \
+    else                                                                                    \
+      gemv_small_launch<DD, false>(X, n_rows, row_base, q_raw, prep, k, out, st);           \
+    break;
+  switch (dim) {
+    VS_SMALL_CASE(128)
+    VS_SMALL_CASE(256)
+    VS_SMALL_CASE(384)
+    VS_SMALL_CASE(512)
+    VS_SMALL_CASE(768)
+    VS_SMALL_CASE(1024)
+    VS_SMALL_CASE(1536)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef VS_SMALL_CASE
+  return hipGetLastError();
 }
 
 // Filter bitmap -> compacted list of the allowed local rows, ascending, for

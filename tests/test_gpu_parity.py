@@ -486,3 +486,35 @@ def test_merge_dedupes_and_zero_fills():
     distinct keys than k and a poisoned output: each key once, the rest 0, on
     the rank, tournament and general paths."""
     assert _run_py(_MERGE_DUP)["bad"] == []
+
+
+@pytest.mark.parametrize("dim", [128, 768, 1536])
+@pytest.mark.parametrize("dtype", [0, 1])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_small_collection_one_launch(pkg, orc, dim, dtype, metric):
+    """One query over <= 256 rows with k <= 16 takes the one-launch path
+    (launch_gemv_small: query prep + scan + merge in one workgroup). Its keys
+    must equal the first k of the three-launch path's (k = 17 takes that path),
+    bit for bit, and the oracle's top k; rows < k, one row and a row_base too."""
+    bf16 = dtype == 1
+    rng = np.random.default_rng(dim * 4 + dtype * 2 + metric)
+    with pkg.VectorEngine(device=0) as eng:
+        for rows, base in ((1, 0), (5, 0), (63, 0), (221, 0), (256, 1000)):
+            name = f"s{rows}"
+            eng.create_collection(name, dim, metric, dtype, 0, base)
+            V = rng.standard_normal((rows, dim)).astype(np.float32)
+            eng.upsert(name, list(range(rows)), V)
+            X = orc.preprocess(V, metric == 0, bf16)
+            for t in range(3):
+                Q = (rng.standard_normal((1, dim)) * (1 + 3 * t)).astype(np.float32)
+                s17, r17, c17 = eng.search(name, Q, 17)
+                Qp = orc.preprocess(Q, metric == 0, bf16)
+                for k in (1, 5, 16):
+                    s, r, c = eng.search(name, Q, k)
+                    assert int(c[0]) == min(rows, k)
+                    assert np.array_equal(s.view(np.uint32), s17[:, :k].view(np.uint32)), (rows, k)
+                    assert np.array_equal(r, r17[:, :k]), (rows, k)
+                    _, s64, rr, cc = orc.search(X, Qp, k, base)
+                    bad = orc.check_topk(s, r, c, s64, rr, cc, orc.rescore(X, Qp, r, c, base), 1e-5)
+                    assert not bad, (rows, k, bad[:3])
+            eng.drop_collection(name)
