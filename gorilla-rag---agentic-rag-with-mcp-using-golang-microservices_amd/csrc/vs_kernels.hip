@@ -500,48 +500,15 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 // rows[] (a selective filter, compact_rows_kernel) instead of the rows
 // themselves; each gathered row is still one contiguous, coalesced read, and
 // the list entries are fetched one step ahead of the row data.
-// PREP (small collections, one workgroup, launch_gemv_small): q is the raw
-// query; wave 0 preprocesses it into LDS first, exactly as query_prep_kernel
-// does (prep bit 0: cosine, bit 1: round to bf16 values).
-template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar, bool PREP = false>
+template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
     uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr, int prep = 0) {
+    const uint32_t* __restrict__ rows = nullptr) {
   using S = GemvShape<D, BF16>;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  __shared__ float qs[PREP ? D : 1];
-  if constexpr (PREP) {
-    static_assert(D % 64 == 0 && D <= 64 * kQPrepMax, "query_prep_kernel's shapes only");
-    if (w == 0) {
-      constexpr int PJ = D / 64;
-      float v[PJ];
-#pragma unroll
-      for (int j = 0; j < PJ; ++j) v[j] = q[lane + 64 * j];
-      bool keep = true;
-      double nrm = 1.0;
-      if (prep & 1) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < PJ; ++j) {
-          const double t = (double)v[j];
-          s = s + t * t;
-        }
-        s = wave_sum_f64(s);
-        keep = vs::cosine_keep(s);
-        nrm = sqrt(s);
-      }
-#pragma unroll
-      for (int j = 0; j < PJ; ++j) {
-        const float y = keep ? v[j] : (float)((double)v[j] / nrm);
-        qs[lane + 64 * j] = (prep & 2) ? vs::bf16_to_f32(vs::f32_to_bf16(y)) : y;
-      }
-    }
-    __syncthreads();
-  }
-  const float* qsrc = PREP ? qs : q;
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
   // VAR 8: waves interleave their RB-row steps over the whole range (wave gw
   // reads steps gw, gw + waves, ...) instead of each streaming a contiguous
@@ -565,7 +532,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
     coff[j] = c % S::CPR;
 #pragma unroll
-    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qsrc[coff[j] * S::EPC + e];
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = q[coff[j] * S::EPC + e];
   }
 
   WaveList<KPL> L;
@@ -852,16 +819,149 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
 // the final k keys (what query prep + gemv + merge produce, bit for bit: the
 // same per-row sums, the same exact top k). Saves two dependent launches of a
 // search that is all launch latency (221 rows).
+// The one workgroup's 8 waves each walk ~n_rows / 8 rows, so the scan is a
+// chain of dependent row steps (load, FMAs, a 6-step shuffle reduction, the
+// list insert): 17 us at 221 rows with one row step at a time, whatever the
+// load depth. Here each wave takes U row groups per step -- all their loads
+// issued first, their U reductions independent -- so the chains overlap
+// (221 rows: 17.1 us -> 12.6 with U = 4).
+// Each row's sum is formed exactly as in gemv_topk_kernel (the same lane /
+// chunk layout, the same accumulation and the same xor tree), so its scores
+// are the same bits. Wave 0 first preprocesses the raw query into LDS as
+// query_prep_kernel does (prep bit 0: cosine, bit 1: round to bf16 values).
+template <int D, bool BF16, int U>
+__global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
+    const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, const float* __restrict__ q,
+    uint32_t k, int prep, uint64_t* __restrict__ out) {
+  using S = GemvShape<D, BF16>;
+  static_assert(D % 64 == 0 && D <= 64 * kQPrepMax, "query_prep_kernel's shapes only");
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ float qs[D];
+  if (w == 0) {
+    constexpr int PJ = D / 64;
+    float v[PJ];
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) v[j] = q[lane + 64 * j];
+    bool keep = true;
+    double nrm = 1.0;
+    if (prep & 1) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        const double t = (double)v[j];
+        s = s + t * t;
+      }
+      s = wave_sum_f64(s);
+      keep = vs::cosine_keep(s);
+      nrm = sqrt(s);
+    }
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const float y = keep ? v[j] : (float)((double)v[j] / nrm);
+      qs[lane + 64 * j] = (prep & 2) ? vs::bf16_to_f32(vs::f32_to_bf16(y)) : y;
+    }
+  }
+  __syncthreads();
+  int rowsel[S::J];
+  int coff[S::J];
+  float qv[S::J][S::EPC];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) {
+    const int c = lane + 64 * j;
+    rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
+    coff[j] = c % S::CPR;
+#pragma unroll
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qs[coff[j] * S::EPC + e];
+  }
+  WaveList<1> L;
+  L.init();
+  uint64_t theta = 0;
+  const char* X = (const char*)Xv;
+  const uint32_t n_groups = (n_rows + S::RB - 1) / S::RB;
+  for (uint32_t g0 = (uint32_t)w; g0 < n_groups; g0 += kGemvWaves * U) {
+    uint4 buf[U][S::J];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        // rows past the end read the last row again (never keyed)
+        uint32_t row = (g0 + (uint32_t)(u * kGemvWaves)) * S::RB + rowsel[j];
+        row = row < n_rows ? row : n_rows - 1;
+        buf[u][j] = *(const uint4*)(X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16);
+      }
+    }
+    float sc[U][S::RB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float p[S::RB];
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) p[b] = 0.f;
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        const float d = chunk_dot<BF16>(buf[u][j], qv[j]);
+        if constexpr (S::RB == 1) {
+          p[0] += d;
+        } else {
+#pragma unroll
+          for (int b = 0; b < S::RB; ++b) p[b] += (rowsel[j] == b) ? d : 0.f;
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) sc[u][b] = wave_sum(p[b]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) {
+        const uint32_t row = (g0 + (uint32_t)(u * kGemvWaves)) * S::RB + b;
+        if (row < n_rows) {
+          const uint64_t key = make_key(sc[u][b], row_base + row);
+          if (key > theta) {
+            L.insert(key, k, lane);
+            theta = L.kth(k);
+          }
+        }
+      }
+    }
+  }
+  // Workgroup merge by rank, not by serial inserts (35 dependent inserts in
+  // wave 0 at k = 5): the first k keys of the 8 wave lists go to LDS; a key's
+  // place in the output is the number of larger keys among them (keys are
+  // unique: distinct rows), so every lane places its own keys at once. The
+  // output is the same sorted top k, zero-filled past the nonzero keys.
+  __shared__ uint64_t sm[kGemvWaves][64];
+  sm[w][lane] = L.e[0];
+  __syncthreads();
+  if (w == 0) {
+    const uint32_t tot = kGemvWaves * k;  // <= 128
+    const uint32_t c0 = (uint32_t)lane, c1 = (uint32_t)lane + 64;
+    const uint64_t x0 = c0 < tot ? sm[c0 / k][c0 % k] : 0;
+    const uint64_t x1 = c1 < tot ? sm[c1 / k][c1 % k] : 0;
+    uint32_t r0 = 0, r1 = 0, nz = 0;
+    for (int ow = 0; ow < kGemvWaves; ++ow)
+      for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t y = sm[ow][j];  // uniform LDS broadcast
+        r0 += y > x0 ? 1u : 0u;
+        r1 += y > x1 ? 1u : 0u;
+        nz += y != 0 ? 1u : 0u;
+      }
+    if (x0 && r0 < k) out[r0] = x0;
+    if (x1 && r1 < k) out[r1] = x1;
+    if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
+  }
+}
+
 template <int D, bool BF16>
 static void gemv_small_launch(const void* X, uint32_t n_rows, uint32_t row_base,
                               const float* q_raw, int prep, uint32_t k, uint64_t* out,
                               hipStream_t st) {
-  using S = GemvShape<D, BF16>;
-  uint32_t rpw = (n_rows + kGemvWaves - 1) / kGemvWaves;
-  rpw = (rpw + S::RB - 1) / S::RB * S::RB;
-  hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1, false, kGemvVar, true>), dim3(1),
-                     dim3(kGemvThreads), 0, st, X, n_rows, row_base, q_raw, nullptr, k, rpw, out,
-                     nullptr, prep);
+  // row groups per step: 4 (8 with the next step's loads issued ahead was
+  // slower: 14.9 us against 12.6 at 221 rows), fewer past 3 chunks per lane
+  constexpr int J = GemvShape<D, BF16>::J;
+  constexpr int U = J <= 3 ? 4 : (12 / J > 0 ? 12 / J : 1);
+  hipLaunchKernelGGL((gemv_small_kernel<D, BF16, U>), dim3(1), dim3(kGemvThreads), 0, st, X,
+                     n_rows, row_base, q_raw, k, prep, out);
 }
 
 bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {

@@ -1,0 +1,159 @@
+// rt_floor.hip: where a small host-API search's fixed cost goes. The
+// one-launch small path did not move the ~37 us per
+// call, so this times the pieces of vs_search's round trip alone, on one
+// stream, host clock, p50 over 20000 calls each:
+//   launch   one empty kernel + event record + polled wait
+//   h2d      3 KiB pinned -> device copy + event + wait
+//   d2h      40 B device -> pinned copy + event + wait
+//   full     h2d + kernel + d2h + event + wait (vs_search's shape)
+//   full_sync  the same, hipStreamSynchronize instead of the polled event
+//   out_map  h2d + kernel writing its 40 B to mapped pinned memory + event
+//   in_map   kernel reading its 3 KiB from mapped pinned memory + d2h + event
+//   vs_search  the engine's host API on config C1 (221 x 768 fp32 cosine,
+//            one query, k = 5): everything above plus the engine's own work
+//
+//   hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rt_floor tools/rt_floor.hip \
+//     -L<pkg>/lib -lvsearch -Wl,-rpath,<pkg>/lib
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <vector>
+
+#include "vsearch.h"
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+__global__ void touch(const float* __restrict__ in, uint64_t* __restrict__ out, int n) {
+  // one workgroup: sum the query (a dependent read of every element) and
+  // write 5 keys, like the small path's first and last accesses
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += in[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 256; ++i) t += red[i];
+    for (int i = 0; i < 5; ++i) out[i] = (uint64_t)__float_as_uint(t) + (uint64_t)i;
+  }
+}
+
+static void wait_polled(hipEvent_t ev) {
+  while (hipEventQuery(ev) == hipErrorNotReady) {
+  }
+}
+
+static double p50(std::vector<double>& v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+int main() {
+  const int n = 768, iters = 20000;
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t ev;
+  CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  float *h_in, *d_in, *m_in;
+  uint64_t *h_out, *d_out, *m_out;
+  CK(hipHostMalloc(&h_in, n * 4, hipHostMallocDefault));
+  CK(hipHostMalloc(&h_out, 64, hipHostMallocDefault));
+  CK(hipHostMalloc(&m_in, n * 4, hipHostMallocCoherent | hipHostMallocMapped));
+  CK(hipHostMalloc(&m_out, 64, hipHostMallocCoherent | hipHostMallocMapped));
+  CK(hipMalloc(&d_in, n * 4));
+  CK(hipMalloc(&d_out, 64));
+  for (int i = 0; i < n; ++i) h_in[i] = m_in[i] = 1.0f / (float)(i + 1);
+
+  struct Case {
+    const char* name;
+    std::function<void()> body;
+    bool sync;
+  };
+  std::vector<Case> cases = {
+      {"launch", [&] { hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n); }, false},
+      {"h2d", [&] { (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st); }, false},
+      {"d2h", [&] { (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st); }, false},
+      {"full",
+       [&] {
+         (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
+         hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n);
+         (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
+       },
+       false},
+      {"full_sync",
+       [&] {
+         (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
+         hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n);
+         (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
+       },
+       true},
+      {"out_map",
+       [&] {
+         (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
+         hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, m_out, n);
+       },
+       false},
+      {"in_map",
+       [&] {
+         hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, m_in, d_out, n);
+         (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
+       },
+       false},
+  };
+  std::printf("{\"tool\": \"rt_floor\", \"p50_us\": {");
+  bool first = true;
+  for (auto& c : cases) {
+    std::vector<double> t;
+    t.reserve(iters);
+    for (int i = 0; i < iters + 500; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      c.body();
+      if (c.sync) {
+        CK(hipStreamSynchronize(st));
+      } else {
+        CK(hipEventRecord(ev, st));
+        wait_polled(ev);
+      }
+      const auto t1 = std::chrono::steady_clock::now();
+      if (i >= 500) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    std::printf("%s\"%s\": %.2f", first ? "" : ", ", c.name, p50(t));
+    first = false;
+    std::fflush(stdout);
+  }
+  {
+    vs_engine* eng = nullptr;
+    vs_config cfg = {0, 0u};
+    if (vs_open(&cfg, &eng) != VS_OK || vs_collection_create(eng, "c1", n, 0, 0, 0, 0) != VS_OK ||
+        vs_generate(eng, "c1", 221, 7) != VS_OK) {
+      std::fprintf(stderr, "engine: %s\n", vs_last_error());
+      return 1;
+    }
+    float sc[5];
+    uint64_t rw[5];
+    uint32_t cnt;
+    std::vector<double> t;
+    for (int i = 0; i < iters + 500; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      if (vs_search(eng, "c1", h_in, 1, n, 5, sc, rw, &cnt) != VS_OK) return 1;
+      const auto t1 = std::chrono::steady_clock::now();
+      if (i >= 500) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    std::printf(", \"vs_search\": %.2f", p50(t));
+    vs_close(eng);
+  }
+  std::printf("}}\n");
+  CK(hipGetLastError());
+  return 0;
+}
