@@ -167,9 +167,25 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
     return el, tm, out
 
 
-def cpu_threads() -> int:
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    return min(n, os.cpu_count() or n)
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 CPU quota (cpu.max "quota period"), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except Exception:
+        return None
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may run on
+    (sched_getaffinity), capped by the cgroup CPU quota when one is set (more
+    threads than the quota grants only queue on it). OMP_NUM_THREADS is
+    recorded, not obeyed: the box sets it to its per-GPU worker share."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    n = min(aff, quota) if quota else aff
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota,
+               "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_blas_batched(X_raw, bf16, Q, k, threads, budget_s):
@@ -212,7 +228,7 @@ def cpu_baseline(cfg, args, n_full):
     rows, dim, dtype, metric, batch, k, _ = cfg
     bf16 = dtype == "bf16"
     ns = n_full if args.cpu_sample_rows <= 0 else min(args.cpu_sample_rows, n_full)
-    threads = cpu_threads()
+    threads, grant = cpu_threads()
     info = oracle.cpu_info()
     t0 = time.perf_counter()
     X = oracle.generate_raw(oracle.SEED_CORPUS, 0, ns, dim, bf16)
@@ -236,7 +252,7 @@ def cpu_baseline(cfg, args, n_full):
                      f"({dtype}, dim {dim}, top-{k}); {el:.2f} s measured",
            "measured_s": round(el, 3), "isa": oracle.cpu_scan_isa(),
            "cpu_model": info["model"], "host_logical_cpus": info["logical_cpus"],
-           "corpus_generate_s": round(gen_s, 2)}
+           "corpus_generate_s": round(gen_s, 2), "threads_grant": grant}
     if batch > 1:
         qps_b, done, el_b = cpu_blas_batched(X, bf16, Q[:batch], k, threads, args.cpu_budget_s)
         part = "" if done >= ns else f" (stopped at {done:,} rows by the budget; scaled)"
@@ -353,7 +369,8 @@ def main():
         "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
-                   "rows_per_gpu": hi - lo, "collective": collective},
+                   "rows_per_gpu": hi - lo, "collective": collective,
+                   "build_id": pkg.build_id()},
         "roofline": roof,
     }
 

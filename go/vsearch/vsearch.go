@@ -15,6 +15,81 @@ package vsearch
 #cgo LDFLAGS: -L${SRCDIR}/../../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/lib -lvsearch -Wl,-rpath,${SRCDIR}/../../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/lib
 #include <stdlib.h>
 #include "vsearch.h"
+
+// vs_last_error() is thread-local, and a goroutine may resume on another OS
+// thread between two cgo calls. So every entry point is called through a
+// wrapper that, on failure, copies the message into the caller's buffer
+// inside the SAME C call (vs_copy_last_error); Go never makes a second call
+// to fetch it.
+typedef struct { char msg[512]; } vsg_err;
+static int vsg_fin(int rc, vsg_err* e) {
+	if (rc != 0) vs_copy_last_error(e->msg, sizeof e->msg);
+	return rc;
+}
+static int vsg_open(const vs_config* c, vs_engine** h, vsg_err* e) { return vsg_fin(vs_open(c, h), e); }
+static int vsg_open_multi(const vs_config_multi* c, vs_engine** h, vsg_err* e) {
+	return vsg_fin(vs_open_multi(c, h), e);
+}
+static int vsg_engine_layout(vs_engine* h, uint32_t* s, uint32_t* d, vsg_err* e) {
+	return vsg_fin(vs_engine_layout(h, s, d), e);
+}
+static int vsg_collection_info(vs_engine* h, const char* n, uint32_t* d, uint64_t* r, vsg_err* e) {
+	return vsg_fin(vs_collection_info(h, n, d, r, NULL, NULL), e);
+}
+static int vsg_collection_create(vs_engine* h, const char* n, uint32_t d, int m, int t, uint64_t cap,
+                                 vsg_err* e) {
+	return vsg_fin(vs_collection_create(h, n, d, m, t, cap, 0), e);
+}
+static int vsg_collection_drop(vs_engine* h, const char* n, vsg_err* e) {
+	return vsg_fin(vs_collection_drop(h, n), e);
+}
+static int vsg_upsert(vs_engine* h, const char* n, uint64_t cnt, uint32_t d, const uint64_t* r,
+                      const float* v, vsg_err* e) {
+	return vsg_fin(vs_upsert(h, n, cnt, d, r, v), e);
+}
+static int vsg_generate(vs_engine* h, const char* n, uint64_t cnt, uint64_t seed, vsg_err* e) {
+	return vsg_fin(vs_generate(h, n, cnt, seed), e);
+}
+static int vsg_search(vs_engine* h, const char* n, const float* q, uint32_t nq, uint32_t d, uint32_t k,
+                      float* s, uint64_t* r, uint32_t* c, vsg_err* e) {
+	return vsg_fin(vs_search(h, n, q, nq, d, k, s, r, c), e);
+}
+static int vsg_search_filtered(vs_engine* h, const char* n, const float* q, uint32_t nq, uint32_t d,
+                               uint32_t k, const uint64_t* a, uint64_t aw, float* s, uint64_t* r,
+                               uint32_t* c, vsg_err* e) {
+	return vsg_fin(vs_search_filtered(h, n, q, nq, d, k, a, aw, s, r, c), e);
+}
+static int vsg_search_filter_id(vs_engine* h, const char* n, const float* q, uint32_t nq, uint32_t d,
+                                uint32_t k, uint64_t fid, float* s, uint64_t* r, uint32_t* c,
+                                vsg_err* e) {
+	return vsg_fin(vs_search_filter_id(h, n, q, nq, d, k, fid, s, r, c), e);
+}
+static int vsg_filter_create(vs_engine* h, const char* n, const uint64_t* a, uint64_t aw,
+                             uint64_t* id, vsg_err* e) {
+	return vsg_fin(vs_filter_create(h, n, a, aw, id), e);
+}
+static int vsg_filter_drop(vs_engine* h, uint64_t id, vsg_err* e) {
+	return vsg_fin(vs_filter_drop(h, id), e);
+}
+static int vsg_snapshot(vs_engine* h, const char* n, const char* p, vsg_err* e) {
+	return vsg_fin(vs_snapshot(h, n, p), e);
+}
+static int vsg_restore(vs_engine* h, const char* n, const char* p, vsg_err* e) {
+	return vsg_fin(vs_restore(h, n, p), e);
+}
+static int vsg_health(vs_engine* h, char* b, size_t len, vsg_err* e) {
+	return vsg_fin(vs_health(h, b, len), e);
+}
+static int vsg_comm_unique_id(unsigned char* id, vsg_err* e) {
+	return vsg_fin(vs_comm_unique_id(id), e);
+}
+static int vsg_comm_init(vs_engine* h, uint32_t n, uint32_t r, const unsigned char* id, vsg_err* e) {
+	return vsg_fin(vs_comm_init(h, n, r, id), e);
+}
+static int vsg_gather_merge_keys(vs_engine* h, const uint64_t* l, uint32_t nq, uint32_t ki,
+                                 uint32_t k, uint64_t* o, void* st, vsg_err* e) {
+	return vsg_fin(vs_gather_merge_keys(h, l, nq, ki, k, o, st), e);
+}
 */
 import "C"
 
@@ -45,7 +120,8 @@ var (
 	ErrIO          = errors.New("i/o error")
 )
 
-// Error carries the status and the library's message (vs_last_error).
+// Error carries the status and the library's message (copied by vs_copy_last_error
+// inside the failing call's own wrapper).
 type Error struct {
 	Code int
 	Msg  string
@@ -75,14 +151,13 @@ func (e *Error) Unwrap() error {
 	return ErrInternal
 }
 
-// vs_last_error is thread-local: read it on the OS thread of the failed call.
-// cgo runs a call and the Go code right after it on the same thread as long
-// as the goroutine does not yield in between, which holds here.
-func check(rc C.int) error {
+// check turns a wrapper's status into an error. The message was copied into
+// e by the same C call that failed (see the vsg_* wrappers above).
+func check(rc C.int, e *C.vsg_err) error {
 	if rc == 0 {
 		return nil
 	}
-	return &Error{Code: int(rc), Msg: C.GoString(C.vs_last_error())}
+	return &Error{Code: int(rc), Msg: C.GoString(&e.msg[0])}
 }
 
 // Engine is one engine handle: one GPU (Open) or row shards over several
@@ -94,7 +169,8 @@ type Engine struct{ h *C.vs_engine }
 func Open(device int) (*Engine, error) {
 	cfg := C.vs_config{device: C.int32_t(device)}
 	var h *C.vs_engine
-	if err := check(C.vs_open(&cfg, &h)); err != nil {
+	var e C.vsg_err
+	if err := check(C.vsg_open(&cfg, &h, &e), &e); err != nil {
 		return nil, err
 	}
 	return &Engine{h}, nil
@@ -116,7 +192,8 @@ func OpenShards(devices []int) (*Engine, error) {
 	}
 	cfg := C.vs_config_multi{devices: devs, n_shards: C.uint32_t(len(devices))}
 	var h *C.vs_engine
-	if err := check(C.vs_open_multi(&cfg, &h)); err != nil {
+	var e C.vsg_err
+	if err := check(C.vsg_open_multi(&cfg, &h, &e), &e); err != nil {
 		return nil, err
 	}
 	return &Engine{h}, nil
@@ -133,7 +210,8 @@ func (e *Engine) Close() {
 // Layout reports the engine's shards and distinct devices.
 func (e *Engine) Layout() (shards, devices int, err error) {
 	var s, d C.uint32_t
-	err = check(C.vs_engine_layout(e.h, &s, &d))
+	var ce C.vsg_err
+	err = check(C.vsg_engine_layout(e.h, &s, &d, &ce), &ce)
 	return int(s), int(d), err
 }
 
@@ -143,7 +221,8 @@ func (e *Engine) Info(name string) (dim uint32, rows uint64, err error) {
 	defer C.free(unsafe.Pointer(cs))
 	var d C.uint32_t
 	var r C.uint64_t
-	err = check(C.vs_collection_info(e.h, cs, &d, &r, nil, nil))
+	var ce C.vsg_err
+	err = check(C.vsg_collection_info(e.h, cs, &d, &r, &ce), &ce)
 	return uint32(d), uint64(r), err
 }
 
@@ -151,15 +230,17 @@ func (e *Engine) Info(name string) (dim uint32, rows uint64, err error) {
 func (e *Engine) Create(name string, dim uint32, metric, dtype int, capacity uint64) error {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
-	return check(C.vs_collection_create(e.h, cs, C.uint32_t(dim), C.int(metric), C.int(dtype),
-		C.uint64_t(capacity), 0))
+	var ce C.vsg_err
+	return check(C.vsg_collection_create(e.h, cs, C.uint32_t(dim), C.int(metric), C.int(dtype),
+		C.uint64_t(capacity), &ce), &ce)
 }
 
 // Drop frees a collection.
 func (e *Engine) Drop(name string) error {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
-	return check(C.vs_collection_drop(e.h, cs))
+	var ce C.vsg_err
+	return check(C.vsg_collection_drop(e.h, cs, &ce), &ce)
 }
 
 // Upsert writes len(rows) vectors (vecs is len(rows)*dim float32, row-major)
@@ -176,15 +257,17 @@ func (e *Engine) Upsert(name string, dim uint32, rows []uint64, vecs []float32) 
 	}
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
-	return check(C.vs_upsert(e.h, cs, C.uint64_t(len(rows)), C.uint32_t(dim),
-		(*C.uint64_t)(unsafe.Pointer(&rows[0])), (*C.float)(unsafe.Pointer(&vecs[0]))))
+	var ce C.vsg_err
+	return check(C.vsg_upsert(e.h, cs, C.uint64_t(len(rows)), C.uint32_t(dim),
+		(*C.uint64_t)(unsafe.Pointer(&rows[0])), (*C.float)(unsafe.Pointer(&vecs[0])), &ce), &ce)
 }
 
 // Generate appends n synthetic unit rows made on the device (benchmarks).
 func (e *Engine) Generate(name string, n, seed uint64) error {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
-	return check(C.vs_generate(e.h, cs, C.uint64_t(n), C.uint64_t(seed)))
+	var ce C.vsg_err
+	return check(C.vsg_generate(e.h, cs, C.uint64_t(n), C.uint64_t(seed), &ce), &ce)
 }
 
 // Hits of one query: rows and scores, best first.
@@ -229,13 +312,17 @@ func (e *Engine) FilterCreate(name string, allow []uint64) (uint64, error) {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
 	var id C.uint64_t
-	err := check(C.vs_filter_create(e.h, cs, (*C.uint64_t)(unsafe.Pointer(&allow[0])),
-		C.uint64_t(len(allow)), &id))
+	var ce C.vsg_err
+	err := check(C.vsg_filter_create(e.h, cs, (*C.uint64_t)(unsafe.Pointer(&allow[0])),
+		C.uint64_t(len(allow)), &id, &ce), &ce)
 	return uint64(id), err
 }
 
 // FilterDrop frees a resident filter.
-func (e *Engine) FilterDrop(id uint64) error { return check(C.vs_filter_drop(e.h, C.uint64_t(id))) }
+func (e *Engine) FilterDrop(id uint64) error {
+	var ce C.vsg_err
+	return check(C.vsg_filter_drop(e.h, C.uint64_t(id), &ce), &ce)
+}
 
 // SearchFilterID searches with a resident filter (stale after an upsert
 // that added rows: rebuild it).
@@ -264,17 +351,18 @@ func (e *Engine) search(name string, queries []float32, dim, k uint32, allow []u
 	ps := (*C.float)(unsafe.Pointer(&scores[0]))
 	pc := (*C.uint32_t)(unsafe.Pointer(&count[0]))
 	var rc C.int
+	var ce C.vsg_err
 	switch {
 	case fid != 0:
-		rc = C.vs_search_filter_id(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
-			C.uint64_t(fid), ps, pr, pc)
+		rc = C.vsg_search_filter_id(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
+			C.uint64_t(fid), ps, pr, pc, &ce)
 	case allow != nil:
-		rc = C.vs_search_filtered(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
-			(*C.uint64_t)(unsafe.Pointer(&allow[0])), C.uint64_t(len(allow)), ps, pr, pc)
+		rc = C.vsg_search_filtered(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k),
+			(*C.uint64_t)(unsafe.Pointer(&allow[0])), C.uint64_t(len(allow)), ps, pr, pc, &ce)
 	default:
-		rc = C.vs_search(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k), ps, pr, pc)
+		rc = C.vsg_search(e.h, cs, q, C.uint32_t(nq), C.uint32_t(dim), C.uint32_t(k), ps, pr, pc, &ce)
 	}
-	if err := check(rc); err != nil {
+	if err := check(rc, &ce); err != nil {
 		return nil, err
 	}
 	out := make([]Hits, nq)
@@ -291,7 +379,8 @@ func (e *Engine) Snapshot(name, path string) error {
 	cn, cp := C.CString(name), C.CString(path)
 	defer C.free(unsafe.Pointer(cn))
 	defer C.free(unsafe.Pointer(cp))
-	return check(C.vs_snapshot(e.h, cn, cp))
+	var ce C.vsg_err
+	return check(C.vsg_snapshot(e.h, cn, cp, &ce), &ce)
 }
 
 // Restore creates a collection from a snapshot (bit-exact, checksum-verified).
@@ -299,7 +388,8 @@ func (e *Engine) Restore(name, path string) error {
 	cn, cp := C.CString(name), C.CString(path)
 	defer C.free(unsafe.Pointer(cn))
 	defer C.free(unsafe.Pointer(cp))
-	return check(C.vs_restore(e.h, cn, cp))
+	var ce C.vsg_err
+	return check(C.vsg_restore(e.h, cn, cp, &ce), &ce)
 }
 
 // Health mirrors systemClient.HealthCheck (main.go:126): the engine's JSON
@@ -307,7 +397,8 @@ func (e *Engine) Restore(name, path string) error {
 func (e *Engine) Health() (string, error) {
 	buf := (*C.char)(C.malloc(4096))
 	defer C.free(unsafe.Pointer(buf))
-	err := check(C.vs_health(e.h, buf, 4096))
+	var ce C.vsg_err
+	err := check(C.vsg_health(e.h, buf, 4096, &ce), &ce)
 	return C.GoString(buf), err
 }
 
@@ -315,7 +406,8 @@ func (e *Engine) Health() (string, error) {
 // on one rank and hand the bytes to every rank (any host transport).
 func CommUniqueID() ([]byte, error) {
 	id := make([]byte, C.VS_COMM_ID_BYTES)
-	err := check(C.vs_comm_unique_id((*C.uchar)(unsafe.Pointer(&id[0]))))
+	var ce C.vsg_err
+	err := check(C.vsg_comm_unique_id((*C.uchar)(unsafe.Pointer(&id[0])), &ce), &ce)
 	return id, err
 }
 
@@ -325,8 +417,9 @@ func (e *Engine) CommInit(nRanks, rank int, id []byte) error {
 	if len(id) != int(C.VS_COMM_ID_BYTES) {
 		return fmt.Errorf("vsearch: comm id must be %d bytes: %w", int(C.VS_COMM_ID_BYTES), ErrInvalidArg)
 	}
-	return check(C.vs_comm_init(e.h, C.uint32_t(nRanks), C.uint32_t(rank),
-		(*C.uchar)(unsafe.Pointer(&id[0]))))
+	var ce C.vsg_err
+	return check(C.vsg_comm_init(e.h, C.uint32_t(nRanks), C.uint32_t(rank),
+		(*C.uchar)(unsafe.Pointer(&id[0])), &ce), &ce)
 }
 
 // GatherMergeKeys exchanges every rank's [nq][kIn] device keys (the output of
@@ -335,6 +428,7 @@ func (e *Engine) CommInit(nRanks, rank int, id []byte) error {
 // dLocal and dOut are device pointers, which cgo passes as plain addresses.
 func (e *Engine) GatherMergeKeys(dLocal, dOut unsafe.Pointer, nq, kIn, k uint32,
 	stream unsafe.Pointer) error {
-	return check(C.vs_gather_merge_keys(e.h, (*C.uint64_t)(dLocal), C.uint32_t(nq),
-		C.uint32_t(kIn), C.uint32_t(k), (*C.uint64_t)(dOut), stream))
+	var ce C.vsg_err
+	return check(C.vsg_gather_merge_keys(e.h, (*C.uint64_t)(dLocal), C.uint32_t(nq),
+		C.uint32_t(kIn), C.uint32_t(k), (*C.uint64_t)(dOut), stream, &ce), &ce)
 }

@@ -5,7 +5,7 @@ The product is the HIP library ``lib/libvsearch.so`` behind the C-ABI in
 :mod:`.service` the host-side mirror of rag/vector-service's HTTP handlers.
 """
 from .engine import (DTYPE_BF16, DTYPE_F32, METRIC_COSINE, METRIC_DOT, VectorEngine,
-                     VSError, device_count, keys_decode, load_library, pack_allow)
+                     VSError, build_id, device_count, keys_decode, load_library, pack_allow)
 
-__all__ = ["VectorEngine", "VSError", "device_count", "keys_decode", "load_library", "pack_allow",
+__all__ = ["VectorEngine", "VSError", "build_id", "device_count", "keys_decode", "load_library", "pack_allow",
            "METRIC_COSINE", "METRIC_DOT", "DTYPE_F32", "DTYPE_BF16"]

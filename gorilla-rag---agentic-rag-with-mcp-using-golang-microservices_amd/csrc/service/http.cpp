@@ -24,6 +24,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -184,7 +185,7 @@ Frame parse_request_head(const char* buf, size_t len, Request* req, size_t* head
   req->expect_continue = false;
   req->chunked = false;
   req->content_length = -1;
-  bool have_host = false;
+  bool have_host = false, saw_te = false;
   for (const std::string& ln : lines) {
     if (ln[0] == ' ' || ln[0] == '\t') return Frame::kBad;  // obsolete line folding
     const size_t c = ln.find(':');
@@ -199,10 +200,14 @@ Frame parse_request_head(const char* buf, size_t len, Request* req, size_t* head
       if (req->content_length >= 0 && req->content_length != cl) return Frame::kBad;
       req->content_length = cl;
     } else if (ieq(name, "transfer-encoding")) {
-      if (!ieq(v, "chunked")) {
+      // net/http: exactly one Transfer-Encoding line, and it must be
+      // "chunked" ("too many transfer encodings" / "unsupported transfer
+      // encoding" -> 501); a second line is ambiguous framing
+      if (saw_te || !ieq(v, "chunked")) {
         *bad_status = 501;
         return Frame::kBad;
       }
+      saw_te = true;
       req->chunked = true;
     } else if (ieq(name, "connection")) {
       if (has_token(v, "close")) req->keep_alive = false;
@@ -251,7 +256,7 @@ Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_leng
   ChunkScan local;
   ChunkScan& st = scan ? *scan : local;
   size_t pos = st.pos;
-  for (;;) {
+  while (!st.in_trailer) {
     const void* nl = std::memchr(buf + pos, '\n', len - pos);
     if (!nl) return len - pos > 4096 ? Frame::kBad : Frame::kNeedMore;
     const size_t e = (const char*)nl - buf;
@@ -272,16 +277,9 @@ Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_leng
       return Frame::kBad;
     size_t p = e + 1;
     if (sz == 0) {
-      // trailer section: header lines up to a blank line
-      for (;;) {
-        const void* tl = std::memchr(buf + p, '\n', len - p);
-        if (!tl) return Frame::kNeedMore;
-        const size_t te = (const char*)tl - buf;
-        const bool blank = te == p || (te == p + 1 && buf[p] == '\r');
-        p = te + 1;
-        if (blank) break;
-      }
-      pos = p;
+      // the last chunk: the trailer section follows (resumable below)
+      st.in_trailer = true;
+      st.pos = pos = p;
       break;
     }
     if ((int64_t)(st.total + sz) > kMaxBodyBytes) return Frame::kBad;
@@ -301,6 +299,22 @@ Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_leng
     st.parts.emplace_back(data, (size_t)sz);
     st.total += sz;
     st.pos = pos = p;
+  }
+  // trailer section: header lines up to a blank line, counted against the
+  // header limit; every complete line is recorded, so a slow trailer is not
+  // rescanned from the start on each receive
+  for (;;) {
+    const void* tl = std::memchr(buf + pos, '\n', len - pos);
+    if (!tl) {
+      if (st.trailer_bytes + (len - pos) > kMaxHeaderBytes) return Frame::kBad;
+      return Frame::kNeedMore;
+    }
+    const size_t te = (const char*)tl - buf;
+    const bool blank = te == pos || (te == pos + 1 && buf[pos] == '\r');
+    st.trailer_bytes += te + 1 - pos;
+    if (st.trailer_bytes > kMaxHeaderBytes) return Frame::kBad;
+    st.pos = pos = te + 1;
+    if (blank) break;
   }
   body->clear();
   body->reserve(st.total);
@@ -599,6 +613,9 @@ struct vsvc_http {
       if (fd < 0) continue;
       const int one = 1;
       ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));  // net/http's default
+      // recv gives up after kIdleTimeoutSec without a byte: the connection closes
+      struct timeval tv = {vshttp::kIdleTimeoutSec, 0};
+      ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
       std::lock_guard<std::mutex> g(mu);
       if (conns.size() >= kMaxConns) {
         send_error_close(fd, 503);

@@ -34,7 +34,13 @@ struct Response {
 };
 
 constexpr size_t kMaxHeaderBytes = 1 << 20;  // net/http DefaultMaxHeaderBytes
-constexpr int64_t kMaxBodyBytes = int64_t(1) << 32;
+// Request bodies past this are refused (413 by Content-Length, 400 for a
+// chunked body that grows past it). A /search body is ~16 KB and an ingest
+// upsert batch a few MB; net/http itself sets no limit.
+constexpr int64_t kMaxBodyBytes = int64_t(256) << 20;
+// A connection that sends nothing for this long (idle keep-alive, or a
+// stalled request) is closed, like net/http's Server.IdleTimeout would.
+constexpr int kIdleTimeoutSec = 120;
 
 // Parses the request head in buf[0, ...). On kDone, *head_len is the byte
 // count of the head (through the blank line) and req's head fields are set.
@@ -46,14 +52,17 @@ Frame parse_request_head(const char* buf, size_t len, Request* req, size_t* head
 // Progress of framing one chunked body across calls (bytes arrive in
 // pieces): the chunks already framed are not scanned again.
 struct ChunkScan {
-  size_t pos = 0;    // offset of the next chunk-size line
+  size_t pos = 0;    // offset of the next chunk-size line (or trailer line)
   size_t total = 0;  // data bytes framed so far
   std::vector<std::pair<size_t, size_t>> parts;  // (offset, length) of each chunk's data
+  bool in_trailer = false;  // the 0-size chunk was framed; pos walks the trailer lines
+  size_t trailer_bytes = 0; // trailer bytes framed so far (capped at kMaxHeaderBytes)
 };
 
 // Frames a body that starts at buf[0]: Content-Length or chunked (trailers
 // skipped). On kDone, *consumed is the byte count of the framed body and
-// *body the decoded bytes. kBad: malformed chunk framing. `scan` (chunked
+// *body the decoded bytes. kBad: malformed chunk framing, a body past
+// kMaxBodyBytes or a trailer past kMaxHeaderBytes. `scan` (chunked
 // only; nullable) carries the progress between calls on a growing buffer;
 // reset it for every new body.
 Frame body_frame(const char* buf, size_t len, bool chunked, int64_t content_length,

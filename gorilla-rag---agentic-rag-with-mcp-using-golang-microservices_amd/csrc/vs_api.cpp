@@ -669,6 +669,17 @@ extern "C" {
 
 const char* vs_last_error(void) { return vsd::last_error(); }
 
+size_t vs_copy_last_error(char* buf, size_t len) {
+  const char* m = vsd::last_error();
+  const size_t n = std::strlen(m);
+  if (buf && len) {
+    const size_t c = n < len - 1 ? n : len - 1;
+    std::memcpy(buf, m, c);
+    buf[c] = '\0';
+  }
+  return n;
+}
+
 int vs_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

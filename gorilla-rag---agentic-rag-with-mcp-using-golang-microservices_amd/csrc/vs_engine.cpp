@@ -891,11 +891,21 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   }
   VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
   std::memcpy(hs->in, queries, qbytes);
-  VS_HIP(hipMemcpyAsync(eng->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, eng->stream),
-         "query H2D");
-  if (abytes)  // pageable: HIP stages it (a shipped-bitmap call, not the batcher's path)
-    VS_HIP(hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream),
-           "filter bitmap H2D");
+  // busy from the first enqueue that reads the slot: a failure after it
+  // drains the stream before the slot is released (a queued H2D may still
+  // read hs->in, a queued D2H write hs->out)
+  hs->busy = true;
+  auto abandon = [&](int rc) {
+    (void)hipStreamSynchronize(eng->stream);
+    hs->busy = false;
+    return rc;
+  };
+  hipError_t e = hipMemcpyAsync(eng->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, eng->stream);
+  if (e != hipSuccess) return abandon(fail_hip(e, "query H2D"));
+  if (abytes) {  // pageable: HIP stages it (a shipped-bitmap call, not the batcher's path)
+    e = hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream);
+    if (e != hipSuccess) return abandon(fail_hip(e, "filter bitmap H2D"));
+  }
   int rc;
   if (df)
     rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
@@ -905,11 +915,10 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
                      abytes ? eng->allow.as<uint64_t>() : nullptr,
                      abytes ? popcount_rows(allow, c->rows) : 0);
-  if (rc != VS_OK) return rc;
-  VS_HIP(hipMemcpyAsync(hs->out, eng->keys.p, kbytes, hipMemcpyDeviceToHost, eng->stream),
-         "keys D2H");
-  VS_HIP(hipEventRecord(hs->done, eng->stream), "search event");
-  hs->busy = true;
+  if (rc != VS_OK) return abandon(rc);
+  e = hipMemcpyAsync(hs->out, eng->keys.p, kbytes, hipMemcpyDeviceToHost, eng->stream);
+  if (e == hipSuccess) e = hipEventRecord(hs->done, eng->stream);
+  if (e != hipSuccess) return abandon(fail_hip(e, "keys D2H"));
   // wait for the device outside work_mu: the next call (q_in, keys and every
   // scratch buffer are ordered on the same stream) enqueues behind this one
   g.unlock();

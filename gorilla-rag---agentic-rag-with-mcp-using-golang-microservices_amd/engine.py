@@ -47,6 +47,7 @@ EXPORTS = (
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
     "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
     "vs_engine_layout", "vs_comm_unique_id", "vs_comm_init", "vs_gather_merge_keys",
+    "vs_copy_last_error", "vs_build_id",
 )
 COMM_ID_BYTES = 128
 
@@ -103,6 +104,8 @@ def load_library(path: str = LIB_PATH):
         "vs_decode_keys": ([vp, vp, u32, u32, vp, vp, vp, vp], i32),
         "vs_health": ([vp, ctypes.c_char_p, ctypes.c_size_t], i32),
         "vs_last_error": ([], ctypes.c_char_p),
+        "vs_copy_last_error": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_size_t),
+        "vs_build_id": ([], ctypes.c_char_p),
         "vs_timing": ([vp, vp, vp, vp, vp, i32], i32),
         "vs_snapshot": ([vp, cp, cp], i32),
         "vs_restore": ([vp, cp, cp], i32),
@@ -136,6 +139,11 @@ def pack_allow(mask: np.ndarray) -> np.ndarray:
     pad = np.zeros((-m.size) % 64, np.bool_)
     bits = np.packbits(np.concatenate([m, pad]), bitorder="little")
     return bits.view("<u8").astype(np.uint64) if bits.size else np.zeros(0, np.uint64)
+
+
+def build_id() -> str:
+    """vs_build_id() of the loaded library: build.py tree_hash() of its sources."""
+    return load_library().vs_build_id().decode()
 
 
 def device_count() -> int:

@@ -311,6 +311,18 @@ int vs_health(vs_engine* eng, char* buf, size_t len);
 /* Thread-local message of the last failure ("" if none). */
 const char* vs_last_error(void);
 
+/* Copies the calling thread's last error message into buf (NUL-terminated,
+ * truncated to len - 1 bytes) and returns its full length. For bindings
+ * whose calls may migrate between OS threads (cgo): a wrapper that makes
+ * the failing call and this copy inside ONE foreign call reads the message
+ * of that call, not of whatever ran on the thread in between. */
+size_t vs_copy_last_error(char* buf, size_t len);
+
+/* Provenance: the first 16 hex digits of the sha256 over the sources this
+ * library was linked from (build.py tree_hash(): every source under csrc,
+ * the headers under include, and build.py). Never fails. */
+const char* vs_build_id(void);
+
 /* With VS_FLAG_TIMING (and VS_FLAG_TIMING_MERGE): average device duration
  * (ms) of scan (and merge) kernel launches recorded since the last reset, and
  * their counts. Blocks until the

@@ -101,3 +101,33 @@ int main(void) {{ for (unsigned i = 0; i < sizeof(S)/sizeof(S[0]); ++i)
     by_rule = sorted(range(len(keys)), key=lambda i: (-float(scores[i]), int(rows[i])))
     # +0.0 / -0.0 compare equal by score but differ in key; compare the rest
     assert [i for i in by_key if scores[i] != 0] == [i for i in by_rule if scores[i] != 0]
+
+
+def test_build_id_is_the_tree_hash(pkg):
+    """The loaded library was linked from exactly the sources of this tree."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_vs_build_t", os.path.join(os.path.dirname(pkg.__file__), "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    bid = pkg.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid)
+    assert bid == b.tree_hash()
+
+
+def test_copy_last_error_is_the_same_call_message(pkg):
+    """vs_copy_last_error (the cgo wrappers' single-call read) returns the
+    thread's last failure text, truncated and NUL-terminated."""
+    import ctypes
+    L = pkg.load_library()
+    rc = L.vs_open(None, None)  # out == NULL -> invalid argument
+    assert rc == -1
+    full = L.vs_last_error()
+    assert full
+    buf = ctypes.create_string_buffer(256)
+    n = L.vs_copy_last_error(buf, len(buf))
+    assert n == len(full) and buf.value == full
+    small = ctypes.create_string_buffer(5)
+    assert L.vs_copy_last_error(small, 5) == len(full)
+    assert small.value == full[:4]
+    assert L.vs_copy_last_error(None, 0) == len(full)

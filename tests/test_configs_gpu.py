@@ -8,10 +8,15 @@
   lists, every score equal to the exact score of the row it names, and the
   batched answer equal to the single-query GEMV answer (two independent
   kernels) up to the north_star near-tie rule.
-* C5 — multi-collection serving: 3 bf16 collections x 200k x 1024 (bulk
-  generated, so the candidate path runs), >= 64 concurrent /search requests
+* C2 — 1M x 768 fp32 Cosine, single-query GEMV searches, one call each, at
+  k = 10 (the rank merge of the waves' lists) and k = 100 (the two-stage
+  merge), against the streaming oracle at the fp32 bar (1e-5).
+* C5 — multi-collection serving: 3 bf16 collections x 1024-d (bulk
+  generated, so the candidate path runs), concurrent /search requests
   through the dynamic batcher with top_k uniform in [3, 50], every reply
-  checked against the oracle (UUID -> row through the synthetic bulk ids).
+  checked against the oracle (UUID -> row through the synthetic bulk ids):
+  at 200k rows per collection (one sample tile per workgroup) and at C5's
+  own 5M rows (the production 1/64 sample fraction and candidate capacity).
 
 Reference anchor: Points.Search, rag/vector-service/main.go:249-254; the
 request body is retrieval-service's searchVectorDB (rag/retrieval-service/
@@ -76,11 +81,45 @@ def _bulk_row(uuid: str) -> int:
 
 
 @pytest.mark.timeout(600)
+def test_c2_full_size_single_queries(engine, orc, pkg):
+    n, dim = 1_000_000, 768
+    name = "c2_full"
+    engine.create_collection(name, dim, pkg.METRIC_COSINE, pkg.DTYPE_F32, n)
+    try:
+        engine.generate(name, n, orc.SEED_CORPUS)
+        nq = 16
+        Q = orc.generate(orc.SEED_QUERY, 7000, nq, dim) * 1.3  # cosine normalises them back
+        Qp = orc.preprocess(Q, cosine=True, bf16=False)
+        for k in (10, 100):
+            got = [engine.search(name, Q[i:i + 1], k) for i in range(nq)]  # one GEMV call each
+            s = np.concatenate([g[0] for g in got])
+            r = np.concatenate([g[1] for g in got])
+            c = np.concatenate([g[2] for g in got])
+            assert np.all(c == k)
+            s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp, k, False)
+            resc = orc.rescore_generated(orc.SEED_CORPUS, Qp, r, c, False)
+            _check(orc, s, r, c, s64, rr, cc, resc, 1e-5)
+    finally:
+        engine.drop_collection(name)
+
+
+@pytest.mark.timeout(600)
 def test_c5_concurrent_mixed_k(pkg, orc):
+    _c5_concurrent_mixed_k(pkg, orc, 200_000, 96)
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_concurrent_mixed_k(pkg, orc):
+    """C5 at its own shape: 3 x 5M x 1024 bf16 (30.7 GB resident), 40
+    concurrent requests per collection."""
+    _c5_concurrent_mixed_k(pkg, orc, 5_000_000, 120)
+
+
+def _c5_concurrent_mixed_k(pkg, orc, n, nreq):
     from importlib import import_module
     svcmod = import_module(pkg.__name__ + ".service")
     names = ["regulatory_docs", "merchant_docs", "kyc_docs"]
-    n, dim = 200_000, 1024
+    dim = 1024
     seeds = {nm: orc.SEED_CORPUS + 17 * i for i, nm in enumerate(names)}
     cfg = {"collections": [{"name": nm, "dim": dim, "metric": "Cosine", "dtype": "bf16"}
                            for nm in names]}
@@ -89,7 +128,6 @@ def test_c5_concurrent_mixed_k(pkg, orc):
     try:
         for nm in names:
             s.bulk_generate(nm, n, seeds[nm])
-        nreq = 96
         rng = np.random.default_rng(55)
         coll = [names[i % 3] for i in range(nreq)]
         ks = rng.integers(3, 51, size=nreq)

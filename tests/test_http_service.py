@@ -303,6 +303,13 @@ def test_head_and_connection_close(lib, server):
     (b"POST /search HTTP/1.1\r\nHost: x\r\nExpect: magic\r\n\r\n", 417),
     (b"POST /search HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n", 400),
     (b"GET /health HTTP/1.1\r\nHost: x\r\n folded: y\r\n\r\n", 400),
+    # two Transfer-Encoding lines: ambiguous framing (net/http: "too many
+    # transfer encodings"), even when both say chunked
+    (b"POST /search HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n"
+     b"Transfer-Encoding: chunked\r\n\r\n0\r\n\r\n", 501),
+    (b"POST /search HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: gzip, chunked\r\n\r\n", 501),
+    # a body announced past the 256 MiB request cap
+    (b"POST /upsert HTTP/1.1\r\nHost: x\r\nContent-Length: 268435457\r\n\r\n", 413),
 ])
 def test_malformed_requests(server, req, status):
     s = _raw(server)
@@ -318,6 +325,33 @@ def test_oversized_head_is_431(server):
     s.sendall(b"GET /health HTTP/1.1\r\nHost: x\r\nX-Big: " + b"a" * (1 << 20) + b"\r\n")
     st, hdr, body, _ = _read_response(s)
     assert st == 431
+    s.close()
+
+
+def test_chunked_trailer_is_bounded(server):
+    """Trailer lines count against the 1 MiB header limit: an endless trailer
+    is refused (400) instead of growing the buffer (and is framed line by
+    line, not rescanned from the last chunk on every receive)."""
+    s = _raw(server)
+    s.sendall(b"POST /search HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+              b"2\r\n{}\r\n0\r\n")
+    line = b"X-T: " + b"a" * 4000 + b"\r\n"
+    try:
+        for _ in range(300):  # ~1.2 MB of trailer lines
+            s.sendall(line * 1)
+    except (BrokenPipeError, ConnectionResetError):
+        pass
+    st, hdr, body, _ = _read_response(s)
+    assert st == 400 and _closed(s)
+    s.close()
+
+
+def test_chunked_body_past_cap_is_refused(server):
+    s = _raw(server)
+    s.sendall(b"POST /upsert HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+              b"10000001\r\n")  # one chunk of 256 MiB + 1
+    st, hdr, body, _ = _read_response(s)
+    assert st == 400 and _closed(s)
     s.close()
 
 
