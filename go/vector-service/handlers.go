@@ -262,13 +262,8 @@ func (s *service) search(w http.ResponseWriter, r *http.Request) {
 	reply := searchReply{Results: make([]hit, 0)}
 	if rows := len(st.ids); rows > 0 {
 		k := body.TopK
-		if k > rows {
+		if k > rows { // Qdrant returns min(limit, points); any limit is served
 			k = rows
-		}
-		if k > vsearch.MaxK {
-			writeError(w, http.StatusInternalServerError, fmt.Sprintf(
-				"Search failed: limit %d exceeds the engine maximum %d", body.TopK, vsearch.MaxK))
-			return
 		}
 		hits, err := s.batch.search(body.Collection, body.Query, uint32(k))
 		if err != nil {

@@ -105,7 +105,6 @@ const (
 	MetricDot    = int(C.VS_METRIC_DOT)
 	DtypeF32     = int(C.VS_DTYPE_F32)
 	DtypeBF16    = int(C.VS_DTYPE_BF16)
-	MaxK         = 1024 // largest k of one search
 )
 
 // Status codes of the C-ABI.
@@ -337,8 +336,8 @@ func (e *Engine) search(name string, queries []float32, dim, k uint32, allow []u
 		return nil, fmt.Errorf("vsearch: %d floats are not whole queries of dim %d: %w",
 			len(queries), dim, ErrInvalidArg)
 	}
-	if k == 0 || k > MaxK {
-		return nil, fmt.Errorf("vsearch: k must be in [1, %d]: %w", MaxK, ErrInvalidArg)
+	if k == 0 {
+		return nil, fmt.Errorf("vsearch: k must be at least 1: %w", ErrInvalidArg)
 	}
 	nq := len(queries) / int(dim)
 	cs := C.CString(name)

@@ -698,12 +698,9 @@ Response handle_search(vsvc* svc, const std::string& method, const char* body, s
   if (req.query.size() != cs->dim)
     return error_json("Search failed: " + dim_error(cs->dim, req.query.size()), 500);
   const uint64_t rows = cs->nrows();
+  // Qdrant returns min(limit, points): any limit is served (k > 1024 takes
+  // the engine's large-k select), and buffers are sized by what can return
   uint64_t k = std::min<uint64_t>(limit, std::max<uint64_t>(rows, 1));
-  if (k > 1024)
-    return error_json("Search failed: " + grpc_error(VS_ERR_INVALID_ARG,
-                                                     "limit " + std::to_string(limit) +
-                                                         " exceeds the engine maximum 1024"),
-                      500);
   std::vector<float> scores(k);
   std::vector<uint64_t> hit_rows(k);
   uint32_t count = 0;

@@ -238,9 +238,9 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
                                     (uint64_t)nq * k, S, E->dev_shards[d][j], 0, de->stream),
              "remap keys");
     if (m > 1) {
-      VS_HIP(vsk::launch_merge(sc_d.keys.as<uint64_t>(), m, (uint64_t)nq * k, k, nq, k, k,
-                               sc_d.merged.as<uint64_t>(), de->stream),
-             "device merge");
+      const int rc = vsd::merge_any(de, sc_d.keys.as<uint64_t>(), m, (uint64_t)nq * k, k, nq, k,
+                                    k, sc_d.merged.as<uint64_t>());
+      if (rc != VS_OK) return rc;
       send[d] = sc_d.merged.as<uint64_t>();
     } else {
       send[d] = sc_d.keys.as<uint64_t>();
@@ -261,17 +261,15 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
   if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
   DevEngine* d0 = E->dev[0];
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
-  VS_HIP(vsk::launch_merge(E->scr[0].gather.as<uint64_t>(), D, (uint64_t)nq * k, k, nq, k, k,
-                           d_out ? d_out : E->scr[0].out.as<uint64_t>(), d0->stream),
-         "cross-device merge");
-  return VS_OK;
+  return vsd::merge_any(d0, E->scr[0].gather.as<uint64_t>(), D, (uint64_t)nq * k, k, nq, k, k,
+                        d_out ? d_out : E->scr[0].out.as<uint64_t>());
 }
 
 int sharded_search_host(vs_engine* E, const char* coll, const float* queries, uint32_t nq,
                         uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                         uint64_t filter_id, float* out_scores, uint64_t* out_rows,
                         uint32_t* out_count) {
-  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (k == 0) return fail(VS_ERR_INVALID_ARG, "k must be at least 1");
   if (nq == 0) return VS_OK;
   if (!queries) return fail(VS_ERR_INVALID_ARG, "queries is NULL");
   auto sc = find_scoll(E, coll);
@@ -883,7 +881,7 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (!eng->sharded)
     return vsd::search_keys(eng->dev[0], coll, d_queries, nq, dim, k, d_keys, stream);
-  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (k == 0) return fail(VS_ERR_INVALID_ARG, "k must be at least 1");
   if (nq == 0) return VS_OK;
   if (!d_queries || !d_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   auto sc = find_scoll(eng, coll);
@@ -943,8 +941,7 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
                          uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (!eng->pcomm) return fail(VS_ERR_INVALID_ARG, "vs_comm_init has not been called");
-  if (k == 0 || k > vsk::kMaxK || k_in == 0 || k_in > vsk::kMaxK)
-    return fail(VS_ERR_INVALID_ARG, "bad merge shape");
+  if (k == 0 || k_in == 0) return fail(VS_ERR_INVALID_ARG, "bad merge shape");
   if (nq == 0) return VS_OK;
   if (!d_local || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   DevEngine* d0 = eng->dev[0];
@@ -961,10 +958,8 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
   const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
                                        eng->pcomm, cs);
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-  VS_HIP(vsk::launch_merge(eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in, nq,
-                           k_in, k, d_out_keys, cs),
-         "rank merge");
-  return VS_OK;
+  return vsd::merge_any(d0, eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in,
+                        nq, k_in, k, d_out_keys);
 }
 
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,

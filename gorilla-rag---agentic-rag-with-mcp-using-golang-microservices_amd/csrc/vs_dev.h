@@ -139,6 +139,10 @@ struct DevEngine {
   DevBuf scratch8;                  // u64 result of the snapshot checksum
   DevBuf allow;                     // filter pre-mask of the current vs_search_filtered
   DevBuf gather_rows, gather_cnt;   // its compacted row list (selective filters) + scan scratch
+  // large-k path (k > vsk::kMaxK): score images, digit histogram (kept
+  // zeroed between uses), select state, the selected keys, sort scratch;
+  // large merges (vs_merge_keys / shard merges at k > kMaxK)
+  DevBuf lk_sc, lk_hist, lk_state, lk_sel, lk_sort, merge_big;
   // device-resident filters (vs_filter_create), guarded by work_mu
   struct DevFilter {
     std::string coll;
@@ -195,6 +199,10 @@ int search_keys(DevEngine* eng, const char* coll, const float* d_queries, uint32
                 uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream);
 int merge_keys(DevEngine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
                uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream);
+// launch_merge for any k on eng->stream (k or k_in > vsk::kMaxK: the sort
+// merge, scratch grown here); work_mu held by the caller.
+int merge_any(DevEngine* eng, const uint64_t* lists, uint32_t L, uint64_t lstride,
+              uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out);
 int decode_keys(DevEngine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream);
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores, uint64_t* rows,

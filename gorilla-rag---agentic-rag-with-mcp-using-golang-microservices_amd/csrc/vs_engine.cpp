@@ -271,6 +271,71 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
   return VS_OK;
 }
 
+// Large k (k > vsk::kMaxK: Qdrant serves any limit, rag/vector-service/
+// main.go:252): per query one score pass over the collection (the GEMV
+// stream writing every row's score image instead of keeping a list), radix
+// select of the k-th key on the device, compaction of the k keys, rocPRIM
+// sort (vs_select.hip). keff = min(k, unmasked rows) keys per query; the
+// rest of each [k] row of d_keys is 0. Exact, no host round trip.
+int search_large_k(DevEngine* eng, Collection& c, const float* qp, uint32_t nq, uint32_t k,
+                   uint64_t* d_keys, const uint64_t* allow, uint64_t avail) {
+  const uint32_t n_rows = (uint32_t)c.rows;
+  const uint32_t keff = (uint32_t)std::min<uint64_t>(k, avail);
+  if (keff < k)
+    VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
+  if (keff == 0) return VS_OK;
+  const size_t sort_bytes = vsk::sort_keys_temp_bytes(keff);
+  if (!sort_bytes) return fail(VS_ERR_INTERNAL, "sort scratch size");
+  if (eng->lk_sc.bytes < (size_t)n_rows * 4 || eng->lk_hist.bytes < vsk::kRselBins * 4 ||
+      eng->lk_state.bytes < sizeof(vsk::RselState) || eng->lk_sel.bytes < (size_t)keff * 8 ||
+      eng->lk_sort.bytes < sort_bytes) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->lk_sc.ensure((size_t)n_rows * 4), "alloc score images");
+    const bool fresh = eng->lk_hist.bytes < vsk::kRselBins * 4;
+    VS_HIP(eng->lk_hist.ensure(vsk::kRselBins * 4), "alloc digit histogram");
+    if (fresh) VS_HIP(hipMemsetAsync(eng->lk_hist.p, 0, eng->lk_hist.bytes, eng->stream), "zero");
+    VS_HIP(eng->lk_state.ensure(sizeof(vsk::RselState)), "alloc select state");
+    VS_HIP(eng->lk_sel.ensure((size_t)keff * 8), "alloc selected keys");
+    VS_HIP(eng->lk_sort.ensure(sort_bytes), "alloc sort scratch");
+  }
+  uint32_t* sc = eng->lk_sc.as<uint32_t>();
+  uint32_t* hist = eng->lk_hist.as<uint32_t>();
+  for (uint32_t i = 0; i < nq; ++i) {
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_gemv_scores(c.data, c.dtype == VS_DTYPE_BF16, c.dim, n_rows,
+                                   qp + (size_t)i * c.dim, allow, sc, hist, eng->stream),
+           "score pass");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+    VS_HIP(vsk::launch_rsel(sc, n_rows, (uint32_t)c.row_base, keff, hist,
+                            eng->lk_state.as<vsk::RselState>(), eng->lk_sel.as<uint64_t>(),
+                            eng->stream),
+           "radix select");
+    VS_HIP(vsk::launch_sort_keys_desc(eng->lk_sel.as<uint64_t>(), d_keys + (size_t)i * k, keff,
+                                      eng->lk_sort.p, eng->lk_sort.bytes, eng->stream),
+           "sort selected keys");
+    VS_HIP(ev_end(eng, eng->merge_ev), "event");
+  }
+  return VS_OK;
+}
+
+int merge_any(DevEngine* eng, const uint64_t* lists, uint32_t L, uint64_t lstride,
+              uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out) {
+  if (k <= vsk::kMaxK && kin <= vsk::kMaxK) {
+    VS_HIP(vsk::launch_merge(lists, L, lstride, qstride, nq, kin, k, out, eng->stream), "merge");
+    return VS_OK;
+  }
+  const size_t need = vsk::merge_large_scratch(L, nq, kin);
+  if (eng->merge_big.bytes < need) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->merge_big.ensure(need), "alloc merge scratch");
+  }
+  VS_HIP(vsk::launch_merge_large(lists, L, lstride, qstride, nq, kin, k, out, eng->merge_big.p,
+                                 eng->merge_big.bytes, eng->stream),
+         "merge (large k)");
+  return VS_OK;
+}
+
 // Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
 // queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
 //  1. sample pass over 1/128 of every workgroup's tiles -> tile maxima ->
@@ -432,6 +497,8 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                                 eng->stream),
          "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
+  if (k > vsk::kMaxK)  // a filter rides along as the bitmap, selective or not
+    return search_large_k(eng, c, qp, nq, k, d_keys, allow, allow ? allowed : c.rows);
   if (gather) {
     if (allowed == 0) {
       VS_HIP(hipMemsetAsync(d_keys, 0, (size_t)nq * k * 8, eng->stream), "clear keys");
@@ -842,7 +909,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count,
                 uint64_t filter_id) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
-  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (k == 0) return fail(VS_ERR_INVALID_ARG, "k must be at least 1");
   if (nq == 0) return VS_OK;
   if (!queries) return fail(VS_ERR_INVALID_ARG, "queries is NULL");
   auto c = find_coll(eng, coll);
@@ -988,7 +1055,7 @@ int filter_drop(DevEngine* eng, uint64_t filter_id) {
 int search_keys(DevEngine* eng, const char* coll, const float* d_queries, uint32_t nq,
                    uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
-  if (k == 0 || k > vsk::kMaxK) return fail(VS_ERR_INVALID_ARG, "k must be in [1, 1024]");
+  if (k == 0) return fail(VS_ERR_INVALID_ARG, "k must be at least 1");
   if (nq == 0) return VS_OK;
   if (!d_queries || !d_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   auto c = find_coll(eng, coll);
@@ -1008,18 +1075,22 @@ int search_keys(DevEngine* eng, const char* coll, const float* d_queries, uint32
 int merge_keys(DevEngine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
                   uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
-  if (k == 0 || k > vsk::kMaxK || k_in == 0 || n_lists == 0)
-    return fail(VS_ERR_INVALID_ARG, "bad merge shape");
+  if (k == 0 || k_in == 0 || n_lists == 0) return fail(VS_ERR_INVALID_ARG, "bad merge shape");
   if (nq == 0) return VS_OK;
   if (!d_lists || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   hipStream_t cs = (hipStream_t)stream;
-  // the merge has no scratch of its own: it runs directly on the caller's stream
-  hipError_t e = vsk::launch_merge(d_lists, n_lists, (uint64_t)nq * k_in, k_in, nq, k_in, k,
-                                   d_out_keys, cs);
-  if (e != hipSuccess) return fail_hip(e, "merge");
-  return VS_OK;
+  if (k <= vsk::kMaxK && k_in <= vsk::kMaxK) {
+    // the list merge has no scratch of its own: it runs directly on the caller's stream
+    hipError_t e = vsk::launch_merge(d_lists, n_lists, (uint64_t)nq * k_in, k_in, nq, k_in, k,
+                                     d_out_keys, cs);
+    if (e != hipSuccess) return fail_hip(e, "merge");
+    return VS_OK;
+  }
+  // the sort merge uses the engine's scratch: ordered after its last user
+  VS_HIP(use_stream(eng, cs), "stream order");
+  return merge_any(eng, d_lists, n_lists, (uint64_t)nq * k_in, k_in, nq, k_in, k, d_out_keys);
 }
 
 int decode_keys(DevEngine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,

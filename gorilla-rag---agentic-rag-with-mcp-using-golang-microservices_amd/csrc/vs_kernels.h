@@ -14,8 +14,46 @@ constexpr uint32_t kMfmaQueries = 256;
 // keeps kMfmaListMaxK keys per query in LDS.
 constexpr uint32_t kMfmaMaxK = 128;
 constexpr uint32_t kMfmaListMaxK = 16;
-// Largest k any scan supports (GEMV register lists: 16 entries per lane).
+// Largest k of the list scans (GEMV register lists: 16 entries per lane) and
+// of the one-workgroup merge; larger k takes the large-k path below.
 constexpr uint32_t kMaxK = 1024;
+// Large-k path (k > kMaxK; Qdrant serves any limit, rag/vector-service/
+// main.go:252): per query, launch_gemv_scores writes every row's score image
+// (the result key's high word: order-preserving, 0 = masked) and counts the
+// first radix digit; launch_rsel finds the k-th largest 64-bit key by radix
+// select (6 digits of 11/11/10 bits over the high word then the row word;
+// a digit pass is skipped once the threshold's bucket holds exactly what is
+// left to take) and compacts the k keys >= it; launch_sort_keys_desc sorts
+// them. Exact, stream-ordered, no host round trip.
+constexpr int kRselBits0 = 11;
+constexpr int kRselBins = 1 << kRselBits0;
+struct RselState {
+  unsigned long long prefix;  // key bits fixed so far (the top plen bits)
+  unsigned long long thr;     // when done: every key >= thr is selected
+  uint32_t plen;              // bits fixed
+  uint32_t krem;              // keys still to take inside the prefix bucket
+  uint32_t done;
+  uint32_t count;             // compaction cursor
+};
+hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                              const float* q, const uint64_t* allow, uint32_t* sc, uint32_t* hist,
+                              hipStream_t st);
+// hist (kRselBins u32, the first digit's counts from launch_gemv_scores) is
+// left zeroed; `keff` = min(k, unmasked rows) keys land in sel (unordered).
+hipError_t launch_rsel(const uint32_t* sc, uint32_t n_rows, uint32_t row_base, uint32_t keff,
+                       uint32_t* hist, RselState* state, uint64_t* sel, hipStream_t st);
+// Descending sort of n 64-bit keys (rocPRIM radix sort); temp / temp_bytes
+// from sort_keys_temp_bytes(n).
+size_t sort_keys_temp_bytes(uint64_t n);
+hipError_t launch_sort_keys_desc(const uint64_t* in, uint64_t* out, uint64_t n, void* temp,
+                                 size_t temp_bytes, hipStream_t st);
+// Merge for any k (the large-k form of launch_merge): the L lists of each
+// query concatenated, sorted (rocPRIM segmented radix sort), repeated keys
+// dropped, the first k kept (0-padded). scratch: merge_large_scratch bytes.
+size_t merge_large_scratch(uint32_t L, uint32_t nq, uint32_t kin);
+hipError_t launch_merge_large(const uint64_t* lists, uint32_t L, uint64_t lstride,
+                              uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k,
+                              uint64_t* out, void* scratch, size_t scratch_bytes, hipStream_t st);
 // MFMA passes: workgroups per launch (<= CUs), most candidate slots per
 // (workgroup, query), sample-pass tiles per workgroup, and the select
 // kernel's LDS buffer (candidates are streamed through it in chunks).

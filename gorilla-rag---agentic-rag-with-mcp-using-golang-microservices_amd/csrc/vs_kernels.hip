@@ -500,13 +500,23 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 // rows[] (a selective filter, compact_rows_kernel) instead of the rows
 // themselves; each gathered row is still one contiguous, coalesced read, and
 // the list entries are fetched one step ahead of the row data.
+// KPL == 0 (large k, vs_kernels.h launch_gemv_scores): no list; every row's
+// score leaves as its order-preserving 32-bit image (the key's high word, 0
+// for a masked row) in sc[row], and the top 11 bits of each unmasked image
+// are counted into hist[2048] (the first digit of the radix select).
 template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
     uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr) {
+    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr) {
   using S = GemvShape<D, BF16>;
+  constexpr bool kScores = KPL == 0;
+  __shared__ uint32_t lhist[kScores ? kRselBins : 1];
+  if constexpr (kScores) {
+    for (int i = threadIdx.x; i < kRselBins; i += kGemvThreads) lhist[i] = 0;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
@@ -535,7 +545,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     for (int e = 0; e < S::EPC; ++e) qv[j][e] = q[coff[j] * S::EPC + e];
   }
 
-  WaveList<KPL> L;
+  WaveList<kScores ? 1 : KPL> L;
   L.init();
   uint64_t theta = 0;
   const char* X = (const char*)Xv;
@@ -599,7 +609,14 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
       for (int b = 0; b < S::RB; ++b) {
         const float s = kDpp ? wave_sum_dpp(p[b]) : wave_sum(p[b]);
         const uint32_t row = r + b;
-        if (row < hi && (GATHER || row_allowed(allow, row))) {
+        if constexpr (kScores) {
+          // lane b stores row r + b (every lane holds every sum)
+          if (row < hi && lane == b) {
+            const uint32_t o = row_allowed(allow, row) ? (uint32_t)(make_key(s, 0) >> 32) : 0u;
+            ((uint32_t*)out)[row] = o;
+            if (o) atomicAdd(&lhist[o >> (32 - kRselBits0)], 1u);
+          }
+        } else if (row < hi && (GATHER || row_allowed(allow, row))) {
           const uint64_t key = make_key(s, row_base + (GATHER ? rows[row] : row));
           if (key > theta) {
             L.insert(key, k, lane);
@@ -613,7 +630,13 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
         for (int j = 0; j < S::J; ++j) buf[d][j] = buf[d + 1][j];
     }
   }
-  gemv_emit<KPL>(L, theta, k, lane, w, out);
+  if constexpr (kScores) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kRselBins; i += kGemvThreads)
+      if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+  } else {
+    gemv_emit<KPL>(L, theta, k, lane, w, out);
+  }
 }
 
 // Any dimension: one row per wave step, lane-strided scalar loads.
@@ -622,14 +645,20 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
     const void* __restrict__ Xv, uint32_t dim, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
     uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr) {
+    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr) {
+  constexpr bool kScores = KPL == 0;  // as in gemv_topk_kernel
+  __shared__ uint32_t lhist[kScores ? kRselBins : 1];
+  if constexpr (kScores) {
+    for (int i = threadIdx.x; i < kRselBins; i += kGemvThreads) lhist[i] = 0;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kGemvWaves + w;
   const uint64_t lo64 = gw * rows_per_wave;
   const uint32_t lo = lo64 < n_rows ? (uint32_t)lo64 : n_rows;
   const uint32_t hi = (uint64_t)lo + rows_per_wave < n_rows ? lo + rows_per_wave : n_rows;
-  WaveList<KPL> L;
+  WaveList<kScores ? 1 : KPL> L;
   L.init();
   uint64_t theta = 0;
   for (uint32_t pos = lo; pos < hi; ++pos) {
@@ -642,13 +671,27 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
       p = fmaf(x, q[d], p);
     }
     const float s = wave_sum(p);
+    if constexpr (kScores) {
+      if (lane == 0) {
+        const uint32_t o = row_allowed(allow, r) ? (uint32_t)(make_key(s, 0) >> 32) : 0u;
+        ((uint32_t*)out)[r] = o;
+        if (o) atomicAdd(&lhist[o >> (32 - kRselBits0)], 1u);
+      }
+      continue;
+    }
     const uint64_t key = make_key(s, row_base + r);
     if (key > theta && (GATHER || row_allowed(allow, r))) {
       L.insert(key, k, lane);
       theta = L.kth(k);
     }
   }
-  gemv_emit<KPL>(L, theta, k, lane, w, out);
+  if constexpr (kScores) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kRselBins; i += kGemvThreads)
+      if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+  } else {
+    gemv_emit<KPL>(L, theta, k, lane, w, out);
+  }
 }
 
 static int g_cu_count = 0;
@@ -812,6 +855,52 @@ hipError_t launch_gemv(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                                         max_lists, nlists, st, rows);
   }
 #undef VS_GEMV_CASE
+}
+
+template <int D, bool BF16>
+static hipError_t gemv_scores_d(const void* X, uint32_t n_rows, const float* q,
+                                const uint64_t* allow, uint32_t* sc, uint32_t* hist,
+                                hipStream_t st) {
+  using S = GemvShape<D, BF16>;
+  const GemvGrid g = gemv_grid(n_rows, S::RB);
+  hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 0, false>), dim3(g.nwg), dim3(kGemvThreads), 0, st,
+                     X, n_rows, 0u, q, allow, 0u, g.rows_per_wave, (uint64_t*)sc, nullptr, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                              const float* q, const uint64_t* allow, uint32_t* sc, uint32_t* hist,
+                              hipStream_t st) {
+  if (n_rows == 0) return hipErrorInvalidValue;
+#define VS_SCORES_CASE(DD) \
+  case DD:                 \
+    return bf16 ? gemv_scores_d<DD, true>(X, n_rows, q, allow, sc, hist, st) \
+                : gemv_scores_d<DD, false>(X, n_rows, q, allow, sc, hist, st);
+  switch (dim) {
+    VS_SCORES_CASE(128)
+    VS_SCORES_CASE(256)
+    VS_SCORES_CASE(384)
+    VS_SCORES_CASE(512)
+    VS_SCORES_CASE(768)
+    VS_SCORES_CASE(1024)
+    VS_SCORES_CASE(1536)
+    VS_SCORES_CASE(2048)
+    VS_SCORES_CASE(3072)
+    VS_SCORES_CASE(4096)
+    default: {
+      const GemvGrid g = gemv_grid(n_rows, 1);
+      if (bf16)
+        hipLaunchKernelGGL((gemv_topk_generic_kernel<true, 0, false>), dim3(g.nwg),
+                           dim3(kGemvThreads), 0, st, X, dim, n_rows, 0u, q, allow, 0u,
+                           g.rows_per_wave, (uint64_t*)sc, nullptr, hist);
+      else
+        hipLaunchKernelGGL((gemv_topk_generic_kernel<false, 0, false>), dim3(g.nwg),
+                           dim3(kGemvThreads), 0, st, X, dim, n_rows, 0u, q, allow, 0u,
+                           g.rows_per_wave, (uint64_t*)sc, nullptr, hist);
+      return hipGetLastError();
+    }
+  }
+#undef VS_SCORES_CASE
 }
 
 // Small collections, one query, k <= 16, no filter: query preprocessing,

@@ -176,7 +176,11 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n,
 /* Replaces Points.Search (main.go:249-254), batched: `nq` queries of `dim`
  * fp32 each (`dim` must equal the collection's, else VS_ERR_DIM_MISMATCH).
  * For query i, out_scores[i*k + j] / out_rows[i*k + j] hold the j-th best (score desc, row asc) for j < out_count[i] = min(k, rows).
- * Rows are global (row_base added). Blocking. k must be in [1, 1024]. */
+ * Rows are global (row_base added). Blocking. Any k >= 1 (Qdrant's limit
+ * is unbounded, main.go:252): k <= 1024 keeps the scans' register lists;
+ * larger k scores every row once and selects the k-th key by a radix select
+ * on the device (DESIGN.md §5 "Large k"). The output arrays are nq x k, so a
+ * caller passes k <= rows where rows is large. */
 int vs_search(vs_engine* eng, const char* coll, const float* queries,
               uint32_t nq, uint32_t dim, uint32_t k, float* out_scores,
               uint64_t* out_rows, uint32_t* out_count);

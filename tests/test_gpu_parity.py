@@ -455,8 +455,11 @@ rng = np.random.default_rng(5)
 bad = []
 # (lists, k_in, k, distinct keys): rank path (<= 512 keys), tournament path
 # (<= 8192 keys, k <= 32), general path (k > 32)
+# and the sort merge of k or k_in > 1024 (vs_select.hip launch_merge_large)
 for L, kin, k, nd in ((8, 10, 10, 6), (8, 10, 64, 30), (40, 100, 20, 15), (40, 100, 20, 300),
-                      (12, 100, 100, 50), (12, 100, 100, 700), (100, 100, 100, 2000)):
+                      (12, 100, 100, 50), (12, 100, 100, 700), (100, 100, 100, 2000),
+                      (4, 2000, 3000, 5000), (3, 1500, 1500, 2000), (8, 10, 2000, 50),
+                      (5, 1200, 1100, 900)):
     nq = 3
     pool = np.unique(rng.integers(1 << 40, 1 << 62, size=nd * 2, dtype=np.uint64))[:nd]
     lists = np.zeros((L, nq, kin), np.uint64)
@@ -484,7 +487,7 @@ print(json.dumps({"bad": bad[:5]}))
 def test_merge_dedupes_and_zero_fills():
     """vs_merge_keys with keys repeated across lists (overlapping shards), fewer
     distinct keys than k and a poisoned output: each key once, the rest 0, on
-    the rank, tournament and general paths."""
+    the rank, tournament and general paths and the large-k sort merge."""
     assert _run_py(_MERGE_DUP)["bad"] == []
 
 
