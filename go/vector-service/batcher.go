@@ -1,21 +1,30 @@
 package main
 
-import "gorilla-rag/vsearch"
+import (
+	"sync"
+
+	"gorilla-rag/vsearch"
+)
 
 // batcher coalesces concurrent /search requests into batched engine calls.
 // net/http runs every handler on its own goroutine (main.go:77); each one
-// hands its query here and waits. One goroutine makes one engine call per
-// turn for the collection of the oldest waiting request, with every waiting
-// request of that collection (up to maxBatch): a batch of queries streams
-// the corpus once (the MFMA path) instead of once per query. While a call
-// runs, new requests queue, so batches grow with the load and a lone request
-// waits for nothing. Exact: each request gets the first k of the batch's
-// k_max results, and results are totally ordered (score desc, row asc).
+// hands its query here and waits. One goroutine per device (lane) makes one
+// engine call per turn for the collection of the oldest waiting request,
+// with every waiting request of that collection (up to maxBatch): a batch of
+// queries streams the corpus once (the MFMA path) instead of once per query.
+// While a call runs, new requests queue, so batches grow with the load and a
+// lone request waits for nothing. Exact: each request gets the first k of
+// the batch's k_max results, and results are totally ordered (score desc,
+// row asc). Lanes: a request goes to the lane of its collection's device
+// (Engine.Placement; -1 for a row-striped collection), so with collections
+// placed on different GPUs (VS_PLACEMENT=collections) their calls run
+// concurrently.
 type batcher struct {
 	eng      *vsearch.Engine
 	dim      uint32
-	in       chan *pending
 	maxBatch int
+	mu       sync.Mutex
+	lanes    map[int]chan *pending
 }
 
 type pending struct {
@@ -35,25 +44,43 @@ type result struct {
 const kMFMA = 128
 
 func newBatcher(eng *vsearch.Engine, dim uint32) *batcher {
-	return &batcher{eng: eng, dim: dim, in: make(chan *pending, 4096), maxBatch: 256}
+	return &batcher{eng: eng, dim: dim, maxBatch: 256, lanes: map[int]chan *pending{}}
+}
+
+// lane returns the queue of the device holding coll, starting its goroutine
+// on first use.
+func (b *batcher) lane(coll string) chan *pending {
+	dev, err := b.eng.Placement(coll)
+	if err != nil {
+		dev = -1
+	}
+	b.mu.Lock()
+	defer b.mu.Unlock()
+	ch, ok := b.lanes[dev]
+	if !ok {
+		ch = make(chan *pending, 4096)
+		b.lanes[dev] = ch
+		go b.run(ch)
+	}
+	return ch
 }
 
 func (b *batcher) search(coll string, q []float32, k uint32) (vsearch.Hits, error) {
 	p := &pending{coll: coll, q: q, k: k, done: make(chan result, 1)}
-	b.in <- p
+	b.lane(coll) <- p
 	r := <-p.done
 	return r.hits, r.err
 }
 
-func (b *batcher) run() {
+func (b *batcher) run(in chan *pending) {
 	var queue []*pending
 	for {
 		if len(queue) == 0 {
-			queue = append(queue, <-b.in)
+			queue = append(queue, <-in)
 		}
 		for more := true; more; {
 			select {
-			case p := <-b.in:
+			case p := <-in:
 				queue = append(queue, p)
 			default:
 				more = false

@@ -10,6 +10,9 @@
 //	PORT            listen port (8082)
 //	VS_DEVICES      comma-separated HIP ordinals, one shard each ("0"); e.g.
 //	                "0,1,2,3,4,5,6,7" row-shards every collection over a node
+//	VS_PLACEMENT    with several devices: "stripes" (default, row shards) or
+//	                "collections" (each collection whole on one device; calls
+//	                for different collections run concurrently)
 //	VS_DTYPE        storage of the collections: "f32" (the reference's) or "bf16"
 //	VS_DIM          vector size (768: text-embedding-004)
 //	VS_SNAPSHOT_DIR when set: restore at start-up from here
@@ -48,6 +51,9 @@ func openEngine() (*vsearch.Engine, error) {
 	if len(devs) == 1 {
 		return vsearch.Open(devs[0])
 	}
+	if env("VS_PLACEMENT", "stripes") == "collections" {
+		return vsearch.OpenPlaced(devs)
+	}
 	return vsearch.OpenShards(devs)
 }
 
@@ -75,7 +81,6 @@ func main() {
 			log.Printf("Warning: restore from %s failed: %v", dir, err)
 		}
 	}
-	go svc.batch.run()
 
 	mux := http.NewServeMux()
 	mux.HandleFunc("/health", svc.health)

@@ -33,6 +33,9 @@ static int vsg_open_multi(const vs_config_multi* c, vs_engine** h, vsg_err* e) {
 static int vsg_engine_layout(vs_engine* h, uint32_t* s, uint32_t* d, vsg_err* e) {
 	return vsg_fin(vs_engine_layout(h, s, d), e);
 }
+static int vsg_collection_placement(vs_engine* h, const char* n, int32_t* d, vsg_err* e) {
+	return vsg_fin(vs_collection_placement(h, n, d), e);
+}
 static int vsg_collection_info(vs_engine* h, const char* n, uint32_t* d, uint64_t* r, vsg_err* e) {
 	return vsg_fin(vs_collection_info(h, n, d, r, NULL, NULL), e);
 }
@@ -175,11 +178,31 @@ func Open(device int) (*Engine, error) {
 	return &Engine{h}, nil
 }
 
+// OpenPlaced opens one engine over several devices that places every
+// collection whole on one of them (VS_FLAG_PLACE_COLLECTIONS): calls for
+// collections on different devices run concurrently, with no collective.
+func OpenPlaced(devices []int) (*Engine, error) {
+	return openMulti(devices, C.VS_FLAG_PLACE_COLLECTIONS)
+}
+
+// Placement reports the HIP device holding the whole collection, or -1 when
+// it is row-striped over several.
+func (e *Engine) Placement(name string) (int, error) {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var d C.int32_t
+	var ce C.vsg_err
+	err := check(C.vsg_collection_placement(e.h, cs, &d, &ce), &ce)
+	return int(d), err
+}
+
 // OpenShards opens one engine over row shards: shard s on HIP device
 // devices[s] (a device may repeat). Collections are then row-striped over
 // the shards and each search ends in one RCCL all-gather; every other call
 // is unchanged.
-func OpenShards(devices []int) (*Engine, error) {
+func OpenShards(devices []int) (*Engine, error) { return openMulti(devices, 0) }
+
+func openMulti(devices []int, flags C.uint32_t) (*Engine, error) {
 	if len(devices) == 0 {
 		return nil, fmt.Errorf("vsearch: no devices: %w", ErrInvalidArg)
 	}
@@ -189,7 +212,7 @@ func OpenShards(devices []int) (*Engine, error) {
 	for i, d := range devices {
 		ds[i] = C.int32_t(d)
 	}
-	cfg := C.vs_config_multi{devices: devs, n_shards: C.uint32_t(len(devices))}
+	cfg := C.vs_config_multi{devices: devs, n_shards: C.uint32_t(len(devices)), flags: flags}
 	var h *C.vs_engine
 	var e C.vsg_err
 	if err := check(C.vsg_open_multi(&cfg, &h, &e), &e); err != nil {

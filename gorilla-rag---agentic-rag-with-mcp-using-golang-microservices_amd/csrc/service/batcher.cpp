@@ -26,6 +26,7 @@ struct Batcher::Req {
   int rc = VS_OK;
   std::string err;
   bool done = false;
+  int lane = -1;  // the collection's device (vs_collection_placement)
   std::condition_variable* cv = nullptr;  // the waiter's
 };
 
@@ -66,17 +67,21 @@ int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint3
     if (err) *err = "service is closing";
     return VS_ERR_INVALID_ARG;
   }
-  if (opt_.caller_runs && !opt_.max_wait_us && queue_.empty() && inflight_end_.empty()) {
-    // Nothing queued and nothing in flight: run this request on the calling
-    // thread (no hand-off to a worker and back: two thread wake-ups less on
-    // an idle service). Requests arriving meanwhile queue as usual and the
-    // workers treat this call as one in flight.
+  r.lane = lane_of(coll);
+  bool lane_queued = false;
+  for (const Req* x : queue_) lane_queued = lane_queued || x->lane == r.lane;
+  if (opt_.caller_runs && !opt_.max_wait_us && !lane_queued &&
+      lanes_[r.lane].inflight_end.empty()) {
+    // Nothing queued and nothing in flight on this request's device: run it
+    // on the calling thread (no hand-off to a worker and back: two thread
+    // wake-ups less on an idle service). Requests arriving meanwhile queue as
+    // usual and the workers treat this call as one in flight.
     std::vector<Req*> batch{&r};
-    const int64_t t0 = now_us(), end = begin_call(coll, t0);
+    const int64_t t0 = now_us(), end = begin_call(coll, r.lane, t0);
     lk.unlock();
     execute(batch);
     lk.lock();
-    end_call(coll, t0, end);
+    end_call(coll, r.lane, t0, end);
     cv_.notify_all();
   } else {
     queue_.push_back(&r);
@@ -87,28 +92,52 @@ int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint3
   return r.rc;
 }
 
-// (mu_ held) registers a call of `coll` starting at t0: the device runs the
-// calls in flight one after another, so it starts when the ones ahead of it
-// are expected to end, and takes its collection's recent service time.
-// Returns its expected end.
-int64_t Batcher::begin_call(const std::string& coll, int64_t t0) {
+int Batcher::lane_of(const std::string& coll) {
+  int32_t dev = -1;
+  if (vs_collection_placement(eng_, coll.c_str(), &dev) != VS_OK) dev = -1;
+  return dev;
+}
+
+// The oldest queued request of a lane with the fewest calls in flight: an
+// idle device is served first, and within a lane requests keep their order.
+std::deque<Batcher::Req*>::iterator Batcher::pick() {
+  auto best = queue_.end();
+  size_t best_n = SIZE_MAX;
+  for (auto it = queue_.begin(); it != queue_.end(); ++it) {
+    const size_t n = lanes_[(*it)->lane].inflight_end.size();
+    if (n < best_n) {
+      best = it;
+      best_n = n;
+      if (n == 0) break;
+    }
+  }
+  return best;
+}
+
+// (mu_ held) registers a call of `coll` on `lane` starting at t0: a device
+// runs the calls in flight on it one after another, so it starts when the
+// ones ahead of it are expected to end, and takes its collection's recent
+// service time. Returns its expected end.
+int64_t Batcher::begin_call(const std::string& coll, int lane, int64_t t0) {
   auto est = call_us_.find(coll);
-  gpu_free_at_ = std::max(gpu_free_at_, t0) + (int64_t)(est == call_us_.end() ? 0.0 : est->second);
-  inflight_end_.push_back(gpu_free_at_);
-  return gpu_free_at_;
+  Lane& L = lanes_[lane];
+  L.free_at = std::max(L.free_at, t0) + (int64_t)(est == call_us_.end() ? 0.0 : est->second);
+  L.inflight_end.push_back(L.free_at);
+  return L.free_at;
 }
 
 // (mu_ held) the call registered as (t0, end) returned: its service time
-// (from its start, or from the previous call's end when it queued behind
-// one) updates the collection's average.
-void Batcher::end_call(const std::string& coll, int64_t t0, int64_t end) {
+// (from its start, or from the previous call's end on its device when it
+// queued behind one) updates the collection's average.
+void Batcher::end_call(const std::string& coll, int lane, int64_t t0, int64_t end) {
+  Lane& L = lanes_[lane];
   const int64_t t1 = now_us();
-  const double took = (double)(t1 - std::max(t0, last_done_));
-  last_done_ = t1;
+  const double took = (double)(t1 - std::max(t0, L.last_done));
+  L.last_done = t1;
   double& avg = call_us_[coll];
   avg = avg == 0.0 ? took : 0.8 * avg + 0.2 * took;
-  inflight_end_.erase(std::find(inflight_end_.begin(), inflight_end_.end(), end));
-  if (inflight_end_.empty()) gpu_free_at_ = 0;
+  L.inflight_end.erase(std::find(L.inflight_end.begin(), L.inflight_end.end(), end));
+  if (L.inflight_end.empty()) L.free_at = 0;
 }
 
 Stats Batcher::stats() {
@@ -128,26 +157,31 @@ void Batcher::run() {
       // another worker may have taken the whole queue while this one lingered
       if (queue_.empty()) continue;
     }
-    // Another call in flight: form this batch late, lead_us before the
-    // earliest in-flight call is expected to end (or at once when it ends
-    // earlier), so requests arriving in the meantime still join it.
-    if (opt_.lead_us && !inflight_end_.empty() && !stop_) {
-      const int64_t wake = *std::min_element(inflight_end_.begin(), inflight_end_.end()) -
-                           (int64_t)opt_.lead_us;
-      const size_t n0 = inflight_end_.size();
-      const int64_t t = now_us();
-      if (wake > t)
-        cv_.wait_until(lk, deadline_in(wake - t), [&] {
-          return stop_ || inflight_end_.size() < n0 || queue_.size() >= opt_.max_batch;
-        });
-      if (queue_.empty()) continue;  // another worker took it
+    // Another call in flight on the chosen request's device: form this batch
+    // late, lead_us before the earliest of them is expected to end (or at
+    // once when it ends earlier), so requests arriving in the meantime still
+    // join it.
+    {
+      const int lane = (*pick())->lane;
+      const std::vector<int64_t>& fl = lanes_[lane].inflight_end;
+      if (opt_.lead_us && !fl.empty() && !stop_) {
+        const int64_t wake = *std::min_element(fl.begin(), fl.end()) - (int64_t)opt_.lead_us;
+        const size_t n0 = fl.size();
+        const int64_t t = now_us();
+        if (wake > t)
+          cv_.wait_until(lk, deadline_in(wake - t), [&] {
+            return stop_ || lanes_[lane].inflight_end.size() < n0 ||
+                   queue_.size() >= opt_.max_batch;
+          });
+        if (queue_.empty()) continue;  // another worker took it
+      }
     }
     // One engine call per turn, for the group (collection, dim, k class) of
-    // the oldest queued request: all of that group's queued requests, up to
+    // the chosen request: all of that group's queued requests, up to
     // max_batch, go together; other groups keep queueing meanwhile, so the
     // next call of each collection finds its whole backlog (a group never
     // waits behind more than one call of every other group: no starvation).
-    const Req* first = queue_.front();
+    const Req* first = *pick();
     std::vector<Req*> batch;
     for (auto it = queue_.begin(); it != queue_.end() && batch.size() < opt_.max_batch;) {
       Req* r = *it;
@@ -159,12 +193,13 @@ void Batcher::run() {
         ++it;
       }
     }
-    const std::string coll = *first->coll;
-    const int64_t t0 = now_us(), end = begin_call(coll, t0);
+    const std::string coll = *batch.front()->coll;
+    const int lane = batch.front()->lane;
+    const int64_t t0 = now_us(), end = begin_call(coll, lane, t0);
     lk.unlock();
     execute(batch);
     lk.lock();
-    end_call(coll, t0, end);
+    end_call(coll, lane, t0, end);
     for (Req* r : batch) {
       r->done = true;
       r->cv->notify_one();

@@ -31,6 +31,14 @@
 // an idle batcher (nothing queued or in flight) runs on its own thread
 // (caller_runs): no hand-off to a worker and back.
 //
+// Devices (lanes): an engine that places collections on different devices
+// (VS_FLAG_PLACE_COLLECTIONS) runs their calls concurrently. Every request's
+// lane is its collection's device (vs_collection_placement; -1 for a striped
+// collection, which uses every device). The in-flight bookkeeping, the
+// lead_us timing and caller_runs are per lane, and a worker takes the oldest
+// request of the least busy lane, so a call on one device never waits for
+// the calls of another.
+//
 // Filtered requests ("filter":"match") carry the id of their device-resident
 // filter (vs_filter_create) and are grouped by it too: requests sharing a
 // filter become one vs_search_filter_id call (the MFMA pass with the bitmap
@@ -97,8 +105,12 @@ class Batcher {
   struct Req;
   void run();
   void execute(std::vector<Req*>& batch);
-  int64_t begin_call(const std::string& coll, int64_t t0);
-  void end_call(const std::string& coll, int64_t t0, int64_t end);
+  int64_t begin_call(const std::string& coll, int lane, int64_t t0);
+  void end_call(const std::string& coll, int lane, int64_t t0, int64_t end);
+
+  // (mu_ held) the lane of a collection, and the queued request to serve next
+  int lane_of(const std::string& coll);
+  std::deque<Req*>::iterator pick();
 
   vs_engine* eng_;
   Options opt_;
@@ -106,11 +118,14 @@ class Batcher {
   std::condition_variable cv_;
   std::deque<Req*> queue_;
   bool stop_ = false;
-  // calls in flight: expected end (steady clock, us) of each, and of the
-  // last one; end of the last call that completed; recent service time per
-  // collection (exponential average, us)
-  std::vector<int64_t> inflight_end_;
-  int64_t gpu_free_at_ = 0, last_done_ = 0;
+  // per lane (device): calls in flight, expected end (steady clock, us) of
+  // each and of the last one; end of the last call that completed
+  struct Lane {
+    std::vector<int64_t> inflight_end;
+    int64_t free_at = 0, last_done = 0;
+  };
+  std::map<int, Lane> lanes_;
+  // recent service time per collection (exponential average, us)
   std::map<std::string, double> call_us_;
   Stats stats_;
   std::vector<std::thread> workers_;

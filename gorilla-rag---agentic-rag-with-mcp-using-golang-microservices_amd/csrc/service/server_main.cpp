@@ -10,6 +10,10 @@
 //   VS_DEVICES         "0" (default) or a comma list "0,1,...,7": one engine
 //                      row-striping every collection over those devices
 //                      (vs_open_multi; RCCL all-gather of the per-device top-k)
+//   VS_PLACEMENT       "stripes" (default: every collection row-striped over
+//                      VS_DEVICES) or "collections" (each collection whole on
+//                      one device, calls for different collections concurrent,
+//                      no collective: VS_FLAG_PLACE_COLLECTIONS)
 //   VS_SERVICE_CONFIG  path of a vsvc_open config JSON (collections, batching,
 //                      filter mode); unset = the reference's defaults
 //   VS_DATA_DIR        restore every collection snapshotted there at start,
@@ -75,7 +79,13 @@ int main() {
     vs_config cfg = {devs[0], 0u};
     rc = vs_open(&cfg, &eng);
   } else {
-    vs_config_multi cfg = {devs.data(), (uint32_t)devs.size(), 0u};
+    const std::string placement = get_env("VS_PLACEMENT", "stripes");
+    if (placement != "stripes" && placement != "collections") {
+      std::fprintf(stderr, "vsearch_server: VS_PLACEMENT must be stripes or collections\n");
+      return 1;
+    }
+    vs_config_multi cfg = {devs.data(), (uint32_t)devs.size(),
+                           placement == "collections" ? VS_FLAG_PLACE_COLLECTIONS : 0u};
     rc = vs_open_multi(&cfg, &eng);
   }
   if (rc != VS_OK) return fail("vs_open", rc);

@@ -780,6 +780,7 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
   };
   std::vector<Spec> specs;
   vsbatch::Options bopt;
+  bool workers_given = false;
   bool filter_match = false;
   if (!config_json) {
     for (const char* n : {"regulatory_docs", "merchant_docs", "kyc_docs"})
@@ -822,8 +823,9 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
         bopt.max_batch = (uint32_t)m->num;
       }
       if (const Json* nw = b->get("workers")) {
-        if (nw->kind != Json::Number || nw->num < 1 || nw->num > 8) return VS_ERR_INVALID_ARG;
+        if (nw->kind != Json::Number || nw->num < 1 || nw->num > 16) return VS_ERR_INVALID_ARG;
         bopt.workers = (uint32_t)nw->num;
+        workers_given = true;
       }
       if (const Json* w = b->get("max_wait_us")) {
         if (w->kind != Json::Number || w->num < 0 || w->num > 1e6) return VS_ERR_INVALID_ARG;
@@ -858,6 +860,20 @@ int vsvc_open(vs_engine* eng, const char* config_json, vsvc** out) {
     cs->dim = dim ? dim : s.dim;
     svc->colls[s.name] = cs;
     svc->listed.push_back(s.name);
+  }
+  // collections placed on different devices (VS_FLAG_PLACE_COLLECTIONS) run
+  // their calls concurrently: two workers per device the collections use,
+  // unless the config says otherwise
+  if (!workers_given) {
+    std::vector<int32_t> lanes;
+    for (const auto& s : specs) {
+      int32_t d = -1;
+      if (vs_collection_placement(eng, s.name.c_str(), &d) == VS_OK &&
+          std::find(lanes.begin(), lanes.end(), d) == lanes.end())
+        lanes.push_back(d);
+    }
+    bopt.workers = (uint32_t)std::min<size_t>(16, 2 * std::max<size_t>(1, lanes.size()));
+    svc->batch_opt.workers = bopt.workers;
   }
   if (bopt.enabled) svc->batcher = std::make_unique<vsbatch::Batcher>(eng, bopt);
   *out = svc.release();

@@ -16,8 +16,18 @@
 //    this process) and merges the D lists on the first device; one D2H of
 //    nq x k keys. Messages are P x nq x k x 8 bytes: latency-bound.
 //
-// Both kinds answer the same C-ABI, so the C++ service mirror and the cgo
-// binding serve a sharded collection unchanged.
+//  * vs_open_multi with VS_FLAG_PLACE_COLLECTIONS: every collection lives
+//    whole on one of the devices (the least loaded at creation), and each
+//    call goes straight to that device's engine: calls for collections on
+//    different devices run concurrently, with no collective (the reference
+//    serves three independent collections from concurrent handlers,
+//    rag/vector-service/main.go:77, :80-119).
+//
+// All kinds answer the same C-ABI, so the C++ service mirror and the cgo
+// binding serve a sharded collection unchanged. A host search (vs_search*)
+// holds the devices' work locks only while it enqueues: its queries and keys
+// go through pinned per-call slots and it waits for the device outside the
+// locks, so concurrent calls overlap their host work with the devices'.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -52,15 +62,18 @@ struct SColl {
   uint64_t gen = 0;
   uint32_t dim = 0;
   int metric = VS_METRIC_COSINE, dtype = VS_DTYPE_F32;
-  uint64_t rows = 0;      // global rows
+  uint64_t rows = 0;      // global rows (striped collections)
   std::shared_mutex mu;   // upsert / generate / restore = writer, search = reader
   std::vector<std::string> iname;  // shard s -> its collection's name on its device
+  int home = -1;          // placed engines: index of the device holding the whole collection
+  uint64_t reserved = 0;  // placed: bytes counted against its device at creation
 };
 
 // A device-resident filter of a multi-shard engine: one per shard.
 struct SFilter {
   uint64_t coll_gen = 0, rows = 0;
-  std::vector<uint64_t> dev_fid;  // shard s -> filter id on its device engine
+  std::vector<uint64_t> dev_fid;   // shard s (placed: entry 0) -> filter id on its device engine
+  std::vector<uint32_t> dev_idx;   // ... and that device's index
 };
 
 int not_found(const char* name) {
@@ -84,8 +97,16 @@ struct vs_engine {
   struct Scratch {
     DevBuf q, keys, merged, gather, out, allow;
     hipEvent_t qev = nullptr;  // dev 0: the caller's queries are ready
+    hipEvent_t kev = nullptr;  // placed: this device's keys reached dev 0
   };
   std::vector<Scratch> scr;
+  // pinned staging of host searches (sharded_search_host), guarded by dev 0's work_mu
+  std::vector<std::unique_ptr<vsd::HostSlot>> host_slots;
+  // VS_FLAG_PLACE_COLLECTIONS: whole collections per device; bytes reserved
+  // and collections per device (the placement balance), guarded by map_mu
+  bool placed = false;
+  std::vector<uint64_t> dev_bytes;
+  std::vector<uint32_t> dev_colls;
   // one process per GPU (vs_comm_init): the ranks' communicator and the
   // all-gather output of vs_gather_merge_keys (guarded by dev[0]->work_mu)
   ncclComm_t pcomm = nullptr;
@@ -265,6 +286,8 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
                         d_out ? d_out : E->scr[0].out.as<uint64_t>());
 }
 
+DevEngine* home_eng(vs_engine* E, const SColl& sc) { return E->dev[sc.home]; }
+
 int sharded_search_host(vs_engine* E, const char* coll, const float* queries, uint32_t nq,
                         uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                         uint64_t filter_id, float* out_scores, uint64_t* out_rows,
@@ -274,6 +297,22 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
   if (!queries) return fail(VS_ERR_INVALID_ARG, "queries is NULL");
   auto sc = find_scoll(E, coll);
   if (!sc) return not_found(coll);
+  SFilter f;
+  if (filter_id) {
+    std::lock_guard<std::mutex> g(E->filt_mu);
+    auto it = E->filters.find(filter_id);
+    if (it == E->filters.end())
+      return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
+    f = it->second;
+  }
+  if (sc->home >= 0) {  // placed: the device engine's own (concurrent) host search
+    if (filter_id && f.coll_gen != sc->gen)
+      return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
+                                          " was built for another collection state");
+    return vsd::search_host(home_eng(E, *sc), sc->iname[0].c_str(), queries, nq, dim, k, allow,
+                            allow_words, out_scores, out_rows, out_count,
+                            filter_id ? f.dev_fid[0] : 0);
+  }
   if (dim != sc->dim)
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(sc->dim) + ", got " + std::to_string(dim));
@@ -282,30 +321,94 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
     return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
                                         " words, the collection needs " +
                                         std::to_string((sc->rows + 63) / 64));
-  SFilter f;
-  if (filter_id) {
-    std::lock_guard<std::mutex> g(E->filt_mu);
-    auto it = E->filters.find(filter_id);
-    if (it == E->filters.end())
-      return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
-    f = it->second;
-    if (f.coll_gen != sc->gen || f.rows != sc->rows)
-      return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
-                                          " was built for another collection state");
-  }
-  AllWork aw(E);
+  if (filter_id && (f.coll_gen != sc->gen || f.rows != sc->rows))
+    return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
+                                        " was built for another collection state");
+  const size_t qbytes = (size_t)nq * dim * 4, kbytes = (size_t)nq * k * 8;
   DevEngine* d0 = E->dev[0];
-  std::vector<std::vector<uint64_t>> bits_keep;  // alive until the sync below
-  int rc = sharded_search(E, *sc, queries, nullptr, false, nullptr, nq, k, allow, &bits_keep,
-                          filter_id ? &f : nullptr, nullptr);
-  if (rc != VS_OK) return rc;
-  d0->h_keys.resize((size_t)nq * k);
+  std::vector<std::vector<uint64_t>> bits_keep;  // alive until the wait below
+  AllWork aw(E);
+  // an idle pinned staging slot: the queries go H2D to every device from it
+  // and the keys come back into it, asynchronously (one slot per call in flight)
+  vsd::HostSlot* hs = nullptr;
+  for (auto& x : E->host_slots)
+    if (!x->busy) {
+      hs = x.get();
+      break;
+    }
+  if (!hs) {
+    E->host_slots.push_back(std::make_unique<vsd::HostSlot>());
+    hs = E->host_slots.back().get();
+  }
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
-  VS_HIP(hipMemcpyAsync(d0->h_keys.data(), E->scr[0].out.p, (size_t)nq * k * 8,
-                        hipMemcpyDeviceToHost, d0->stream),
-         "keys D2H");
-  VS_HIP(hipStreamSynchronize(d0->stream), "search sync");
-  vsd::decode_host(d0->h_keys.data(), nq, k, out_scores, out_rows, out_count);
+  VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
+  std::memcpy(hs->in, queries, qbytes);
+  hs->busy = true;
+  // a failure after the first enqueue drains every device before the slot is
+  // released (queued copies may still read or write it)
+  auto abandon = [&](int rc) {
+    const std::string msg = vsd::last_error();
+    for (DevEngine* de : E->dev) {
+      (void)vsd::set_dev(de);
+      (void)hipStreamSynchronize(de->stream);
+    }
+    hs->busy = false;
+    return fail(rc, msg);
+  };
+  int rc = sharded_search(E, *sc, (const float*)hs->in, nullptr, false, nullptr, nq, k, allow,
+                          &bits_keep, filter_id ? &f : nullptr, nullptr);
+  if (rc != VS_OK) return abandon(rc);
+  hipError_t e = vsd::set_dev(d0);
+  if (e != hipSuccess) return abandon(vsd::fail_hip(e, "hipSetDevice"));
+  e = hipMemcpyAsync(hs->out, E->scr[0].out.p, kbytes, hipMemcpyDeviceToHost, d0->stream);
+  if (e == hipSuccess) e = hipEventRecord(hs->done, d0->stream);
+  if (e != hipSuccess) return abandon(vsd::fail_hip(e, "keys D2H"));
+  // wait outside the work locks: the next call enqueues behind this one on
+  // every device (all scratch is ordered by the devices' streams)
+  aw.locks.clear();
+  const hipError_t we = vsd::wait_event(hs->done);
+  if (we == hipSuccess) vsd::decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+  {
+    std::lock_guard<std::mutex> g(d0->work_mu);
+    hs->busy = false;
+  }
+  VS_HIP(we, "search sync");
+  return VS_OK;
+}
+
+// The device-pointer search of a placed collection on device `home` != 0:
+// the queries (dev 0, ordered on cs) are copied to the home device, searched
+// there on its own stream, and the keys copied back to d_keys on dev 0; cs
+// waits for them. Holds the home device's work lock while it enqueues.
+int placed_search_keys(vs_engine* E, SColl& sc, const float* d_q, uint32_t nq, uint32_t k,
+                       uint64_t* d_keys, hipStream_t cs) {
+  DevEngine* d0 = E->dev[0];
+  DevEngine* de = home_eng(E, sc);
+  auto& sd = E->scr[sc.home];
+  auto c = vsd::find_coll(de, sc.iname[0].c_str());
+  if (!c) return not_found(sc.name.c_str());
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  const size_t qbytes = (size_t)nq * c->dim * 4, kbytes = (size_t)nq * k * 8;
+  std::unique_lock<std::mutex> g0(d0->work_mu, std::defer_lock), gh(de->work_mu, std::defer_lock);
+  std::lock(g0, gh);  // dev 0's events + the home device's scratch
+  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+  VS_HIP(hipEventRecord(E->scr[0].qev, cs), "query event");
+  VS_HIP(vsd::set_dev(de), "hipSetDevice");
+  VS_HIP(vsd::use_stream(de, de->own), "stream order");
+  if (sd.q.bytes < qbytes || sd.keys.bytes < kbytes) {
+    VS_HIP(hipStreamSynchronize(de->stream), "sync");
+    VS_HIP(sd.q.ensure(qbytes), "alloc queries");
+    VS_HIP(sd.keys.ensure(kbytes), "alloc keys");
+  }
+  VS_HIP(hipStreamWaitEvent(de->stream, E->scr[0].qev, 0), "query order");
+  VS_HIP(hipMemcpyPeerAsync(sd.q.p, de->device, d_q, d0->device, qbytes, de->stream), "query peer copy");
+  const int rc = vsd::search_core(de, *c, sd.q.as<float>(), nq, k, sd.keys.as<uint64_t>());
+  if (rc != VS_OK) return rc;
+  VS_HIP(hipMemcpyPeerAsync(d_keys, d0->device, sd.keys.p, de->device, kbytes, de->stream),
+         "keys peer copy");
+  VS_HIP(hipEventRecord(sd.kev, de->stream), "keys event");
+  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+  VS_HIP(hipStreamWaitEvent(cs, sd.kev, 0), "keys order");
   return VS_OK;
 }
 
@@ -369,13 +472,15 @@ uint64_t header_sum(const SnapHeader& h) {
 
 int sharded_drop(vs_engine* E, const char* name);
 int sharded_create(vs_engine* E, const char* name, uint32_t dim, int metric, int dtype,
-                   uint64_t capacity_hint, uint64_t row_base);
+                   uint64_t capacity_hint, uint64_t row_base, const char* restore_path = nullptr);
+void unplace(vs_engine* E, const SColl& sc);
 
 // The same file as an unsharded snapshot of the collection (rows in global
 // order, the global checksum), so a snapshot restores on any shard layout.
 int sharded_snapshot(vs_engine* E, const char* coll, const char* path) {
   auto sc = find_scoll(E, coll);
   if (!sc) return not_found(coll);
+  if (sc->home >= 0) return vsd::snapshot(home_eng(E, *sc), sc->iname[0].c_str(), path);
   std::shared_lock<std::shared_mutex> rl(sc->mu);  // upserts wait, searches proceed
   SnapHeader h{};
   std::memcpy(h.magic, kSnapMagic, 8);
@@ -415,6 +520,16 @@ int sharded_snapshot(vs_engine* E, const char* coll, const char* path) {
 }
 
 int sharded_restore(vs_engine* E, const char* coll, const char* path) {
+  if (E->placed) {  // dim / metric / dtype come from the file on the home device
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(VS_ERR_IO, std::string("cannot open ") + path);
+    SnapHeader h{};
+    const bool ok = std::fread(&h, sizeof(h), 1, f) == 1;
+    std::fclose(f);
+    if (!ok || std::memcmp(h.magic, kSnapMagic, 8) != 0)
+      return fail(VS_ERR_IO, std::string("not a vsearch snapshot (bad header): ") + path);
+    return sharded_create(E, coll, h.dim, h.metric, h.dtype, h.rows, h.row_base, path);
+  }
   FILE* f = std::fopen(path, "rb");
   if (!f) return fail(VS_ERR_IO, std::string("cannot open ") + path);
   SnapHeader h{};
@@ -480,17 +595,65 @@ int sharded_restore(vs_engine* E, const char* coll, const char* path) {
   return VS_OK;
 }
 
+// a placed collection leaves the engine's map and its device's balance
+void unplace(vs_engine* E, const SColl& sc) {
+  std::lock_guard<std::mutex> g(E->map_mu);
+  auto it = E->colls.find(sc.name);
+  if (it != E->colls.end() && it->second.get() == &sc) E->colls.erase(it);
+  E->dev_bytes[sc.home] -= sc.reserved;
+  E->dev_colls[sc.home] -= 1;
+}
+
+// restore_path (placed engines only): the collection is made by vs_restore of
+// that snapshot on its device instead of created empty
 int sharded_create(vs_engine* E, const char* name, uint32_t dim, int metric, int dtype,
-                   uint64_t capacity_hint, uint64_t row_base) {
+                   uint64_t capacity_hint, uint64_t row_base, const char* restore_path) {
   if (!name || !*name) return fail(VS_ERR_INVALID_ARG, "collection name required");
-  if (row_base != 0)
-    return fail(VS_ERR_INVALID_ARG, "row_base must be 0 on a sharded engine (rows are striped)");
   auto sc = std::make_shared<SColl>();
   sc->name = name;
   sc->gen = g_scoll_gen.fetch_add(1);
   sc->dim = dim;
   sc->metric = metric;
   sc->dtype = dtype;
+  if (E->placed) {
+    // the whole collection on the device with the fewest reserved bytes
+    // (then the fewest collections, then the lowest index)
+    sc->iname.push_back(std::string(name) + "\x1fp");
+    sc->reserved = capacity_hint * dim * (dtype == VS_DTYPE_BF16 ? 2u : 4u);
+    {
+      std::lock_guard<std::mutex> g(E->map_mu);
+      if (E->colls.count(name))
+        return fail(VS_ERR_EXISTS, std::string("collection ") + name + " already exists");
+      uint32_t best = 0;
+      for (uint32_t d = 1; d < E->dev.size(); ++d)
+        if (std::make_pair(E->dev_bytes[d], E->dev_colls[d]) <
+            std::make_pair(E->dev_bytes[best], E->dev_colls[best]))
+          best = d;
+      sc->home = (int)best;
+      E->dev_bytes[best] += sc->reserved;
+      E->dev_colls[best] += 1;
+      E->colls[name] = sc;
+    }
+    if (restore_path) {
+      const int rc = vsd::restore(home_eng(E, *sc), sc->iname[0].c_str(), restore_path);
+      if (rc != VS_OK) {
+        const std::string msg = vsd::last_error();
+        unplace(E, *sc);
+        return fail(rc, msg);
+      }
+      return VS_OK;
+    }
+    const int rc = vsd::collection_create(home_eng(E, *sc), sc->iname[0].c_str(), dim, metric,
+                                          dtype, capacity_hint, row_base);
+    if (rc != VS_OK) {
+      const std::string msg = vsd::last_error();
+      unplace(E, *sc);
+      return fail(rc, msg);
+    }
+    return VS_OK;
+  }
+  if (row_base != 0)
+    return fail(VS_ERR_INVALID_ARG, "row_base must be 0 on a sharded engine (rows are striped)");
   const uint32_t S = E->shards();
   for (uint32_t s = 0; s < S; ++s) sc->iname.push_back(std::string(name) + "\x1f" + std::to_string(s));
   {
@@ -529,6 +692,13 @@ int sharded_drop(vs_engine* E, const char* name) {
     for (auto it = E->filters.begin(); it != E->filters.end();)
       it = it->second.coll_gen == sc->gen ? E->filters.erase(it) : std::next(it);
   }
+  if (sc->home >= 0) {
+    (void)vsd::collection_drop(home_eng(E, *sc), sc->iname[0].c_str());  // frees its filters
+    std::lock_guard<std::mutex> g(E->map_mu);
+    E->dev_bytes[sc->home] -= sc->reserved;
+    E->dev_colls[sc->home] -= 1;
+    return VS_OK;
+  }
   for (uint32_t s = 0; s < E->shards(); ++s)
     (void)vsd::collection_drop(shard_eng(E, s), sc->iname[s].c_str());  // frees shard filters
   return VS_OK;
@@ -540,6 +710,7 @@ int sharded_upsert(vs_engine* E, const char* coll, uint64_t n, uint32_t dim, con
   if (!rows || !vecs) return fail(VS_ERR_INVALID_ARG, "rows and vecs are required");
   auto sc = find_scoll(E, coll);
   if (!sc) return not_found(coll);
+  if (sc->home >= 0) return vsd::upsert(home_eng(E, *sc), sc->iname[0].c_str(), n, dim, rows, vecs);
   if (dim != sc->dim)
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(sc->dim) + ", got " + std::to_string(dim));
@@ -577,6 +748,8 @@ int sharded_upsert(vs_engine* E, const char* coll, uint64_t n, uint32_t dim, con
 int sharded_generate(vs_engine* E, const char* coll, uint64_t n, uint64_t seed) {
   auto sc = find_scoll(E, coll);
   if (!sc) return not_found(coll);
+  if (sc->home >= 0)
+    return vsd::generate(home_eng(E, *sc), sc->iname[0].c_str(), n, seed, UINT64_MAX, 1);
   if (n == 0) return VS_OK;
   std::unique_lock<std::shared_mutex> wl(sc->mu);
   if (sc->rows + n >= 0xFFFFFFFFull) return fail(VS_ERR_INVALID_ARG, "too many rows");
@@ -597,13 +770,24 @@ int sharded_filter_create(vs_engine* E, const char* coll, const uint64_t* allow,
   if (!allow || !filter_id) return fail(VS_ERR_INVALID_ARG, "NULL argument");
   auto sc = find_scoll(E, coll);
   if (!sc) return not_found(coll);
+  SFilter f;
+  f.coll_gen = sc->gen;
+  if (sc->home >= 0) {  // the device engine binds it to the collection's state
+    uint64_t id = 0;
+    const int rc = vsd::filter_create(home_eng(E, *sc), sc->iname[0].c_str(), allow, allow_words, &id);
+    if (rc != VS_OK) return rc;
+    f.dev_fid.push_back(id);
+    f.dev_idx.push_back((uint32_t)sc->home);
+    std::lock_guard<std::mutex> g(E->filt_mu);
+    *filter_id = E->next_filter++;
+    E->filters.emplace(*filter_id, std::move(f));
+    return VS_OK;
+  }
   std::shared_lock<std::shared_mutex> rl(sc->mu);
   if (allow_words < (sc->rows + 63) / 64)
     return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
                                         " words, the collection needs " +
                                         std::to_string((sc->rows + 63) / 64));
-  SFilter f;
-  f.coll_gen = sc->gen;
   f.rows = sc->rows;
   std::vector<uint64_t> bits;
   for (uint32_t s = 0; s < E->shards(); ++s) {
@@ -617,6 +801,7 @@ int sharded_filter_create(vs_engine* E, const char* coll, const uint64_t* allow,
       return fail(rc, msg);
     }
     f.dev_fid.push_back(id);
+    f.dev_idx.push_back(E->shard_dev[s]);
   }
   std::lock_guard<std::mutex> g(E->filt_mu);
   *filter_id = E->next_filter++;
@@ -634,8 +819,8 @@ int sharded_filter_drop(vs_engine* E, uint64_t filter_id) {
     f = std::move(it->second);
     E->filters.erase(it);
   }
-  for (uint32_t s = 0; s < f.dev_fid.size(); ++s)
-    (void)vsd::filter_drop(shard_eng(E, s), f.dev_fid[s]);  // gone already if its shard was dropped
+  for (uint32_t s = 0; s < f.dev_fid.size(); ++s)  // gone already if its collection was dropped
+    (void)vsd::filter_drop(E->dev[f.dev_idx[s]], f.dev_fid[s]);
   return VS_OK;
 }
 
@@ -645,6 +830,7 @@ void destroy(vs_engine* E) {
     if (d < E->scr.size()) {
       if (E->dev[d]) (void)hipStreamSynchronize(E->dev[d]->stream);
       if (E->scr[d].qev) (void)hipEventDestroy(E->scr[d].qev);
+      if (E->scr[d].kev) (void)hipEventDestroy(E->scr[d].kev);
       auto& x = E->scr[d];  // freed with the device current
       for (DevBuf* b : {&x.q, &x.keys, &x.merged, &x.gather, &x.out, &x.allow}) b->release();
     }
@@ -653,6 +839,7 @@ void destroy(vs_engine* E) {
   if (!E->dev.empty() && E->dev[0]) {
     (void)hipSetDevice(E->dev[0]->device);
     (void)hipStreamSynchronize(E->dev[0]->stream);
+    E->host_slots.clear();
     E->pgather.release();
     if (E->pcomm) (void)ncclCommDestroy(E->pcomm);
   }
@@ -714,6 +901,7 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out) {
   }
   auto* E = new vs_engine();
   E->sharded = cfg->n_shards > 1;
+  E->placed = E->sharded && (cfg->flags & VS_FLAG_PLACE_COLLECTIONS);
   std::vector<int> devlist;
   for (uint32_t s = 0; s < cfg->n_shards; ++s) {
     auto it = std::find(devlist.begin(), devlist.end(), ord[s]);
@@ -735,21 +923,42 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out) {
   }
   if (E->sharded) {
     E->scr.resize(E->dev.size());
-    E->comm.assign(E->dev.size(), nullptr);
-    const ncclResult_t r = ncclCommInitAll(E->comm.data(), (int)devlist.size(), devlist.data());
-    if (r != ncclSuccess) {
-      const std::string msg = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
-      E->comm.clear();
-      destroy(E);
-      return fail(VS_ERR_DEVICE, msg);
+    if (!E->placed) {  // placed collections never exchange keys: no communicator
+      E->comm.assign(E->dev.size(), nullptr);
+      const ncclResult_t r = ncclCommInitAll(E->comm.data(), (int)devlist.size(), devlist.data());
+      if (r != ncclSuccess) {
+        const std::string msg = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+        E->comm.clear();
+        destroy(E);
+        return fail(VS_ERR_DEVICE, msg);
+      }
     }
-    (void)hipSetDevice(E->dev[0]->device);
-    if (hipEventCreateWithFlags(&E->scr[0].qev, hipEventDisableTiming) != hipSuccess) {
-      destroy(E);
-      return fail(VS_ERR_DEVICE, "event");
+    E->dev_bytes.assign(E->dev.size(), 0);
+    E->dev_colls.assign(E->dev.size(), 0);
+    for (size_t d = 0; d < E->dev.size(); ++d) {
+      (void)hipSetDevice(E->dev[d]->device);
+      if ((d == 0 && hipEventCreateWithFlags(&E->scr[0].qev, hipEventDisableTiming) != hipSuccess) ||
+          hipEventCreateWithFlags(&E->scr[d].kev, hipEventDisableTiming) != hipSuccess) {
+        destroy(E);
+        return fail(VS_ERR_DEVICE, "event");
+      }
     }
   }
   *out = E;
+  return VS_OK;
+}
+
+int vs_collection_placement(vs_engine* eng, const char* name, int32_t* device) {
+  if (!eng || !device) return fail(VS_ERR_INVALID_ARG, "engine and device are required");
+  if (!eng->sharded) {
+    if (!vsd::find_coll(eng->dev[0], name)) return not_found(name);
+    *device = eng->dev[0]->device;
+    return VS_OK;
+  }
+  auto sc = find_scoll(eng, name);
+  if (!sc) return not_found(name);
+  *device = sc->home >= 0 ? home_eng(eng, *sc)->device
+                          : (eng->dev.size() == 1 ? eng->dev[0]->device : -1);
   return VS_OK;
 }
 
@@ -783,6 +992,8 @@ int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim, uint64_t
   if (!eng->sharded) return vsd::collection_info(eng->dev[0], name, dim, rows, metric, dtype);
   auto sc = find_scoll(eng, name);
   if (!sc) return not_found(name);
+  if (sc->home >= 0)
+    return vsd::collection_info(home_eng(eng, *sc), sc->iname[0].c_str(), dim, rows, metric, dtype);
   std::shared_lock<std::shared_mutex> rl(sc->mu);
   if (dim) *dim = sc->dim;
   if (rows) *rows = sc->rows;
@@ -821,6 +1032,7 @@ int vs_read_rows(vs_engine* eng, const char* coll, uint64_t first, uint64_t n, f
   if (!eng->sharded) return vsd::read_rows(eng->dev[0], coll, first, n, out);
   auto sc = find_scoll(eng, coll);
   if (!sc) return not_found(coll);
+  if (sc->home >= 0) return vsd::read_rows(home_eng(eng, *sc), sc->iname[0].c_str(), first, n, out);
   std::shared_lock<std::shared_mutex> rl(sc->mu);
   if (first + n > sc->rows || first + n < first)
     return fail(VS_ERR_INVALID_ARG, "row range out of bounds");
@@ -886,6 +1098,18 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
   if (!d_queries || !d_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   auto sc = find_scoll(eng, coll);
   if (!sc) return not_found(coll);
+  if (sc->home == 0)
+    return vsd::search_keys(eng->dev[0], sc->iname[0].c_str(), d_queries, nq, dim, k, d_keys, stream);
+  if (sc->home > 0) {
+    uint32_t cdim = 0;
+    const int rc = vsd::collection_info(home_eng(eng, *sc), sc->iname[0].c_str(), &cdim, nullptr,
+                                        nullptr, nullptr);
+    if (rc != VS_OK) return rc;
+    if (dim != cdim)
+      return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
+                                           std::to_string(cdim) + ", got " + std::to_string(dim));
+    return placed_search_keys(eng, *sc, d_queries, nq, k, d_keys, (hipStream_t)stream);
+  }
   if (dim != sc->dim)
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(sc->dim) + ", got " + std::to_string(dim));
@@ -973,6 +1197,7 @@ int vs_checksum(vs_engine* eng, const char* coll, uint64_t* out) {
   if (!eng->sharded) return vsd::checksum(eng->dev[0], coll, out);
   auto sc = find_scoll(eng, coll);
   if (!sc) return not_found(coll);
+  if (sc->home >= 0) return vsd::checksum(home_eng(eng, *sc), sc->iname[0].c_str(), out);
   std::shared_lock<std::shared_mutex> rl(sc->mu);
   return sharded_checksum(eng, *sc, out);
 }

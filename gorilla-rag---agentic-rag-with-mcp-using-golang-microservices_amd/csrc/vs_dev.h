@@ -214,6 +214,8 @@ int health(DevEngine* eng, char* buf, size_t len);
 int timing(DevEngine* eng, double* scan_ms_sum, uint64_t* scan_count, double* merge_ms_sum,
            uint64_t* merge_count, int reset);
 uint64_t popcount_rows(const uint64_t* allow, uint64_t rows);
+// Waits for ev: a short spin on hipEventQuery, then hipEventSynchronize.
+hipError_t wait_event(hipEvent_t ev);
 
 // Search of device queries d_q (nq x dim fp32 on this device, ordered on
 // eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and

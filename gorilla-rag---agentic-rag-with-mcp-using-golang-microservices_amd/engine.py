@@ -36,6 +36,7 @@ DTYPE_BF16 = 1
 FLAG_TIMING = 1
 FLAG_TIMING_MERGE = 2
 FLAG_TIMING_SAMPLE = 4
+FLAG_PLACE_COLLECTIONS = 8
 
 # Every function include/vsearch.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -47,7 +48,7 @@ EXPORTS = (
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
     "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
     "vs_engine_layout", "vs_comm_unique_id", "vs_comm_init", "vs_gather_merge_keys",
-    "vs_copy_last_error", "vs_build_id",
+    "vs_copy_last_error", "vs_build_id", "vs_collection_placement",
 )
 COMM_ID_BYTES = 128
 
@@ -86,6 +87,7 @@ def load_library(path: str = LIB_PATH):
         "vs_open": ([ctypes.POINTER(_Config), ctypes.POINTER(vp)], i32),
         "vs_open_multi": ([ctypes.POINTER(_ConfigMulti), ctypes.POINTER(vp)], i32),
         "vs_engine_layout": ([vp, vp, vp], i32),
+        "vs_collection_placement": ([vp, cp, vp], i32),
         "vs_close": ([vp], None),
         "vs_device_count": ([], i32),
         "vs_collection_create": ([vp, cp, u32, i32, i32, u64, u64], i32),
@@ -170,14 +172,18 @@ class VectorEngine:
     ``shards``: HIP device ordinal of every shard (may repeat), e.g.
     ``[0, 1, 2, 3, 4, 5, 6, 7]`` for one shard per GPU of a node; collections
     are then row-striped over the shards and searched with one RCCL
-    all-gather per call (include/vsearch.h "multi-GPU engine")."""
+    all-gather per call (include/vsearch.h "multi-GPU engine"), or with
+    ``place_collections`` each placed whole on one device
+    (VS_FLAG_PLACE_COLLECTIONS)."""
 
     def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False,
-                 timing_sample: bool = False, shards: Optional[Sequence[int]] = None):
+                 timing_sample: bool = False, shards: Optional[Sequence[int]] = None,
+                 place_collections: bool = False):
         L = load_library()
         flags = ((FLAG_TIMING if timing else 0) |
                  (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
-                 (FLAG_TIMING_SAMPLE if timing and timing_sample else 0))
+                 (FLAG_TIMING_SAMPLE if timing and timing_sample else 0) |
+                 (FLAG_PLACE_COLLECTIONS if place_collections else 0))
         h = ctypes.c_void_p()
         if shards is None:
             cfg = _Config(device, flags)
@@ -194,6 +200,12 @@ class VectorEngine:
         s, d = ctypes.c_uint32(), ctypes.c_uint32()
         _check(self._L.vs_engine_layout(self._h, ctypes.byref(s), ctypes.byref(d)))
         return s.value, d.value
+
+    def placement(self, name: str) -> int:
+        """HIP device holding the whole collection, or -1 when it is row-striped."""
+        d = ctypes.c_int32()
+        _check(self._L.vs_collection_placement(self._h, name.encode(), ctypes.byref(d)))
+        return d.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -88,6 +88,16 @@ typedef struct vs_config {
  * first after a vs_timing reset (a sampled
  * average that keeps the event gaps out of 3 of 4 steps). */
 #define VS_FLAG_TIMING_SAMPLE 4u
+/* vs_open_multi only: place every collection WHOLE on one of the engine's
+ * devices (the one with the fewest bytes reserved by capacity hints, then
+ * the fewest collections) instead of row-striping it over all shards. Each
+ * call then goes to that device alone, so calls for collections on
+ * different devices run concurrently and no collective is needed: the
+ * layout for several independent collections that each fit one HBM (config
+ * C5: 3 x 5M x 1024 bf16 = 10 GB each; the reference serves three
+ * collections from concurrent handlers, main.go:77, :80-119). Row-striping
+ * stays the layout for one collection larger than one device. */
+#define VS_FLAG_PLACE_COLLECTIONS 8u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 
@@ -108,7 +118,8 @@ void vs_close(vs_engine* eng);
  * shards of each device on that device, all-gathers one [nq][k] key list per
  * device over RCCL (one communicator from ncclCommInitAll) and merges them on
  * the first device, whose stream and memory the device-pointer forms use.
- * row_base must be 0 (stripes, not blocks). Snapshots of a sharded
+ * row_base must be 0 (stripes, not blocks; a placed collection, see
+ * VS_FLAG_PLACE_COLLECTIONS, takes any). Snapshots of a sharded
  * collection hold its rows in global order: the file is the same as that of
  * the collection on one device. n_shards == 1 is vs_open on devices[0]. */
 typedef struct vs_config_multi {
@@ -121,6 +132,11 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out);
 
 /* Shards and distinct devices of an engine (1 and 1 for vs_open). */
 int vs_engine_layout(vs_engine* eng, uint32_t* n_shards, uint32_t* n_devices);
+
+/* The HIP device ordinal holding the whole collection, or -1 when it is
+ * row-striped over several devices. Callers that schedule per device (the
+ * service's batcher) key their queues on it. */
+int vs_collection_placement(vs_engine* eng, const char* name, int32_t* device);
 
 /* Number of visible HIP devices (0 when none). Never fails. */
 int vs_device_count(void);

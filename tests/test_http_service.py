@@ -52,6 +52,7 @@ class _Lib:
         L.vsvc_http_stop.argtypes = [vp]
         L.vsvc_loadgen.argtypes = [vp, cp, ctypes.POINTER(vp)]
         L.vsvc_stats.argtypes = [vp, ctypes.POINTER(vp)]
+        L.vs_collection_placement.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_int32)]
         self.L = L
         self.eng = vp()
         assert L.vs_open(None, ctypes.byref(self.eng)) == 0
@@ -426,7 +427,14 @@ def test_batcher_policies_over_http(lib, server):
     concurrent keep-alive clients are coalesced into multi-query calls, two
     in flight, each request still answered with exactly its own top k."""
     st0 = lib.stats()
-    assert st0["batching"]["workers"] == 2 and st0["batching"]["caller_runs"]
+    # two workers per device the collections live on (the test double
+    # pretends two devices, vs_collection_placement by name hash)
+    devs = set()
+    for coll in json.loads(lib.handle("GET", "/collections")[1])["collections"]:
+        d = ctypes.c_int32()
+        assert lib.L.vs_collection_placement(lib.eng, coll.encode(), ctypes.byref(d)) == 0
+        devs.add(d.value)
+    assert st0["batching"]["workers"] == 2 * len(devs) and st0["batching"]["caller_runs"]
     c = http.client.HTTPConnection("127.0.0.1", server, timeout=30)
     for i in range(10):
         b = _search_body(5000 + i, "docs", 4)

@@ -330,3 +330,44 @@ def test_sharded_concurrent_calls(sharded, orc):
     finally:
         for nm in names + ["cc_up"]:
             sharded.drop_collection(nm)
+
+
+def test_two_concurrent_calls_overlap(sharded, orc):
+    """A sharded engine holds the devices' work locks only while it enqueues
+    (pinned per-call staging, the wait outside the locks): two threads
+    calling at once finish their calls in well under twice one thread's time.
+    Small collection (the host side of a call dominates), many calls."""
+    import threading
+    import time
+    dim, n = 256, 20_000
+    sharded.create_collection("ov", dim, 1, 1, n)
+    try:
+        sharded.generate("ov", n, orc.SEED_CORPUS)
+        Q = orc.generate(orc.SEED_QUERY, 3, 2, dim)
+        want = [sharded.search("ov", Q[i:i + 1], 10) for i in range(2)]
+        calls = 300
+
+        def run(i, out):
+            for _ in range(calls):
+                s, r, c = sharded.search("ov", Q[i:i + 1], 10)
+            out.append(np.array_equal(r, want[i][1]) and np.array_equal(s, want[i][0]))
+
+        for _ in range(30):
+            sharded.search("ov", Q[:1], 10)  # warm
+        ok = []
+        t0 = time.perf_counter()
+        run(0, ok)
+        one = time.perf_counter() - t0
+        th = [threading.Thread(target=run, args=(i, ok)) for i in range(2)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        two = time.perf_counter() - t0
+        assert all(ok)
+        print(f"one thread {one * 1e6 / calls:.1f} us/call; two threads {two * 1e6 / calls:.1f} "
+              f"us per pair of calls; ratio {two / one:.2f}")
+        assert two < 1.6 * one, (one, two)
+    finally:
+        sharded.drop_collection("ov")

@@ -70,6 +70,15 @@ int vs_open(const vs_config*, vs_engine** out) {
 
 void vs_close(vs_engine* e) { delete e; }
 
+// Two pretend devices: a collection's "device" is a hash of its name, so the
+// service's per-device batcher lanes run under TSAN too.
+int vs_collection_placement(vs_engine* e, const char* name, int32_t* device) {
+  std::shared_lock<std::shared_mutex> g(e->mu);
+  if (!e->colls.count(name)) return fail(VS_ERR_NOT_FOUND, "not found");
+  *device = (int32_t)(std::hash<std::string>()(name) % 2);
+  return VS_OK;
+}
+
 const char* vs_last_error(void) { return t_err.c_str(); }
 
 int vs_collection_create(vs_engine* e, const char* name, uint32_t dim, int metric, int dtype,

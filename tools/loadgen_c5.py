@@ -34,6 +34,12 @@ def main():
     ap.add_argument("--transport", default="inproc", choices=["inproc", "http", "both"])
     ap.add_argument("--server", action="store_true",
                     help="serve from a separate lib/vsearch_server process (HTTP only)")
+    ap.add_argument("--devices", default="0", help="--server: VS_DEVICES of the server")
+    ap.add_argument("--placement", default="stripes", choices=["stripes", "collections"],
+                    help="--server: VS_PLACEMENT of the server (with several devices)")
+    ap.add_argument("--workers-default", action="store_true",
+                    help="--server: leave the batcher's worker count to the service "
+                         "(two per device the collections use)")
     args = ap.parse_args()
     if args.server:
         return run_server(args)
@@ -105,13 +111,17 @@ def run_server(args):
     svcmod = import_module(pkg.__name__ + ".service")
     L = svcmod.load_service_library()
     names = ["regulatory_docs", "merchant_docs", "kyc_docs"]
+    batching = {"lead_us": args.lead_us}
+    if not args.workers_default:
+        batching["workers"] = args.workers
     cfg = {"collections": [{"name": n, "dim": args.dim, "metric": "Cosine", "dtype": "bf16"}
                            for n in names],
-           "batching": {"workers": args.workers, "lead_us": args.lead_us}}
+           "batching": batching}
     d = tempfile.mkdtemp(prefix="c5srv")
     cfgp = os.path.join(d, "cfg.json")
     open(cfgp, "w").write(js.dumps(cfg))
-    env = dict(os.environ, PORT="0", VS_SERVICE_CONFIG=cfgp,
+    env = dict(os.environ, PORT="0", VS_SERVICE_CONFIG=cfgp, VS_DEVICES=args.devices,
+               VS_PLACEMENT=args.placement,
                VS_BULK=",".join(f"{n}={args.rows}:{0x5EED + i}" for i, n in enumerate(names)))
     server = os.path.join(os.path.dirname(svcmod.SVC_LIB_PATH), "vsearch_server")
     t0 = time.time()
@@ -144,7 +154,9 @@ def run_server(args):
             line = {"workload": f"C5: 3 x {args.rows} x {args.dim} bf16, k in [3,50], closed "
                                 "loop, HTTP clients -> vsearch_server process",
                     "transport": "http (separate server process)", "clients": clients,
-                    "workers": args.workers, "lead_us": args.lead_us,
+                    "devices": args.devices, "placement": args.placement,
+                    "workers": "service default" if args.workers_default else args.workers,
+                    "lead_us": args.lead_us,
                     "qps": round(rep["qps"], 1), "requests": rep["requests"],
                     "errors": rep["errors"], "first_error": rep["first_error"][:200],
                     "lat_ms": {k: round(v, 3) for k, v in rep["lat_ms"].items()}}
