@@ -9,9 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -893,13 +894,21 @@ uint64_t popcount_rows(const uint64_t* allow, uint64_t rows) {
 // collection's search completes within tens of microseconds, and a blocking
 // wait adds the thread's wake-up to its latency), then a blocking wait (a
 // long scan does not keep a host core busy).
-constexpr int64_t kSpinUs = 60;
+// VS_SPIN_US overrides the 60 us (read once; 0 = block at once).
+int64_t spin_us() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("VS_SPIN_US");
+    return e ? (int64_t)std::atoll(e) : (int64_t)60;
+  }();
+  return v;
+}
 hipError_t wait_event(hipEvent_t ev) {
+  const int64_t lim = spin_us();
   const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
+  while (lim > 0) {
     const hipError_t q = hipEventQuery(ev);
     if (q != hipErrorNotReady) return q;
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(lim)) break;
   }
   return hipEventSynchronize(ev);
 }
