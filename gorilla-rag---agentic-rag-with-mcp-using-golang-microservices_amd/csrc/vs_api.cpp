@@ -87,21 +87,31 @@ struct vs_engine {
   std::vector<uint32_t> shard_dev;             // shard -> dev index
   std::vector<std::vector<uint32_t>> dev_shards;  // dev index -> its shards, ascending
   bool sharded = false;                        // vs_open_multi with more than one shard
-  std::vector<ncclComm_t> comm;                // one per dev (ncclCommInitAll)
   std::mutex map_mu;
   std::unordered_map<std::string, std::shared_ptr<SColl>> colls;
   std::mutex filt_mu;
   std::unordered_map<uint64_t, SFilter> filters;
   uint64_t next_filter = 1;
-  // per-device scratch of the multi-shard search (guarded by that device's work_mu)
+  // per-device scratch of the multi-shard search (guarded by that device
+  // context's work_mu)
   struct Scratch {
     DevBuf q, keys, merged, gather, out, allow;
     hipEvent_t qev = nullptr;  // dev 0: the caller's queries are ready
     hipEvent_t kev = nullptr;  // placed: this device's keys reached dev 0
   };
-  std::vector<Scratch> scr;
-  // pinned staging of host searches (sharded_search_host), guarded by dev 0's work_mu
-  std::vector<std::unique_ptr<vsd::HostSlot>> host_slots;
+  // One context set: search context j of every device (vs_dev.h DevStore),
+  // its scratch, its RCCL communicator (ncclCommInitAll; none when placed)
+  // and its pinned staging. Set 0 holds the devices' primary contexts (the
+  // device-pointer searches use it); a host search takes an idle set, so
+  // concurrent host searches run on separate streams of every device.
+  struct CtxSet {
+    std::vector<DevEngine*> dev;
+    std::vector<Scratch> scr;
+    std::vector<ncclComm_t> comm;
+    std::vector<std::unique_ptr<vsd::HostSlot>> host_slots;  // guarded by dev[0]'s work_mu
+    std::atomic<int> inflight{0};
+  };
+  std::vector<std::unique_ptr<CtxSet>> sets;
   // VS_FLAG_PLACE_COLLECTIONS: whole collections per device; bytes reserved
   // and collections per device (the placement balance), guarded by map_mu
   bool placed = false;
@@ -144,14 +154,46 @@ void deinterleave_bits(const uint64_t* allow, uint64_t rows, uint32_t S, uint32_
   }
 }
 
-// Holds every device's work lock, in device order (the one lock order of the
-// library: single-device calls take one of them).
+using CtxSet = vs_engine::CtxSet;
+
+// Holds the work lock of every device context of a set, in device order (the
+// one lock order of the library: single-device calls take one of them).
 struct AllWork {
   std::vector<std::unique_lock<std::mutex>> locks;
-  explicit AllWork(vs_engine* E) {
-    for (DevEngine* d : E->dev) locks.emplace_back(d->work_mu);
+  AllWork() = default;
+  explicit AllWork(const CtxSet& cs) {
+    for (DevEngine* d : cs.dev) locks.emplace_back(d->work_mu);
   }
 };
+
+// The context set a host search should use: an idle one whose locks are all
+// free (taken on return), else the least busy one (waited for).
+CtxSet* pick_set(vs_engine* E, AllWork* aw) {
+  for (auto& up : E->sets) {
+    CtxSet* cs = up.get();
+    if (cs->inflight.load(std::memory_order_relaxed) != 0) continue;
+    AllWork w;
+    bool ok = true;
+    for (DevEngine* d : cs->dev) {
+      std::unique_lock<std::mutex> g(d->work_mu, std::try_to_lock);
+      if (!g.owns_lock()) {
+        ok = false;
+        break;
+      }
+      w.locks.push_back(std::move(g));
+    }
+    if (ok) {
+      *aw = std::move(w);
+      return cs;
+    }
+  }
+  CtxSet* best = E->sets[0].get();
+  for (auto& up : E->sets)
+    if (up->inflight.load(std::memory_order_relaxed) < best->inflight.load(std::memory_order_relaxed))
+      best = up.get();
+  *aw = AllWork(*best);
+  return best;
+}
 
 int nccl_fail(ncclResult_t r, const char* what) {
   return fail(VS_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
@@ -167,16 +209,17 @@ struct ShardFilter {
 // The multi-shard search. Queries: host h_q, or device d_q0 on dev 0
 // (ordered on the caller's stream cs0 when caller_stream; dev 0's work then
 // runs on it). The final [nq][k] keys (global rows) are written
-// to d_out on dev 0 (null: the engine's result buffer E->scr[0].out),
+// to d_out on dev 0 (null: the engine's result buffer the set's scr[0].out),
 // ordered on dev 0's current stream. The caller holds
 // sc.mu (reader) and every device's work lock (AllWork).
 // Filters: h_allow (global bitmap, shipped per call; the per-shard host
 // bitmaps live in *bits_keep until the caller has synchronised) or fid
 // (resident).
-int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
+int sharded_search(vs_engine* E, CtxSet& cx, SColl& sc, const float* h_q, const float* d_q0,
                    bool caller_stream, hipStream_t cs0, uint32_t nq, uint32_t k,
                    const uint64_t* h_allow, std::vector<std::vector<uint64_t>>* bits_keep,
-                   const SFilter* fid, uint64_t* d_out) {
+                   const SFilter* fid, std::vector<std::shared_ptr<vsd::DevFilter>>* fkeep,
+                   uint64_t* d_out) {
   const uint32_t S = E->shards(), D = (uint32_t)E->dev.size(), dim = sc.dim;
   const size_t qbytes = (size_t)nq * dim * 4, lbytes = (size_t)nq * k * 8;
   std::vector<std::vector<std::shared_ptr<vsd::Collection>>> held(D);
@@ -185,8 +228,8 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
   // 1. every shard's scan, device by device (all asynchronous: the devices
   //    scan in parallel)
   for (uint32_t d = 0; d < D; ++d) {
-    DevEngine* de = E->dev[d];
-    auto& sc_d = E->scr[d];
+    DevEngine* de = cx.dev[d];
+    auto& sc_d = cx.scr[d];
     VS_HIP(vsd::set_dev(de), "hipSetDevice");
     VS_HIP(vsd::use_stream(de, d == 0 && caller_stream ? cs0 : de->own), "stream order");
     const uint32_t m = (uint32_t)E->dev_shards[d].size();
@@ -208,8 +251,8 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
     } else if (d == 0) {
       q_d = d_q0;
     } else {  // peer copy from dev 0, after the caller's stream produced them
-      VS_HIP(hipStreamWaitEvent(de->stream, E->scr[0].qev, 0), "query order");
-      VS_HIP(hipMemcpyPeerAsync(sc_d.q.p, de->device, d_q0, E->dev[0]->device, qbytes,
+      VS_HIP(hipStreamWaitEvent(de->stream, cx.scr[0].qev, 0), "query order");
+      VS_HIP(hipMemcpyPeerAsync(sc_d.q.p, de->device, d_q0, cx.dev[0]->device, qbytes,
                                 de->stream),
              "query peer copy");
       q_d = sc_d.q.as<float>();
@@ -233,9 +276,10 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
         f.bits = dst;
         f.allowed = vsd::popcount_rows(bits_tmp.data(), c->rows);
       } else if (fid) {
-        auto it = de->filters.find(fid->dev_fid[s]);
-        if (it == de->filters.end()) return fail(VS_ERR_NOT_FOUND, "filter shard not found");
-        const auto* df = it->second.get();
+        std::shared_ptr<vsd::DevFilter> dfp = vsd::find_filter(de, fid->dev_fid[s]);
+        if (!dfp) return fail(VS_ERR_NOT_FOUND, "filter shard not found");
+        const vsd::DevFilter* df = dfp.get();
+        fkeep->push_back(std::move(dfp));  // until the device is done with it
         if (df->coll_gen != c->gen || df->rows != c->rows)
           return fail(VS_ERR_INVALID_ARG, "filter was built for another collection state");
         f.bits = df->bits.as<uint64_t>();
@@ -250,8 +294,8 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
   // 2. local rows -> global rows; the shards of a device merged on it
   std::vector<const uint64_t*> send(D);
   for (uint32_t d = 0; d < D; ++d) {
-    DevEngine* de = E->dev[d];
-    auto& sc_d = E->scr[d];
+    DevEngine* de = cx.dev[d];
+    auto& sc_d = cx.scr[d];
     VS_HIP(vsd::set_dev(de), "hipSetDevice");
     const uint32_t m = (uint32_t)E->dev_shards[d].size();
     for (uint32_t j = 0; j < m; ++j)
@@ -271,8 +315,8 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
   ncclResult_t r = ncclGroupStart();
   if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
   for (uint32_t d = 0; d < D; ++d) {
-    r = ncclAllGather(send[d], E->scr[d].gather.p, (size_t)nq * k, ncclUint64, E->comm[d],
-                      E->dev[d]->stream);
+    r = ncclAllGather(send[d], cx.scr[d].gather.p, (size_t)nq * k, ncclUint64, cx.comm[d],
+                      cx.dev[d]->stream);
     if (r != ncclSuccess) {
       (void)ncclGroupEnd();
       return nccl_fail(r, "ncclAllGather");
@@ -280,10 +324,10 @@ int sharded_search(vs_engine* E, SColl& sc, const float* h_q, const float* d_q0,
   }
   r = ncclGroupEnd();
   if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
-  DevEngine* d0 = E->dev[0];
+  DevEngine* d0 = cx.dev[0];
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
-  return vsd::merge_any(d0, E->scr[0].gather.as<uint64_t>(), D, (uint64_t)nq * k, k, nq, k, k,
-                        d_out ? d_out : E->scr[0].out.as<uint64_t>());
+  return vsd::merge_any(d0, cx.scr[0].gather.as<uint64_t>(), D, (uint64_t)nq * k, k, nq, k, k,
+                        d_out ? d_out : cx.scr[0].out.as<uint64_t>());
 }
 
 DevEngine* home_eng(vs_engine* E, const SColl& sc) { return E->dev[sc.home]; }
@@ -325,20 +369,29 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
     return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
                                         " was built for another collection state");
   const size_t qbytes = (size_t)nq * dim * 4, kbytes = (size_t)nq * k * 8;
-  DevEngine* d0 = E->dev[0];
   std::vector<std::vector<uint64_t>> bits_keep;  // alive until the wait below
-  AllWork aw(E);
+  std::vector<std::shared_ptr<vsd::DevFilter>> fkeep;  // likewise
+  // a context set (one search context per device): an idle one if any, so
+  // concurrent host searches run on separate streams of every device
+  AllWork aw;
+  CtxSet& cx = *pick_set(E, &aw);
+  cx.inflight.fetch_add(1, std::memory_order_relaxed);
+  struct Leave {
+    CtxSet& cx;
+    ~Leave() { cx.inflight.fetch_sub(1, std::memory_order_relaxed); }
+  } leave{cx};
+  DevEngine* d0 = cx.dev[0];
   // an idle pinned staging slot: the queries go H2D to every device from it
   // and the keys come back into it, asynchronously (one slot per call in flight)
   vsd::HostSlot* hs = nullptr;
-  for (auto& x : E->host_slots)
+  for (auto& x : cx.host_slots)
     if (!x->busy) {
       hs = x.get();
       break;
     }
   if (!hs) {
-    E->host_slots.push_back(std::make_unique<vsd::HostSlot>());
-    hs = E->host_slots.back().get();
+    cx.host_slots.push_back(std::make_unique<vsd::HostSlot>());
+    hs = cx.host_slots.back().get();
   }
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
   VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
@@ -348,19 +401,19 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
   // released (queued copies may still read or write it)
   auto abandon = [&](int rc) {
     const std::string msg = vsd::last_error();
-    for (DevEngine* de : E->dev) {
+    for (DevEngine* de : cx.dev) {
       (void)vsd::set_dev(de);
       (void)hipStreamSynchronize(de->stream);
     }
     hs->busy = false;
     return fail(rc, msg);
   };
-  int rc = sharded_search(E, *sc, (const float*)hs->in, nullptr, false, nullptr, nq, k, allow,
-                          &bits_keep, filter_id ? &f : nullptr, nullptr);
+  int rc = sharded_search(E, cx, *sc, (const float*)hs->in, nullptr, false, nullptr, nq, k, allow,
+                          &bits_keep, filter_id ? &f : nullptr, &fkeep, nullptr);
   if (rc != VS_OK) return abandon(rc);
   hipError_t e = vsd::set_dev(d0);
   if (e != hipSuccess) return abandon(vsd::fail_hip(e, "hipSetDevice"));
-  e = hipMemcpyAsync(hs->out, E->scr[0].out.p, kbytes, hipMemcpyDeviceToHost, d0->stream);
+  e = hipMemcpyAsync(hs->out, cx.scr[0].out.p, kbytes, hipMemcpyDeviceToHost, d0->stream);
   if (e == hipSuccess) e = hipEventRecord(hs->done, d0->stream);
   if (e != hipSuccess) return abandon(vsd::fail_hip(e, "keys D2H"));
   // wait outside the work locks: the next call enqueues behind this one on
@@ -382,9 +435,10 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
 // waits for them. Holds the home device's work lock while it enqueues.
 int placed_search_keys(vs_engine* E, SColl& sc, const float* d_q, uint32_t nq, uint32_t k,
                        uint64_t* d_keys, hipStream_t cs) {
+  CtxSet& cx = *E->sets[0];  // the primary contexts, as every device-pointer search
   DevEngine* d0 = E->dev[0];
   DevEngine* de = home_eng(E, sc);
-  auto& sd = E->scr[sc.home];
+  auto& sd = cx.scr[sc.home];
   auto c = vsd::find_coll(de, sc.iname[0].c_str());
   if (!c) return not_found(sc.name.c_str());
   std::shared_lock<std::shared_mutex> rl(c->mu);
@@ -392,7 +446,7 @@ int placed_search_keys(vs_engine* E, SColl& sc, const float* d_q, uint32_t nq, u
   std::unique_lock<std::mutex> g0(d0->work_mu, std::defer_lock), gh(de->work_mu, std::defer_lock);
   std::lock(g0, gh);  // dev 0's events + the home device's scratch
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
-  VS_HIP(hipEventRecord(E->scr[0].qev, cs), "query event");
+  VS_HIP(hipEventRecord(cx.scr[0].qev, cs), "query event");
   VS_HIP(vsd::set_dev(de), "hipSetDevice");
   VS_HIP(vsd::use_stream(de, de->own), "stream order");
   if (sd.q.bytes < qbytes || sd.keys.bytes < kbytes) {
@@ -400,7 +454,7 @@ int placed_search_keys(vs_engine* E, SColl& sc, const float* d_q, uint32_t nq, u
     VS_HIP(sd.q.ensure(qbytes), "alloc queries");
     VS_HIP(sd.keys.ensure(kbytes), "alloc keys");
   }
-  VS_HIP(hipStreamWaitEvent(de->stream, E->scr[0].qev, 0), "query order");
+  VS_HIP(hipStreamWaitEvent(de->stream, cx.scr[0].qev, 0), "query order");
   VS_HIP(hipMemcpyPeerAsync(sd.q.p, de->device, d_q, d0->device, qbytes, de->stream), "query peer copy");
   const int rc = vsd::search_core(de, *c, sd.q.as<float>(), nq, k, sd.keys.as<uint64_t>());
   if (rc != VS_OK) return rc;
@@ -825,21 +879,29 @@ int sharded_filter_drop(vs_engine* E, uint64_t filter_id) {
 }
 
 void destroy(vs_engine* E) {
-  for (size_t d = 0; d < E->dev.size(); ++d) {
-    if (E->dev[d]) (void)hipSetDevice(E->dev[d]->device);
-    if (d < E->scr.size()) {
-      if (E->dev[d]) (void)hipStreamSynchronize(E->dev[d]->stream);
-      if (E->scr[d].qev) (void)hipEventDestroy(E->scr[d].qev);
-      if (E->scr[d].kev) (void)hipEventDestroy(E->scr[d].kev);
-      auto& x = E->scr[d];  // freed with the device current
-      for (DevBuf* b : {&x.q, &x.keys, &x.merged, &x.gather, &x.out, &x.allow}) b->release();
+  for (auto& up : E->sets) {
+    CtxSet& cx = *up;
+    for (size_t d = 0; d < cx.dev.size(); ++d) {
+      if (!cx.dev[d]) continue;
+      (void)hipSetDevice(cx.dev[d]->device);
+      (void)hipStreamSynchronize(cx.dev[d]->stream);
+      if (d < cx.scr.size()) {
+        auto& x = cx.scr[d];  // freed with the device current
+        if (x.qev) (void)hipEventDestroy(x.qev);
+        if (x.kev) (void)hipEventDestroy(x.kev);
+        for (DevBuf* b : {&x.q, &x.keys, &x.merged, &x.gather, &x.out, &x.allow}) b->release();
+      }
+      if (d < cx.comm.size() && cx.comm[d]) (void)ncclCommDestroy(cx.comm[d]);
     }
-    if (d < E->comm.size() && E->comm[d]) (void)ncclCommDestroy(E->comm[d]);
+    if (!cx.dev.empty() && cx.dev[0]) {
+      (void)hipSetDevice(cx.dev[0]->device);
+      cx.host_slots.clear();
+    }
   }
+  E->sets.clear();
   if (!E->dev.empty() && E->dev[0]) {
     (void)hipSetDevice(E->dev[0]->device);
     (void)hipStreamSynchronize(E->dev[0]->stream);
-    E->host_slots.clear();
     E->pgather.release();
     if (E->pcomm) (void)ncclCommDestroy(E->pcomm);
   }
@@ -922,25 +984,34 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out) {
     E->dev_shards[d].push_back(s);
   }
   if (E->sharded) {
-    E->scr.resize(E->dev.size());
-    if (!E->placed) {  // placed collections never exchange keys: no communicator
-      E->comm.assign(E->dev.size(), nullptr);
-      const ncclResult_t r = ncclCommInitAll(E->comm.data(), (int)devlist.size(), devlist.data());
-      if (r != ncclSuccess) {
-        const std::string msg = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
-        E->comm.clear();
-        destroy(E);
-        return fail(VS_ERR_DEVICE, msg);
-      }
-    }
     E->dev_bytes.assign(E->dev.size(), 0);
     E->dev_colls.assign(E->dev.size(), 0);
-    for (size_t d = 0; d < E->dev.size(); ++d) {
-      (void)hipSetDevice(E->dev[d]->device);
-      if ((d == 0 && hipEventCreateWithFlags(&E->scr[0].qev, hipEventDisableTiming) != hipSuccess) ||
-          hipEventCreateWithFlags(&E->scr[d].kev, hipEventDisableTiming) != hipSuccess) {
-        destroy(E);
-        return fail(VS_ERR_DEVICE, "event");
+    // context set j = search context j of every device
+    size_t nsets = SIZE_MAX;
+    for (DevEngine* de : E->dev) nsets = std::min(nsets, de->store->ctx.size());
+    for (size_t j = 0; j < nsets; ++j) {
+      auto cs = std::make_unique<CtxSet>();
+      for (DevEngine* de : E->dev) cs->dev.push_back(de->store->ctx[j]);
+      cs->scr.resize(E->dev.size());
+      E->sets.push_back(std::move(cs));
+      CtxSet& cx = *E->sets.back();
+      if (!E->placed) {  // placed collections never exchange keys: no communicator
+        cx.comm.assign(E->dev.size(), nullptr);
+        const ncclResult_t r = ncclCommInitAll(cx.comm.data(), (int)devlist.size(), devlist.data());
+        if (r != ncclSuccess) {
+          const std::string msg = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+          cx.comm.clear();
+          destroy(E);
+          return fail(VS_ERR_DEVICE, msg);
+        }
+      }
+      for (size_t d = 0; d < E->dev.size(); ++d) {
+        (void)hipSetDevice(E->dev[d]->device);
+        if ((d == 0 && hipEventCreateWithFlags(&cx.scr[0].qev, hipEventDisableTiming) != hipSuccess) ||
+            hipEventCreateWithFlags(&cx.scr[d].kev, hipEventDisableTiming) != hipSuccess) {
+          destroy(E);
+          return fail(VS_ERR_DEVICE, "event");
+        }
       }
     }
   }
@@ -1114,14 +1185,15 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(sc->dim) + ", got " + std::to_string(dim));
   std::shared_lock<std::shared_mutex> rl(sc->mu);
-  AllWork aw(eng);
+  CtxSet& cx = *eng->sets[0];  // the primary contexts: the caller's stream orders the work
+  AllWork aw(cx);
   DevEngine* d0 = eng->dev[0];
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
   hipStream_t cs = (hipStream_t)stream;
   // the other devices copy the queries once the caller's stream wrote them
-  if (eng->dev.size() > 1) VS_HIP(hipEventRecord(eng->scr[0].qev, cs), "query event");
-  return sharded_search(eng, *sc, nullptr, d_queries, true, cs, nq, k, nullptr, nullptr, nullptr,
-                        d_keys);
+  if (eng->dev.size() > 1) VS_HIP(hipEventRecord(cx.scr[0].qev, cs), "query event");
+  return sharded_search(eng, cx, *sc, nullptr, d_queries, true, cs, nq, k, nullptr, nullptr,
+                        nullptr, nullptr, d_keys);
 }
 
 int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,

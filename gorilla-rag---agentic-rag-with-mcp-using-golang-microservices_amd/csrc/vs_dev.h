@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -122,15 +123,42 @@ struct HostSlot {
 };
 
 
+// A device-resident filter (vs_filter_create): bitmap, popcount and, when
+// selective, the compacted row list. Shared: a search holds its reference
+// until the device has finished with it, so a concurrent drop is safe.
+struct DevFilter {
+  std::string coll;
+  uint64_t coll_gen = 0;           // Collection::gen it was built for
+  uint64_t rows = 0, allowed = 0;  // collection rows it was built over
+  DevBuf bits, list;               // bitmap; compacted rows when selective
+};
+
+struct DevEngine;
+
+// What the search contexts of one device share: the resident collections and
+// filters. ctx[0] is the primary context (stores, filters, device-pointer
+// searches, snapshots); host searches take any idle context.
+struct DevStore {
+  std::mutex map_mu;
+  std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
+  std::mutex filt_mu;
+  std::unordered_map<uint64_t, std::shared_ptr<DevFilter>> filters;
+  uint64_t next_filter = 1;
+  std::vector<DevEngine*> ctx;
+};
+
+// One search context of a device: its stream, its scratch and its staging.
+// Contexts of a device run concurrently (separate streams): two host
+// searches on different contexts overlap on the device, not only on the host.
 struct DevEngine {
   int device = 0;
   uint32_t flags = 0;
-  hipStream_t own = nullptr;     // the engine's stream
+  hipStream_t own = nullptr;     // the context's stream
   hipStream_t stream = nullptr;  // the stream device work is enqueued on now (own or a caller's)
   hipEvent_t xev = nullptr;      // orders a newly used stream after the previous one
   std::string device_name;
-  std::mutex map_mu;
-  std::unordered_map<std::string, std::shared_ptr<Collection>> colls;
+  std::shared_ptr<DevStore> store;
+  std::atomic<int> inflight{0};  // host searches on this context not yet returned
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound, upsert_vecs, upsert_rows;
   DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
@@ -143,15 +171,6 @@ struct DevEngine {
   // zeroed between uses), select state, the selected keys, sort scratch;
   // large merges (vs_merge_keys / shard merges at k > kMaxK)
   DevBuf lk_sc, lk_hist, lk_state, lk_sel, lk_sort, merge_big;
-  // device-resident filters (vs_filter_create), guarded by work_mu
-  struct DevFilter {
-    std::string coll;
-    uint64_t coll_gen = 0;           // Collection::gen it was built for
-    uint64_t rows = 0, allowed = 0;  // collection rows it was built over
-    DevBuf bits, list;               // bitmap; compacted rows when selective
-  };
-  std::unordered_map<uint64_t, std::unique_ptr<DevFilter>> filters;
-  uint64_t next_filter = 1;
   std::vector<uint64_t> h_keys;
   std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing
@@ -164,9 +183,16 @@ struct DevEngine {
 };
 
 // ---- per-device operations (vs_engine.cpp); same contracts as the C-ABI
-// functions of the same name, for one device and its local rows ----
+// functions of the same name, for one device and its local rows. `eng` is a
+// device's primary context unless said otherwise ----
+// Opens the primary context and VS_CONTEXTS - 1 more (default 2 in all).
 int open(int device, uint32_t flags, DevEngine** out);
-void close(DevEngine* eng);
+void close(DevEngine* eng);  // the primary: closes every context of the device
+// A filter of the device's store (nullptr: none); the reference keeps it alive.
+std::shared_ptr<DevFilter> find_filter(DevEngine* eng, uint64_t filter_id);
+// The context a host search should use: an idle one if any (locked on
+// return: `lk` owns its work_mu), else the least busy one (waited for).
+DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk);
 std::shared_ptr<Collection> find_coll(DevEngine* eng, const char* name);
 hipError_t set_dev(DevEngine* eng);
 hipError_t use_stream(DevEngine* eng, hipStream_t s);

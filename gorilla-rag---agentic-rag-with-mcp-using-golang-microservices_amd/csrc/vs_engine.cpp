@@ -45,9 +45,37 @@ int fail_hip(hipError_t e, const char* what) {
 std::atomic<uint64_t> g_coll_gen{1};
 
 std::shared_ptr<Collection> find_coll(DevEngine* eng, const char* name) {
-  std::lock_guard<std::mutex> g(eng->map_mu);
-  auto it = eng->colls.find(name ? name : "");
-  return it == eng->colls.end() ? nullptr : it->second;
+  DevStore& st = *eng->store;
+  std::lock_guard<std::mutex> g(st.map_mu);
+  auto it = st.colls.find(name ? name : "");
+  return it == st.colls.end() ? nullptr : it->second;
+}
+
+std::shared_ptr<DevFilter> find_filter(DevEngine* eng, uint64_t filter_id) {
+  DevStore& st = *eng->store;
+  std::lock_guard<std::mutex> g(st.filt_mu);
+  auto it = st.filters.find(filter_id);
+  return it == st.filters.end() ? nullptr : it->second;
+}
+
+DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk) {
+  const std::vector<DevEngine*>& cx = eng->store->ctx;
+  // an idle context first (no host search in flight on it), then any free lock
+  for (int pass = 0; pass < 2; ++pass)
+    for (DevEngine* c : cx) {
+      if (pass == 0 && c->inflight.load(std::memory_order_relaxed) != 0) continue;
+      std::unique_lock<std::mutex> g(c->work_mu, std::try_to_lock);
+      if (g.owns_lock()) {
+        *lk = std::move(g);
+        return c;
+      }
+    }
+  DevEngine* best = cx[0];
+  for (DevEngine* c : cx)
+    if (c->inflight.load(std::memory_order_relaxed) < best->inflight.load(std::memory_order_relaxed))
+      best = c;
+  *lk = std::unique_lock<std::mutex>(best->work_mu);
+  return best;
 }
 
 hipError_t set_dev(DevEngine* eng) { return hipSetDevice(eng->device); }
@@ -544,33 +572,17 @@ void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
 
 const char* last_error() { return g_last_error.c_str(); }
 
-int open(int dev, uint32_t flags, DevEngine** out) {
-  if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
-  *out = nullptr;
-  int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0)
-    return fail(VS_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
-  if (dev < 0) VS_HIP(hipGetDevice(&dev), "hipGetDevice");
-  if (dev >= n) return fail(VS_ERR_INVALID_ARG, "device ordinal out of range");
-  VS_HIP(hipSetDevice(dev), "hipSetDevice");
-  auto eng = std::make_unique<DevEngine>();
-  eng->device = dev;
-  eng->flags = flags;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
-    eng->device_name = std::string(prop.name) + " " + prop.gcnArchName;
-  VS_HIP(hipStreamCreateWithFlags(&eng->own, hipStreamNonBlocking), "stream");
-  eng->stream = eng->own;
-  VS_HIP(hipEventCreateWithFlags(&eng->xev, hipEventDisableTiming), "event");
-  vsk::device_cu_count();
-  *out = eng.release();
-  return VS_OK;
+// Search contexts per device (VS_CONTEXTS, read once; default 2, at most 8).
+int contexts_per_device() {
+  static const int v = [] {
+    const char* e = std::getenv("VS_CONTEXTS");
+    const int x = e ? std::atoi(e) : 2;
+    return x < 1 ? 1 : (x > 8 ? 8 : x);
+  }();
+  return v;
 }
 
-void close(DevEngine* eng) {
-  if (!eng) return;
-  (void)hipSetDevice(eng->device);
+void close_context(DevEngine* eng) {
   (void)hipStreamSynchronize(eng->stream);
   for (auto& p : eng->scan_ev) {
     (void)hipEventDestroy(p.a);
@@ -581,11 +593,66 @@ void close(DevEngine* eng) {
     (void)hipEventDestroy(p.b);
   }
   for (hipEvent_t ev : eng->ev_pool) (void)hipEventDestroy(ev);
-  eng->colls.clear();
+  eng->host_slots.clear();
   (void)hipStreamSynchronize(eng->own);
   if (eng->xev) (void)hipEventDestroy(eng->xev);
-  (void)hipStreamDestroy(eng->own);
+  if (eng->own) (void)hipStreamDestroy(eng->own);
   delete eng;
+}
+
+int open(int dev, uint32_t flags, DevEngine** out) {
+  if (!out) return fail(VS_ERR_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0)
+    return fail(VS_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
+  if (dev < 0) VS_HIP(hipGetDevice(&dev), "hipGetDevice");
+  if (dev >= n) return fail(VS_ERR_INVALID_ARG, "device ordinal out of range");
+  VS_HIP(hipSetDevice(dev), "hipSetDevice");
+  std::string name;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
+    name = std::string(prop.name) + " " + prop.gcnArchName;
+  auto store = std::make_shared<DevStore>();
+  const int nctx = contexts_per_device();
+  for (int i = 0; i < nctx; ++i) {
+    auto eng = std::make_unique<DevEngine>();
+    eng->device = dev;
+    eng->flags = flags;
+    eng->device_name = name;
+    eng->store = store;
+    hipError_t he = hipStreamCreateWithFlags(&eng->own, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&eng->xev, hipEventDisableTiming);
+    if (he != hipSuccess) {
+      const int rc = fail_hip(he, "context stream");
+      if (eng->own) (void)hipStreamDestroy(eng->own);
+      for (DevEngine* c : store->ctx) close_context(c);
+      return rc;
+    }
+    eng->stream = eng->own;
+    store->ctx.push_back(eng.release());
+  }
+  vsk::device_cu_count();
+  *out = store->ctx[0];
+  return VS_OK;
+}
+
+void close(DevEngine* eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->device);
+  std::shared_ptr<DevStore> st = eng->store;
+  for (DevEngine* c : st->ctx) (void)hipStreamSynchronize(c->stream);
+  {
+    std::lock_guard<std::mutex> g(st->filt_mu);
+    st->filters.clear();
+  }
+  {
+    std::lock_guard<std::mutex> g(st->map_mu);
+    st->colls.clear();
+  }
+  for (DevEngine* c : st->ctx) close_context(c);
+  st->ctx.clear();
 }
 
 int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric, int dtype,
@@ -604,11 +671,12 @@ int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric
   c->metric = metric;
   c->dtype = dtype;
   c->row_base = row_base;
+  DevStore& st = *eng->store;
   {
-    std::lock_guard<std::mutex> g(eng->map_mu);
-    if (eng->colls.count(name))
+    std::lock_guard<std::mutex> g(st.map_mu);
+    if (st.colls.count(name))
       return fail(VS_ERR_EXISTS, std::string("collection ") + name + " already exists");
-    eng->colls[name] = c;
+    st.colls[name] = c;
   }
   if (capacity_hint) {
     std::unique_lock<std::shared_mutex> wl(c->mu);
@@ -616,8 +684,8 @@ int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric
     VS_HIP(use_stream(eng, eng->own), "stream order");
     int rc = grow(eng, *c, capacity_hint);
     if (rc != VS_OK) {
-      std::lock_guard<std::mutex> g2(eng->map_mu);
-      eng->colls.erase(name);
+      std::lock_guard<std::mutex> g2(st.map_mu);
+      st.colls.erase(name);
       return rc;
     }
   }
@@ -641,14 +709,15 @@ int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* r
 int collection_drop(DevEngine* eng, const char* name) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   std::shared_ptr<Collection> c;
+  DevStore& st = *eng->store;
   {
-    std::lock_guard<std::mutex> g(eng->map_mu);
-    auto it = eng->colls.find(name ? name : "");
-    if (it == eng->colls.end())
+    std::lock_guard<std::mutex> g(st.map_mu);
+    auto it = st.colls.find(name ? name : "");
+    if (it == st.colls.end())
       return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (name ? name : "") +
                                         " not found");
     c = it->second;
-    eng->colls.erase(it);
+    st.colls.erase(it);
   }
   std::unique_lock<std::shared_mutex> wl(c->mu);
   std::lock_guard<std::mutex> g(eng->work_mu);
@@ -657,8 +726,9 @@ int collection_drop(DevEngine* eng, const char* name) {
   (void)hipStreamSynchronize(eng->stream);
   // the collection's resident filters go with it (their HBM, and no later
   // collection of the same name and row count can pick them up)
-  for (auto it = eng->filters.begin(); it != eng->filters.end();)
-    it = it->second->coll_gen == c->gen ? eng->filters.erase(it) : std::next(it);
+  std::lock_guard<std::mutex> gf(st.filt_mu);
+  for (auto it = st.filters.begin(); it != st.filters.end();)
+    it = it->second->coll_gen == c->gen ? st.filters.erase(it) : std::next(it);
   return VS_OK;  // memory released with the last reference
 }
 
@@ -932,38 +1002,46 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
                                         " words, the collection needs " +
                                         std::to_string((c->rows + 63) / 64));
-  std::unique_lock<std::mutex> g(eng->work_mu);
-  const DevEngine::DevFilter* df = nullptr;
+  // the filter stays referenced until the device is done with it (a
+  // concurrent vs_filter_drop only unlinks it)
+  std::shared_ptr<DevFilter> df;
   if (filter_id) {
-    auto it = eng->filters.find(filter_id);
-    if (it == eng->filters.end())
-      return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
-    df = it->second.get();
+    df = find_filter(eng, filter_id);
+    if (!df) return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
     if (df->coll_gen != c->gen || df->rows != c->rows)
       return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
                                           " was built for another collection state");
   }
-  VS_HIP(set_dev(eng), "hipSetDevice");
-  VS_HIP(use_stream(eng, eng->own), "stream order");
+  // a search context of the device: an idle one if any, so concurrent host
+  // searches run on separate streams (and overlap on the device)
+  std::unique_lock<std::mutex> g;
+  DevEngine* cx = pick_context(eng, &g);
+  cx->inflight.fetch_add(1, std::memory_order_relaxed);
+  struct Leave {
+    DevEngine* cx;
+    ~Leave() { cx->inflight.fetch_sub(1, std::memory_order_relaxed); }
+  } leave{cx};
+  VS_HIP(set_dev(cx), "hipSetDevice");
+  VS_HIP(use_stream(cx, cx->own), "stream order");
   const size_t qbytes = (size_t)nq * c->dim * 4;
   const size_t kbytes = (size_t)nq * k * 8;
   const size_t abytes = allow ? (size_t)((c->rows + 63) / 64) * 8 : 0;
-  if (eng->q_in.bytes < qbytes || eng->keys.bytes < kbytes || eng->allow.bytes < abytes) {
-    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-    VS_HIP(eng->q_in.ensure(qbytes), "alloc query input");
-    VS_HIP(eng->keys.ensure(kbytes), "alloc keys");
-    VS_HIP(eng->allow.ensure(abytes), "alloc filter bitmap");
+  if (cx->q_in.bytes < qbytes || cx->keys.bytes < kbytes || cx->allow.bytes < abytes) {
+    VS_HIP(hipStreamSynchronize(cx->stream), "sync");
+    VS_HIP(cx->q_in.ensure(qbytes), "alloc query input");
+    VS_HIP(cx->keys.ensure(kbytes), "alloc keys");
+    VS_HIP(cx->allow.ensure(abytes), "alloc filter bitmap");
   }
-  // an idle pinned staging slot (one per call in flight)
+  // an idle pinned staging slot (one per call in flight on this context)
   HostSlot* hs = nullptr;
-  for (auto& x : eng->host_slots)
+  for (auto& x : cx->host_slots)
     if (!x->busy) {
       hs = x.get();
       break;
     }
   if (!hs) {
-    eng->host_slots.push_back(std::make_unique<HostSlot>());
-    hs = eng->host_slots.back().get();
+    cx->host_slots.push_back(std::make_unique<HostSlot>());
+    hs = cx->host_slots.back().get();
   }
   VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
   std::memcpy(hs->in, queries, qbytes);
@@ -972,31 +1050,31 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   // read hs->in, a queued D2H write hs->out)
   hs->busy = true;
   auto abandon = [&](int rc) {
-    (void)hipStreamSynchronize(eng->stream);
+    (void)hipStreamSynchronize(cx->stream);
     hs->busy = false;
     return rc;
   };
-  hipError_t e = hipMemcpyAsync(eng->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, eng->stream);
+  hipError_t e = hipMemcpyAsync(cx->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "query H2D"));
   if (abytes) {  // pageable: HIP stages it (a shipped-bitmap call, not the batcher's path)
-    e = hipMemcpyAsync(eng->allow.p, allow, abytes, hipMemcpyHostToDevice, eng->stream);
+    e = hipMemcpyAsync(cx->allow.p, allow, abytes, hipMemcpyHostToDevice, cx->stream);
     if (e != hipSuccess) return abandon(fail_hip(e, "filter bitmap H2D"));
   }
   int rc;
   if (df)
-    rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
+    rc = search_core(cx, *c, cx->q_in.as<float>(), nq, k, cx->keys.as<uint64_t>(),
                      df->bits.as<uint64_t>(), df->allowed,
                      df->list.p ? df->list.as<uint32_t>() : nullptr);
   else
-    rc = search_core(eng, *c, eng->q_in.as<float>(), nq, k, eng->keys.as<uint64_t>(),
-                     abytes ? eng->allow.as<uint64_t>() : nullptr,
+    rc = search_core(cx, *c, cx->q_in.as<float>(), nq, k, cx->keys.as<uint64_t>(),
+                     abytes ? cx->allow.as<uint64_t>() : nullptr,
                      abytes ? popcount_rows(allow, c->rows) : 0);
   if (rc != VS_OK) return abandon(rc);
-  e = hipMemcpyAsync(hs->out, eng->keys.p, kbytes, hipMemcpyDeviceToHost, eng->stream);
-  if (e == hipSuccess) e = hipEventRecord(hs->done, eng->stream);
+  e = hipMemcpyAsync(hs->out, cx->keys.p, kbytes, hipMemcpyDeviceToHost, cx->stream);
+  if (e == hipSuccess) e = hipEventRecord(hs->done, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "keys D2H"));
-  // wait for the device outside work_mu: the next call (q_in, keys and every
-  // scratch buffer are ordered on the same stream) enqueues behind this one
+  // wait for the device outside work_mu: the next call on this context (its
+  // q_in, keys and scratch are ordered on its stream) enqueues behind this one
   g.unlock();
   const hipError_t we = wait_event(hs->done);
   if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
@@ -1021,7 +1099,7 @@ int filter_create(DevEngine* eng, const char* coll, const uint64_t* allow,
   std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(use_stream(eng, eng->own), "stream order");
-  auto f = std::make_unique<DevEngine::DevFilter>();
+  auto f = std::make_shared<DevFilter>();
   f->coll = coll;
   f->coll_gen = c->gen;
   f->rows = c->rows;
@@ -1043,21 +1121,31 @@ int filter_create(DevEngine* eng, const char* coll, const uint64_t* allow,
                                     eng->stream),
            "compact filter rows");
   }
-  VS_HIP(hipStreamSynchronize(eng->stream), "filter sync");
-  *filter_id = eng->next_filter++;
-  eng->filters.emplace(*filter_id, std::move(f));
+  VS_HIP(hipStreamSynchronize(eng->stream), "filter sync");  // ready for every context
+  DevStore& st = *eng->store;
+  std::lock_guard<std::mutex> gf(st.filt_mu);
+  *filter_id = st.next_filter++;
+  st.filters.emplace(*filter_id, std::move(f));
   return VS_OK;
 }
 
 int filter_drop(DevEngine* eng, uint64_t filter_id) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
-  std::lock_guard<std::mutex> g(eng->work_mu);
-  auto it = eng->filters.find(filter_id);
-  if (it == eng->filters.end())
-    return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
-  VS_HIP(set_dev(eng), "hipSetDevice");
-  VS_HIP(hipStreamSynchronize(eng->stream), "sync");  // no search still reads it
-  eng->filters.erase(it);
+  std::shared_ptr<DevFilter> f;  // freed here unless a search still holds it
+  {
+    DevStore& st = *eng->store;
+    std::lock_guard<std::mutex> gf(st.filt_mu);
+    auto it = st.filters.find(filter_id);
+    if (it == st.filters.end())
+      return fail(VS_ERR_NOT_FOUND, "filter " + std::to_string(filter_id) + " not found");
+    f = std::move(it->second);
+    st.filters.erase(it);
+  }
+  if (f.use_count() == 1) {  // the primary's device-pointer searches may still read it
+    std::lock_guard<std::mutex> g(eng->work_mu);
+    VS_HIP(set_dev(eng), "hipSetDevice");
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+  }
   return VS_OK;
 }
 
@@ -1271,8 +1359,8 @@ int health(DevEngine* eng, char* buf, size_t len) {
   }
   size_t ncoll;
   {
-    std::lock_guard<std::mutex> g(eng->map_mu);
-    ncoll = eng->colls.size();
+    std::lock_guard<std::mutex> g(eng->store->map_mu);
+    ncoll = eng->store->colls.size();
   }
   int n = std::snprintf(buf, len,
                         "{\"status\":\"%s\",\"engine\":\"vsearch-hip\",\"device\":%d,"
@@ -1288,32 +1376,37 @@ int health(DevEngine* eng, char* buf, size_t len) {
 int timing(DevEngine* eng, double* scan_ms_sum, uint64_t* scan_count, double* merge_ms_sum,
            uint64_t* merge_count, int reset) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
-  std::lock_guard<std::mutex> g(eng->work_mu);
   VS_HIP(set_dev(eng), "hipSetDevice");
   VS_HIP(hipDeviceSynchronize(), "timing sync");
-  auto drain = [eng](std::vector<EventPair>& v, double& acc, uint64_t& n) {
-    for (auto& p : v) {
-      float ms = 0.f;
-      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
-        acc += ms;
-        ++n;
+  double sm = 0, mm = 0;
+  uint64_t sn = 0, mn = 0;
+  for (DevEngine* cx : eng->store->ctx) {  // every search context of the device
+    std::lock_guard<std::mutex> g(cx->work_mu);
+    auto drain = [cx](std::vector<EventPair>& v, double& acc, uint64_t& n) {
+      for (auto& p : v) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+          acc += ms;
+          ++n;
+        }
+        cx->ev_pool.push_back(p.a);
+        cx->ev_pool.push_back(p.b);
       }
-      eng->ev_pool.push_back(p.a);
-      eng->ev_pool.push_back(p.b);
+      v.clear();
+    };
+    drain(cx->scan_ev, cx->scan_ms, cx->scan_n);
+    drain(cx->merge_ev, cx->merge_ms, cx->merge_n);
+    sm += cx->scan_ms, sn += cx->scan_n, mm += cx->merge_ms, mn += cx->merge_n;
+    if (reset) {
+      cx->scan_ms = cx->merge_ms = 0;
+      cx->scan_n = cx->merge_n = 0;
+      cx->scan_tick = 0;  // the next scan is bracketed (VS_FLAG_TIMING_SAMPLE)
     }
-    v.clear();
-  };
-  drain(eng->scan_ev, eng->scan_ms, eng->scan_n);
-  drain(eng->merge_ev, eng->merge_ms, eng->merge_n);
-  if (scan_ms_sum) *scan_ms_sum = eng->scan_ms;
-  if (scan_count) *scan_count = eng->scan_n;
-  if (merge_ms_sum) *merge_ms_sum = eng->merge_ms;
-  if (merge_count) *merge_count = eng->merge_n;
-  if (reset) {
-    eng->scan_ms = eng->merge_ms = 0;
-    eng->scan_n = eng->merge_n = 0;
-    eng->scan_tick = 0;  // the next scan is bracketed (VS_FLAG_TIMING_SAMPLE)
   }
+  if (scan_ms_sum) *scan_ms_sum = sm;
+  if (scan_count) *scan_count = sn;
+  if (merge_ms_sum) *merge_ms_sum = mm;
+  if (merge_count) *merge_count = mn;
   return VS_OK;
 }
 
