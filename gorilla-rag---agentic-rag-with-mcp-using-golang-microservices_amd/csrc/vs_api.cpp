@@ -166,9 +166,15 @@ struct AllWork {
   }
 };
 
-// The context set a host search should use: an idle one whose locks are all
-// free (taken on return), else the least busy one (waited for).
-CtxSet* pick_set(vs_engine* E, AllWork* aw) {
+// The context set a host search should use: set 0 for a heavy search
+// (vs_engine.cpp heavy_search: batched scans of large shards queue on one
+// stream per device), else an idle one whose locks are all free (taken on
+// return), else the least busy one (waited for).
+CtxSet* pick_set(vs_engine* E, AllWork* aw, bool heavy) {
+  if (heavy) {
+    *aw = AllWork(*E->sets[0]);
+    return E->sets[0].get();
+  }
   for (auto& up : E->sets) {
     CtxSet* cs = up.get();
     if (cs->inflight.load(std::memory_order_relaxed) != 0) continue;
@@ -373,8 +379,14 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
   std::vector<std::shared_ptr<vsd::DevFilter>> fkeep;  // likewise
   // a context set (one search context per device): an idle one if any, so
   // concurrent host searches run on separate streams of every device
+  // heavy: a batched search whose shards are large (the per-shard test of
+  // vsd::heavy_search on a shard's share of the rows)
+  vsd::Collection probe;
+  probe.dim = sc->dim;
+  probe.dtype = sc->dtype;
+  probe.rows = sc->rows / std::max<uint32_t>(1, E->shards());
   AllWork aw;
-  CtxSet& cx = *pick_set(E, &aw);
+  CtxSet& cx = *pick_set(E, &aw, vsd::heavy_search(probe, nq));
   cx.inflight.fetch_add(1, std::memory_order_relaxed);
   struct Leave {
     CtxSet& cx;

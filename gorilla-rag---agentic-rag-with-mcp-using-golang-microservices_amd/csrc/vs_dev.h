@@ -190,9 +190,11 @@ int open(int device, uint32_t flags, DevEngine** out);
 void close(DevEngine* eng);  // the primary: closes every context of the device
 // A filter of the device's store (nullptr: none); the reference keeps it alive.
 std::shared_ptr<DevFilter> find_filter(DevEngine* eng, uint64_t filter_id);
-// The context a host search should use: an idle one if any (locked on
-// return: `lk` owns its work_mu), else the least busy one (waited for).
-DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk);
+// The context a host search should use (locked on return: `lk` owns its
+// work_mu): the primary for a heavy search (vs_engine.cpp heavy_search),
+// else an idle one if any, else the least busy one (waited for).
+DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk, bool heavy = false);
+bool heavy_search(const Collection& c, uint32_t nq);
 std::shared_ptr<Collection> find_coll(DevEngine* eng, const char* name);
 hipError_t set_dev(DevEngine* eng);
 hipError_t use_stream(DevEngine* eng, hipStream_t s);

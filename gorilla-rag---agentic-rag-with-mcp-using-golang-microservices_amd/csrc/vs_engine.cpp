@@ -58,8 +58,12 @@ std::shared_ptr<DevFilter> find_filter(DevEngine* eng, uint64_t filter_id) {
   return it == st.filters.end() ? nullptr : it->second;
 }
 
-DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk) {
+DevEngine* pick_context(DevEngine* eng, std::unique_lock<std::mutex>* lk, bool heavy) {
   const std::vector<DevEngine*>& cx = eng->store->ctx;
+  if (heavy) {  // batched scans of large collections queue on the primary's stream
+    *lk = std::unique_lock<std::mutex>(cx[0]->work_mu);
+    return cx[0];
+  }
   // an idle context first (no host search in flight on it), then any free lock
   for (int pass = 0; pass < 2; ++pass)
     for (DevEngine* c : cx) {
@@ -135,6 +139,8 @@ constexpr uint64_t kGatherDensityDen = 8;
 // Per-query launch overhead of a gathered scan (scan + merge launches,
 // ~10 us) in bytes of HBM streaming, for the batch decision in search_core.
 constexpr uint64_t kGatherCallBytes = 64ull << 20;
+// Collection bytes from which a batched host search is "heavy" (heavy_search).
+constexpr uint64_t kHeavyBytes = 256ull << 20;
 // Smallest batch of an fp32 collection that takes the MFMA pass.
 constexpr uint32_t kF32MfmaMinQueries = 4;
 
@@ -306,6 +312,22 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
 // select of the k-th key on the device, compaction of the k keys, rocPRIM
 // sort (vs_select.hip). keff = min(k, unmasked rows) keys per query; the
 // rest of each [k] row of d_keys is 0. Exact, no host round trip.
+// Smallest k of the large-k path for a streamed scan (VS_LARGE_K_FROM
+// overrides, read once; never above kMaxK + 1, the list scans' limit). The
+// GEMV list path keeps k <= 128 in 1-2 registers per lane; past that (16 per
+// lane) its inserts cost more than the select: at 10M x 768 bf16 one query
+// took 3.30 / 4.15 / 8.12 ms at k = 129 / 256 / 1024 on the list path
+// against 2.63-2.66 ms for any k on the large-k path (2.34-2.49 ms for the
+// list path at k <= 128; profiles/r03_large_k_threshold.jsonl).
+uint32_t large_k_from() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("VS_LARGE_K_FROM");
+    const long x = e ? std::atol(e) : (long)vsk::kMfmaMaxK + 1;
+    return (uint32_t)std::min<long>(std::max<long>(x, 1), (long)vsk::kMaxK + 1);
+  }();
+  return v;
+}
+
 int search_large_k(DevEngine* eng, Collection& c, const float* qp, uint32_t nq, uint32_t k,
                    uint64_t* d_keys, const uint64_t* allow, uint64_t avail) {
   const uint32_t n_rows = (uint32_t)c.rows;
@@ -526,7 +548,9 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                                 eng->stream),
          "query preprocess");
   if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
-  if (k > vsk::kMaxK)  // a filter rides along as the bitmap, selective or not
+  // k past the list scans, or past the list path's break-even on a streamed
+  // scan (a selective filter's gather reads only its rows: lists up to 1024)
+  if (k > vsk::kMaxK || (k >= large_k_from() && !gather))
     return search_large_k(eng, c, qp, nq, k, d_keys, allow, allow ? allowed : c.rows);
   if (gather) {
     if (allowed == 0) {
@@ -983,6 +1007,16 @@ hipError_t wait_event(hipEvent_t ev) {
   return hipEventSynchronize(ev);
 }
 
+// A batched search of a large collection (the MFMA passes fill every CU for
+// milliseconds): such calls queue behind each other on the primary context,
+// so two of them never split the device and the batcher's pipelining (the
+// next batch formed as the running one ends) keeps its batches whole. C5,
+// 3 x 5M x 1024: two batched calls on two streams cut the mean batch at 64
+// clients from 21 to 16 and QPS by 20% (profiles/r03_c5_contexts_*.jsonl).
+bool heavy_search(const Collection& c, uint32_t nq) {
+  return nq >= 2 && c.rows * c.row_bytes() >= kHeavyBytes;
+}
+
 int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t nq,
                 uint32_t dim, uint32_t k, const uint64_t* allow, uint64_t allow_words,
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count,
@@ -1015,7 +1049,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   // a search context of the device: an idle one if any, so concurrent host
   // searches run on separate streams (and overlap on the device)
   std::unique_lock<std::mutex> g;
-  DevEngine* cx = pick_context(eng, &g);
+  DevEngine* cx = pick_context(eng, &g, heavy_search(*c, nq));
   cx->inflight.fetch_add(1, std::memory_order_relaxed);
   struct Leave {
     DevEngine* cx;

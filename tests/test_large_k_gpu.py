@@ -1,5 +1,6 @@
-"""Searches with k > 1024 (the large-k path: score pass + device radix select
-+ sort, vs_select.hip), checked against the oracle on the device.
+"""Searches with k > 128 (the large-k path from k = 129: score pass + device
+radix select + sort, vs_select.hip; k > 1024 has no other path), checked
+against the oracle on the device.
 
 The reference passes `Limit: uint64(req.TopK)` straight to Qdrant
 (rag/vector-service/main.go:249-254), which serves any limit and returns
@@ -10,7 +11,7 @@ list limit, k far past it, k above the row count, single queries and
 batches, exact ties at the threshold (the row-word digits of the select),
 filters (dense, selective, resident, fewer allowed rows than k), a row_base,
 a sharded engine, vs_merge_keys at large k, the /search handler at 20k and
-1M rows, and the first 1024 of a large-k answer equal to the k = 1024 list
+1M rows, and the first 128 of a large-k answer equal to the k = 128 list
 path's answer bit for bit (the same per-row arithmetic).
 """
 import json
@@ -43,7 +44,7 @@ def lk_corpora(engine, orc):
     return out
 
 
-@pytest.mark.parametrize("k", [1025, 2000, 5000, 20000, 25000])
+@pytest.mark.parametrize("k", [129, 700, 1025, 2000, 5000, 20000, 25000])
 @pytest.mark.parametrize("dtype,metric", [(0, 0), (1, 0), (1, 1), (0, 1)])
 def test_large_k_single_and_batched(engine, orc, lk_corpora, dtype, metric, k):
     name, X = lk_corpora[(dtype, metric)]
@@ -59,14 +60,18 @@ def test_large_k_single_and_batched(engine, orc, lk_corpora, dtype, metric, k):
 
 @pytest.mark.parametrize("dtype", [0, 1])
 def test_large_k_prefix_equals_list_path(engine, orc, lk_corpora, dtype):
-    """The first 1024 keys of a k = 3000 answer are the k = 1024 answer, bit for bit."""
+    """The first 128 keys of a large-k answer (k = 129: the large-k path from
+    there, vs_engine.cpp large_k_from; and k = 3000) are the k = 128 list
+    path's answer, bit for bit: the score pass forms every row's sum as the
+    list scan does."""
     name, _ = lk_corpora[(dtype, 0)]
     Q = orc.generate(orc.SEED_QUERY, 90, 2, 768)
     for i in range(2):
-        s1, r1, _ = engine.search(name, Q[i], 1024)
-        s3, r3, _ = engine.search(name, Q[i], 3000)
-        assert np.array_equal(r3[:, :1024], r1)
-        assert np.array_equal(s3[:, :1024].view(np.uint32), s1.view(np.uint32))
+        s1, r1, _ = engine.search(name, Q[i], 128)
+        for kk in (129, 3000):
+            s3, r3, _ = engine.search(name, Q[i], kk)
+            assert np.array_equal(r3[:, :128], r1)
+            assert np.array_equal(s3[:, :128].view(np.uint32), s1.view(np.uint32))
 
 
 @pytest.mark.parametrize("dim,dtype", [(128, 0), (1536, 1), (100, 1), (100, 0)])
