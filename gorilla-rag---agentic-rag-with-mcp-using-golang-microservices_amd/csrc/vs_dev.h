@@ -171,6 +171,9 @@ struct DevEngine {
   // zeroed between uses), select state, the selected keys, sort scratch;
   // large merges (vs_merge_keys / shard merges at k > kMaxK)
   DevBuf lk_sc, lk_hist, lk_state, lk_sel, lk_sort, merge_big;
+  // small-collection search spread over workgroups: their keys + the
+  // completion counter (zeroed at allocation; each launch leaves it zero)
+  DevBuf small_part;
   std::vector<uint64_t> h_keys;
   std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing

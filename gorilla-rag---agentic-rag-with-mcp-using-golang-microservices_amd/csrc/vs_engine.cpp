@@ -493,9 +493,16 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   // one query over a small collection (config C1): prep, scan and merge in
   // one launch (the same keys as the three launches below, bit for bit)
   if (nq == 1 && !allow && vsk::gemv_small_ok(dim, (uint32_t)c.rows, k)) {
+    constexpr size_t kPartBytes = (size_t)vsk::kGemvSmallMaxParts * vsk::kGemvSmallMaxK * 8;
+    if (eng->small_part.bytes < kPartBytes + 64) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->small_part.ensure(kPartBytes + 64), "alloc small-scan parts");
+      VS_HIP(hipMemsetAsync(eng->small_part.p, 0, eng->small_part.bytes, eng->stream), "zero");
+    }
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_gemv_small(c.data, bf16, dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q,
-                                  cosine, k, d_keys, eng->stream),
+                                  cosine, k, d_keys, eng->stream, eng->small_part.as<uint64_t>(),
+                                  (uint32_t*)((char*)eng->small_part.p + kPartBytes)),
            "small scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     return VS_OK;

@@ -549,6 +549,18 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   L.init();
   uint64_t theta = 0;
   const char* X = (const char*)Xv;
+  // score mode: lane i of (obuf, rbuf) holds the i-th buffered row's image
+  // and row number; nbuf rows are buffered (wave-uniform)
+  uint32_t obuf = 0, rbuf = 0;
+  int nbuf = 0;
+  auto flush_scores = [&]() {
+    if (lane < nbuf) {
+      ((uint32_t*)out)[rbuf] = obuf;
+      if (obuf) atomicAdd(&lhist[obuf >> (32 - kRselBits0)], 1u);
+    }
+    nbuf = 0;
+  };
+  (void)flush_scores;
 
   if (lo < hi) {
     constexpr bool kNT = (VAR & 1) != 0, kDpp = (VAR & 2) != 0;
@@ -610,11 +622,14 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
         const float s = kDpp ? wave_sum_dpp(p[b]) : wave_sum(p[b]);
         const uint32_t row = r + b;
         if constexpr (kScores) {
-          // lane b stores row r + b (every lane holds every sum)
-          if (row < hi && lane == b) {
+          // every lane holds every sum: the wave-uniform image goes into lane
+          // `nbuf` of a 64-row buffer, written out (one store and one LDS
+          // histogram add per 64 rows) when full
+          if (row < hi) {
             const uint32_t o = row_allowed(allow, row) ? (uint32_t)(make_key(s, 0) >> 32) : 0u;
-            ((uint32_t*)out)[row] = o;
-            if (o) atomicAdd(&lhist[o >> (32 - kRselBits0)], 1u);
+            obuf = lane == nbuf ? o : obuf;
+            rbuf = lane == nbuf ? row : rbuf;
+            ++nbuf;
           }
         } else if (row < hi && (GATHER || row_allowed(allow, row))) {
           const uint64_t key = make_key(s, row_base + (GATHER ? rows[row] : row));
@@ -624,6 +639,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
           }
         }
       }
+      if constexpr (kScores) {
+        if (nbuf > 64 - S::RB) flush_scores();
+      }
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
@@ -631,6 +649,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     }
   }
   if constexpr (kScores) {
+    flush_scores();
     __syncthreads();
     for (int i = threadIdx.x; i < kRselBins; i += kGemvThreads)
       if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
@@ -863,8 +882,13 @@ static hipError_t gemv_scores_d(const void* X, uint32_t n_rows, const float* q,
                                 hipStream_t st) {
   using S = GemvShape<D, BF16>;
   const GemvGrid g = gemv_grid(n_rows, S::RB);
-  hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 0, false>), dim3(g.nwg), dim3(kGemvThreads), 0, st,
-                     X, n_rows, 0u, q, allow, 0u, g.rows_per_wave, (uint64_t*)sc, nullptr, hist);
+  // contiguous row slices per wave (no step interleave): a wave's 64
+  // buffered images are 64 consecutive rows, one coalesced 256-B store (the
+  // interleaved order scattered them over 32 lines shared with other waves:
+  // 2.62 ms against 2.29 for the list scan at 10M x 768 bf16)
+  hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 0, false, (kGemvVar & ~8)>), dim3(g.nwg),
+                     dim3(kGemvThreads), 0, st, X, n_rows, 0u, q, allow, 0u, g.rows_per_wave,
+                     (uint64_t*)sc, nullptr, hist);
   return hipGetLastError();
 }
 
@@ -918,14 +942,54 @@ hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n
 // chunk layout, the same accumulation and the same xor tree), so its scores
 // are the same bits. Wave 0 first preprocesses the raw query into LDS as
 // query_prep_kernel does (prep bit 0: cosine, bit 1: round to bf16 values).
+//
+// Several workgroups (r03): one workgroup reads the whole collection through
+// one CU (221 rows x 3 KB at C1: the CU's bandwidth and the row steps were
+// most of the 12.7 us), so the rows are spread over gridDim.x workgroups,
+// each preparing the query itself. Each writes its k keys to part[wg][k]
+// with agent-scope (sc1) stores, waits for them (vmcnt), and adds 1 to
+// *counter (agent-scope atomic); the workgroup whose add returns
+// gridDim.x - 1 reads every part with sc1 loads after a workgroup barrier
+// and writes the merged top k, then resets the counter (MI355X_MICROARCH.md
+// cross-CU hand-off, first row: one signaling lane per storing workgroup,
+// the last adder consumes). One launch of one workgroup when gridDim.x == 1.
 template <int D, bool BF16, int U>
 __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, const float* __restrict__ q,
-    uint32_t k, int prep, uint64_t* __restrict__ out) {
+    uint32_t k, int prep, uint64_t* __restrict__ out, uint64_t* __restrict__ part,
+    uint32_t* __restrict__ counter) {
   using S = GemvShape<D, BF16>;
   static_assert(D % 64 == 0 && D <= 64 * kQPrepMax, "query_prep_kernel's shapes only");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the first row step's loads go out before the query prep (they do not
+  // depend on it), so their HBM latency hides under wave 0's fp64 prep
+  int rowsel[S::J];
+  int coff[S::J];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) {
+    const int c = lane + 64 * j;
+    rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
+    coff[j] = c % S::CPR;
+  }
+  const char* X = (const char*)Xv;
+  const uint32_t n_groups = (n_rows + S::RB - 1) / S::RB;
+  const uint32_t nw = gridDim.x * kGemvWaves;  // waves of the launch
+  const uint32_t gfirst = blockIdx.x * kGemvWaves + (uint32_t)w;
+  uint4 buf[U][S::J];
+  auto load_step = [&](uint32_t g0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) {
+        // rows past the end read the last row again (never keyed)
+        uint32_t row = (g0 + (uint32_t)u * nw) * S::RB + rowsel[j];
+        row = row < n_rows ? row : n_rows - 1;
+        buf[u][j] = *(const uint4*)(X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16);
+      }
+    }
+  };
+  if (gfirst < n_groups) load_step(gfirst);
   __shared__ float qs[D];
   if (w == 0) {
     constexpr int PJ = D / 64;
@@ -952,34 +1016,16 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
     }
   }
   __syncthreads();
-  int rowsel[S::J];
-  int coff[S::J];
   float qv[S::J][S::EPC];
 #pragma unroll
-  for (int j = 0; j < S::J; ++j) {
-    const int c = lane + 64 * j;
-    rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
-    coff[j] = c % S::CPR;
+  for (int j = 0; j < S::J; ++j)
 #pragma unroll
     for (int e = 0; e < S::EPC; ++e) qv[j][e] = qs[coff[j] * S::EPC + e];
-  }
   WaveList<1> L;
   L.init();
   uint64_t theta = 0;
-  const char* X = (const char*)Xv;
-  const uint32_t n_groups = (n_rows + S::RB - 1) / S::RB;
-  for (uint32_t g0 = (uint32_t)w; g0 < n_groups; g0 += kGemvWaves * U) {
-    uint4 buf[U][S::J];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int j = 0; j < S::J; ++j) {
-        // rows past the end read the last row again (never keyed)
-        uint32_t row = (g0 + (uint32_t)(u * kGemvWaves)) * S::RB + rowsel[j];
-        row = row < n_rows ? row : n_rows - 1;
-        buf[u][j] = *(const uint4*)(X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16);
-      }
-    }
+  for (uint32_t g0 = gfirst; g0 < n_groups; g0 += nw * U) {
+    if (g0 != gfirst) load_step(g0);
     float sc[U][S::RB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1003,7 +1049,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) {
-        const uint32_t row = (g0 + (uint32_t)(u * kGemvWaves)) * S::RB + b;
+        const uint32_t row = (g0 + (uint32_t)u * nw) * S::RB + b;
         if (row < n_rows) {
           const uint64_t key = make_key(sc[u][b], row_base + row);
           if (key > theta) {
@@ -1020,8 +1066,10 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
   // unique: distinct rows), so every lane places its own keys at once. The
   // output is the same sorted top k, zero-filled past the nonzero keys.
   __shared__ uint64_t sm[kGemvWaves][64];
+  __shared__ int last_wg;
   sm[w][lane] = L.e[0];
   __syncthreads();
+  const bool multi = gridDim.x > 1;
   if (w == 0) {
     const uint32_t tot = kGemvWaves * k;  // <= 128
     const uint32_t c0 = (uint32_t)lane, c1 = (uint32_t)lane + 64;
@@ -1035,22 +1083,86 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
         r1 += y > x1 ? 1u : 0u;
         nz += y != 0 ? 1u : 0u;
       }
-    if (x0 && r0 < k) out[r0] = x0;
-    if (x1 && r1 < k) out[r1] = x1;
-    if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
+    if (!multi) {
+      if (x0 && r0 < k) out[r0] = x0;
+      if (x1 && r1 < k) out[r1] = x1;
+      if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
+    } else {
+      // this workgroup's k keys (0-padded) -> part, agent-scope stores
+      uint64_t* dst = part + (size_t)blockIdx.x * k;
+      if (x0 && r0 < k) __hip_atomic_store(dst + r0, x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (x1 && r1 < k) __hip_atomic_store(dst + r1, x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)lane >= nz && (uint32_t)lane < k)
+        __hip_atomic_store(dst + lane, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores landed before the add
+      int l = 0;
+      if (lane == 0)
+        l = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            gridDim.x - 1;
+      l = __shfl(l, 0, 64);
+      if (lane == 0) last_wg = l;
+    }
   }
+  if (!multi) return;
+  __syncthreads();  // last_wg published; the adding wave's add has returned
+  if (!last_wg) return;
+  // the last workgroup: every part (sc1 loads, after the barrier above), ranked
+  __shared__ uint64_t pk[kGemvSmallMaxParts * kGemvSmallMaxK];
+  const uint32_t tot = gridDim.x * k;
+  for (uint32_t i = threadIdx.x; i < tot; i += kGemvThreads)
+    pk[i] = __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (w == 0) {
+    uint32_t nz = 0;
+    uint32_t r[kGemvSmallMaxParts * kGemvSmallMaxK / 64];
+    uint64_t x[kGemvSmallMaxParts * kGemvSmallMaxK / 64];
+#pragma unroll
+    for (int i = 0; i < kGemvSmallMaxParts * kGemvSmallMaxK / 64; ++i) {
+      const uint32_t c = (uint32_t)lane + 64u * i;
+      x[i] = c < tot ? pk[c] : 0;
+      r[i] = 0;
+    }
+    for (uint32_t j = 0; j < tot; ++j) {
+      const uint64_t y = pk[j];  // uniform LDS broadcast
+      nz += y != 0 ? 1u : 0u;
+#pragma unroll
+      for (int i = 0; i < kGemvSmallMaxParts * kGemvSmallMaxK / 64; ++i) r[i] += y > x[i] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kGemvSmallMaxParts * kGemvSmallMaxK / 64; ++i)
+      if (x[i] && r[i] < k) out[r[i]] = x[i];
+    if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
+    if (lane == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+uint32_t gemv_small_parts(uint32_t dim, bool bf16, uint32_t n_rows) {
+  // one row-group step per wave: 8 waves x U groups x RB rows per workgroup
+  const uint32_t epc = bf16 ? 8 : 4, cpr = dim / epc;
+  uint32_t g = 64, c = cpr;  // RB = 64 / gcd(CPR, 64)
+  while (c) {
+    const uint32_t t = g % c;
+    g = c;
+    c = t;
+  }
+  const uint32_t rb = 64 / g, j = rb * cpr / 64;
+  const uint32_t u = j <= 3 ? 4 : (12 / j > 0 ? 12 / j : 1);
+  const uint32_t per_wg = (uint32_t)kGemvWaves * u * rb;
+  const uint32_t w = (n_rows + per_wg - 1) / per_wg;
+  return std::min<uint32_t>(std::max<uint32_t>(w, 1), kGemvSmallMaxParts);
 }
 
 template <int D, bool BF16>
 static void gemv_small_launch(const void* X, uint32_t n_rows, uint32_t row_base,
                               const float* q_raw, int prep, uint32_t k, uint64_t* out,
-                              hipStream_t st) {
+                              uint64_t* part, uint32_t* counter, hipStream_t st) {
   // row groups per step: 4 (8 with the next step's loads issued ahead was
   // slower: 14.9 us against 12.6 at 221 rows), fewer past 3 chunks per lane
   constexpr int J = GemvShape<D, BF16>::J;
   constexpr int U = J <= 3 ? 4 : (12 / J > 0 ? 12 / J : 1);
-  hipLaunchKernelGGL((gemv_small_kernel<D, BF16, U>), dim3(1), dim3(kGemvThreads), 0, st, X,
-                     n_rows, row_base, q_raw, k, prep, out);
+  const uint32_t nwg = part ? gemv_small_parts(D, BF16, n_rows) : 1;
+  hipLaunchKernelGGL((gemv_small_kernel<D, BF16, U>), dim3(nwg), dim3(kGemvThreads), 0, st, X,
+                     n_rows, row_base, q_raw, k, prep, out, part, counter);
 }
 
 bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
@@ -1063,15 +1175,18 @@ bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
 
 hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
-                             uint64_t* out, hipStream_t st) {
+                             uint64_t* out, hipStream_t st, uint64_t* part, uint32_t* counter) {
   if (!gemv_small_ok(dim, n_rows, k)) return hipErrorInvalidValue;
+  if (!counter) part = nullptr;
   const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
 #define VS_SMALL_CASE(DD)                                                                   \
   case DD:                                                                                  \
     if (bf16)                                                                               \
-      gemv_small_launch<DD, true>(X, n_rows, row_base, q_raw, prep, k, out, st);            \
+      gemv_small_launch<DD, true>(X, n_rows, row_base, q_raw, prep, k, out, part, counter,  \
+                                  st);                                                      \
     else                                                                                    \
-      gemv_small_launch<DD, false>(X, n_rows, row_base, q_raw, prep, k, out, st);           \
+      gemv_small_launch<DD, false>(X, n_rows, row_base, q_raw, prep, k, out, part, counter, \
+                                   st);                                                     \
     break;
   switch (dim) {
     VS_SMALL_CASE(128)
