@@ -1149,7 +1149,13 @@ uint32_t gemv_small_parts(uint32_t dim, bool bf16, uint32_t n_rows) {
   const uint32_t u = j <= 3 ? 4 : (12 / j > 0 ? 12 / j : 1);
   const uint32_t per_wg = (uint32_t)kGemvWaves * u * rb;
   const uint32_t w = (n_rows + per_wg - 1) / per_wg;
-  return std::min<uint32_t>(std::max<uint32_t>(w, 1), kGemvSmallMaxParts);
+  // VS_SMALL_PARTS caps the workgroups (read once; ablation)
+  static const uint32_t cap = [] {
+    const char* e = getenv("VS_SMALL_PARTS");
+    const int x = e ? atoi(e) : (int)kGemvSmallMaxParts;
+    return (uint32_t)std::min(std::max(x, 1), (int)kGemvSmallMaxParts);
+  }();
+  return std::min<uint32_t>(std::max<uint32_t>(w, 1), cap);
 }
 
 template <int D, bool BF16>
@@ -1620,6 +1626,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // prefetch survives scheduling (3.38 vs 3.63 ms at 10M rows); the sorted-list
   // pass would spill with it
   constexpr bool kPin = (VAR & 128) != 0 || MODE != 8;
+  // VAR 4194304 (ablation, r03): instead of pinning a step's fragment reads
+  // ahead of its MFMAs, ask the scheduler to interleave them: after every G
+  // MFMAs one ds_read_b128 of a later step (sched_group_barrier), so the LDS
+  // reads issue in the MFMA gaps rather than in one burst
+  constexpr bool kIlvSched = (VAR & 4194304) != 0;
   // VAR 8192 (ablation): per-workgroup start / end wall clock into a.lists
   constexpr bool kClock = (VAR & 8192) != 0;
   uint64_t tclk0 = 0;
@@ -1884,7 +1895,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
               afr[(sig + kPD) % NB][hr] =
                   sp < S::CT ? lds_a(sb, sp, hr) : lds_a(sbn, sp - S::CT, hr);
           }
-          if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+          if constexpr (kPin && !kIlvSched) __builtin_amdgcn_sched_barrier(0);
           if constexpr (F32) {
             // lane (col, kq) holds k = 16 step + 4 kq + j in element j of both
             // fragments: MFMA j sums those k over the four lane quarters
@@ -1913,6 +1924,13 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
                 acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][qs], acc[hr][g], 0,
                                                                      0, 0);
               }
+            }
+          }
+          if constexpr (kIlvSched) {
+#pragma unroll
+            for (int hr = 0; hr < 2; ++hr) {
+              __builtin_amdgcn_sched_group_barrier(0x008, G, 0);  // G MFMAs
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
             }
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);

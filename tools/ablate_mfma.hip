@@ -166,6 +166,18 @@ int main(int argc, char** argv) {
             {"no-epi G4 pd1", run<1, 2048 + 256, 4>, false, {}},
             {"no-epi G4 pd3 pin", run<1, 2048 + 256 + 64 + 128, 4>, false, {}},
             {"no-epi G4 pd2 pin", run<1, 2048 + 256 + 32 + 128, 4>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "g4i")) {
+    // r03: the one-wave-per-SIMD 64-query layout with the step's fragment
+    // reads interleaved into its MFMAs by sched_group_barrier (VAR 4194304),
+    // against the product and the product interleaved the same way
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
+            {"main ilv", run<0, 2048 + 256 + 4194304, 2>, true, {}},
+            {"main G4 ilv", run<0, 2048 + 256 + 4194304, 4>, true, {}},
+            {"no-epi (product)", run<1, 2048 + 256, 2>, false, {}},
+            {"no-epi ilv", run<1, 2048 + 256 + 4194304, 2>, false, {}},
+            {"no-epi G4 pd1", run<1, 2048 + 256, 4>, false, {}},
+            {"no-epi G4 ilv", run<1, 2048 + 256 + 4194304, 4>, false, {}},
+            {"no-epi G4 pd2 ilv", run<1, 2048 + 256 + 32 + 4194304, 4>, false, {}}};
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "product")) {
     // the product main pass alone (sample-tile sweeps: argv[3])
     arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}}};
