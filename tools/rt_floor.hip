@@ -9,6 +9,11 @@
 //   full_sync  the same, hipStreamSynchronize instead of the polled event
 //   out_map  h2d + kernel writing its 40 B to mapped pinned memory + event
 //   in_map   kernel reading its 3 KiB from mapped pinned memory + d2h + event
+//   graph    full's three operations captured once into a hipGraph, one
+//            graph launch + event + wait per call (r03)
+//   flag_map h2d + a kernel that writes its keys and then a sequence word to
+//            mapped pinned memory (system-scope fence between); the host
+//            spins on the word, no event (r03)
 //   vs_search  the engine's host API on config C1 (221 x 768 fp32 cosine,
 //            one query, k = 5): everything above plus the engine's own work
 //
@@ -49,6 +54,23 @@ __global__ void touch(const float* __restrict__ in, uint64_t* __restrict__ out, 
   }
 }
 
+// keys to mapped host memory, then (after a system-scope fence) the call's
+// sequence number: a host that sees the number sees the keys
+__global__ void touch_flag(const float* __restrict__ in, uint64_t* out, int n, uint64_t seq) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += in[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 256; ++i) t += red[i];
+    for (int i = 0; i < 5; ++i) out[i] = (uint64_t)__float_as_uint(t) + (uint64_t)i;
+    __threadfence_system();
+    __hip_atomic_store(out + 7, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 static void wait_polled(hipEvent_t ev) {
   while (hipEventQuery(ev) == hipErrorNotReady) {
   }
@@ -78,38 +100,57 @@ int main() {
   struct Case {
     const char* name;
     std::function<void()> body;
-    bool sync;
+    int sync;  // 0: event + polled wait, 1: hipStreamSynchronize, 2: the body waits
   };
+  hipGraph_t graph;
+  hipGraphExec_t gexec;
+  CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
+  hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n);
+  (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
+  CK(hipStreamEndCapture(st, &graph));
+  CK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+  uint64_t seq = 0;
   std::vector<Case> cases = {
-      {"launch", [&] { hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n); }, false},
-      {"h2d", [&] { (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st); }, false},
-      {"d2h", [&] { (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st); }, false},
+      {"launch", [&] { hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n); }, 0},
+      {"h2d", [&] { (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st); }, 0},
+      {"d2h", [&] { (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st); }, 0},
       {"full",
        [&] {
          (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
          hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n);
          (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
        },
-       false},
+       0},
       {"full_sync",
        [&] {
          (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
          hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, d_out, n);
          (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
        },
-       true},
+       1},
       {"out_map",
        [&] {
          (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
          hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, d_in, m_out, n);
        },
-       false},
+       0},
       {"in_map",
        [&] {
          hipLaunchKernelGGL(touch, dim3(1), dim3(256), 0, st, m_in, d_out, n);
          (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
        },
-       false},
+       0},
+      {"graph", [&] { (void)hipGraphLaunch(gexec, st); }, 0},
+      {"flag_map",
+       [&] {
+         ++seq;
+         (void)hipMemcpyAsync(d_in, h_in, n * 4, hipMemcpyHostToDevice, st);
+         hipLaunchKernelGGL(touch_flag, dim3(1), dim3(256), 0, st, d_in, m_out, n, seq);
+         while (__atomic_load_n((volatile uint64_t*)(m_out + 7), __ATOMIC_ACQUIRE) != seq) {
+         }
+       },
+       2},
   };
   std::printf("{\"tool\": \"rt_floor\", \"p50_us\": {");
   bool first = true;
@@ -119,9 +160,9 @@ int main() {
     for (int i = 0; i < iters + 500; ++i) {
       const auto t0 = std::chrono::steady_clock::now();
       c.body();
-      if (c.sync) {
+      if (c.sync == 1) {
         CK(hipStreamSynchronize(st));
-      } else {
+      } else if (c.sync == 0) {
         CK(hipEventRecord(ev, st));
         wait_polled(ev);
       }
