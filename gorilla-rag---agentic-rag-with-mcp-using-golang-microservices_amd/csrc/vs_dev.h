@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -92,6 +93,11 @@ struct HostSlot {
   size_t in_bytes = 0, out_bytes = 0;
   hipEvent_t done = nullptr;
   bool busy = false;  // between its enqueue and the end of its decode
+  // small-path completion (r03): kGemvSmallMaxK keys + the sequence word, in
+  // coherent mapped pinned memory the kernel writes directly (HostDirect)
+  uint64_t* mapped = nullptr;
+  uint64_t* mapped_dev = nullptr;  // the same memory as the device sees it
+  uint64_t seq = 0;
   HostSlot() = default;
   HostSlot(const HostSlot&) = delete;
   HostSlot& operator=(const HostSlot&) = delete;
@@ -99,6 +105,23 @@ struct HostSlot {
     if (in) (void)hipHostFree(in);
     if (out) (void)hipHostFree(out);
     if (done) (void)hipEventDestroy(done);
+    if (mapped) (void)hipHostFree(mapped);
+  }
+  hipError_t ensure_mapped(size_t words) {
+    if (mapped) return hipSuccess;
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, words * 8, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return e;
+    std::memset(p, 0, words * 8);
+    void* d = nullptr;
+    const hipError_t e2 = hipHostGetDevicePointer(&d, p, 0);
+    if (e2 != hipSuccess) {
+      (void)hipHostFree(p);
+      return e2;
+    }
+    mapped = (uint64_t*)p;
+    mapped_dev = (uint64_t*)d;
+    return hipSuccess;
   }
   // grows the pinned buffers (the slot is idle: nothing in flight uses them)
   hipError_t ensure(size_t in_b, size_t out_b) {
@@ -252,8 +275,17 @@ hipError_t wait_event(hipEvent_t ev);
 // eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and
 // the collection's reader lock held by the caller. Asynchronous: nothing
 // waits on the device unless a scratch buffer has to grow.
+// With `direct`, a search that takes the one-launch small path writes its
+// keys to direct->keys (mapped pinned host memory) and then direct->seq to
+// *direct->flag, and sets direct->used; d_keys is then not written.
+struct HostDirect {
+  uint64_t* keys = nullptr;  // device views of the mapped buffer
+  uint64_t* flag = nullptr;
+  uint64_t seq = 0;
+  bool used = false;
+};
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
-                const uint32_t* allow_list = nullptr);
+                const uint32_t* allow_list = nullptr, HostDirect* direct = nullptr);
 
 }  // namespace vsd

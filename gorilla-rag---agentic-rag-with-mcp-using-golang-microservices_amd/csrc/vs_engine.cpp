@@ -480,7 +480,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 // reader lock are held by the caller.
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow, uint64_t allowed,
-                const uint32_t* allow_list) {
+                const uint32_t* allow_list, HostDirect* direct) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const bool cosine = c.metric == VS_METRIC_COSINE;
@@ -501,10 +501,13 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     }
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_gemv_small(c.data, bf16, dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q,
-                                  cosine, k, d_keys, eng->stream, eng->small_part.as<uint64_t>(),
-                                  (uint32_t*)((char*)eng->small_part.p + kPartBytes)),
+                                  cosine, k, direct ? direct->keys : d_keys, eng->stream,
+                                  eng->small_part.as<uint64_t>(),
+                                  (uint32_t*)((char*)eng->small_part.p + kPartBytes),
+                                  direct ? direct->flag : nullptr, direct ? direct->seq : 0),
            "small scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    if (direct) direct->used = true;
     return VS_OK;
   }
 
@@ -1014,6 +1017,29 @@ hipError_t wait_event(hipEvent_t ev) {
   return hipEventSynchronize(ev);
 }
 
+// Spins on a completion word in mapped host memory for up to spin_us(): true
+// once it holds seq.
+bool wait_word(const uint64_t* w, uint64_t seq) {
+  const int64_t lim = spin_us();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return true;
+    if ((i & 63) == 63 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(lim))
+      return false;
+  }
+}
+
+// The small path's host completion word (on unless VS_DIRECT_COMPLETION=0;
+// read once): the D2H copy + event it replaces cost ~6 us of C1's round trip.
+bool direct_completion() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_DIRECT_COMPLETION");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // A batched search of a large collection (the MFMA passes fill every CU for
 // milliseconds): such calls queue behind each other on the primary context,
 // so two of them never split the device and the batcher's pipelining (the
@@ -1101,6 +1127,18 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     e = hipMemcpyAsync(cx->allow.p, allow, abytes, hipMemcpyHostToDevice, cx->stream);
     if (e != hipSuccess) return abandon(fail_hip(e, "filter bitmap H2D"));
   }
+  // a one-query call may take the one-launch small path, which then writes
+  // its keys and a completion word straight to the slot's mapped buffer
+  HostDirect hd;
+  HostDirect* hdp = nullptr;
+  if (nq == 1 && !abytes && !df && k <= vsk::kGemvSmallMaxK && direct_completion()) {
+    e = hs->ensure_mapped(vsk::kGemvSmallMaxK + 1);
+    if (e != hipSuccess) return abandon(fail_hip(e, "alloc mapped completion"));
+    hd.keys = hs->mapped_dev;
+    hd.flag = hs->mapped_dev + vsk::kGemvSmallMaxK;
+    hd.seq = ++hs->seq;
+    hdp = &hd;
+  }
   int rc;
   if (df)
     rc = search_core(cx, *c, cx->q_in.as<float>(), nq, k, cx->keys.as<uint64_t>(),
@@ -1109,16 +1147,30 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   else
     rc = search_core(cx, *c, cx->q_in.as<float>(), nq, k, cx->keys.as<uint64_t>(),
                      abytes ? cx->allow.as<uint64_t>() : nullptr,
-                     abytes ? popcount_rows(allow, c->rows) : 0);
+                     abytes ? popcount_rows(allow, c->rows) : 0, nullptr, hdp);
   if (rc != VS_OK) return abandon(rc);
-  e = hipMemcpyAsync(hs->out, cx->keys.p, kbytes, hipMemcpyDeviceToHost, cx->stream);
+  if (!hd.used) e = hipMemcpyAsync(hs->out, cx->keys.p, kbytes, hipMemcpyDeviceToHost, cx->stream);
   if (e == hipSuccess) e = hipEventRecord(hs->done, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "keys D2H"));
   // wait for the device outside work_mu: the next call on this context (its
   // q_in, keys and scratch are ordered on its stream) enqueues behind this one
   g.unlock();
-  const hipError_t we = wait_event(hs->done);
-  if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+  hipError_t we = hipSuccess;
+  if (hd.used) {
+    // the kernel's completion word: its keys are in place once it reads seq
+    // (the H2D that read hs->in ran before the kernel; nothing after the
+    // kernel touches the slot). Past the spin limit, the stream's event.
+    const uint64_t* word = hs->mapped + vsk::kGemvSmallMaxK;
+    if (!wait_word(word, hd.seq)) {
+      we = hipEventSynchronize(hs->done);
+      if (we == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != hd.seq)
+        we = hipErrorLaunchFailure;  // the stream completed without the word
+    }
+    if (we == hipSuccess) decode_host(hs->mapped, nq, k, out_scores, out_rows, out_count);
+  } else {
+    we = wait_event(hs->done);
+    if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+  }
   g.lock();
   hs->busy = false;
   VS_HIP(we, "search sync");

@@ -108,6 +108,9 @@ uint32_t compact_scratch_words(uint32_t n_rows);
 // u32, zero between launches; the kernel leaves it zero), the rows are spread
 // over gemv_small_parts() workgroups and the last one to finish merges; both
 // buffers belong to one stream (concurrent launches need their own).
+// With `flag`, `out` is mapped pinned host memory (k keys) and the kernel
+// stores `seq` to *flag (mapped host memory) after the keys are visible to
+// the host, which may then read them without waiting for the stream.
 constexpr uint32_t kGemvSmallMaxRows = 256;  // 32 rows per wave
 constexpr uint32_t kGemvSmallMaxK = 16;  // the workgroup merge is serial in k
 constexpr uint32_t kGemvSmallMaxParts = 16;
@@ -116,7 +119,8 @@ uint32_t gemv_small_parts(uint32_t dim, bool bf16, uint32_t n_rows);
 hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
                              uint64_t* out, hipStream_t st, uint64_t* part = nullptr,
-                             uint32_t* counter = nullptr);
+                             uint32_t* counter = nullptr, uint64_t* flag = nullptr,
+                             uint64_t seq = 0);
 
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);

@@ -927,6 +927,13 @@ hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n
 #undef VS_SCORES_CASE
 }
 
+// The wave's earlier stores (every lane's) reach host-visible memory before
+// lane 0 publishes `seq`: a host that reads the word then reads the keys.
+__device__ __forceinline__ void signal_host(uint64_t* flag, uint64_t seq, int lane) {
+  __threadfence_system();
+  if (lane == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Small collections, one query, k <= 16, no filter: query preprocessing,
 // scan and the workgroup merge in one launch of one workgroup, which writes
 // the final k keys (what query prep + gemv + merge produce, bit for bit: the
@@ -953,11 +960,17 @@ hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n
 // and writes the merged top k, then resets the counter (MI355X_MICROARCH.md
 // cross-CU hand-off, first row: one signaling lane per storing workgroup,
 // the last adder consumes). One launch of one workgroup when gridDim.x == 1.
+//
+// Host completion word (r03): with `flag`, `out` is mapped pinned host memory
+// and the writing wave, after its key stores, fences at system scope and
+// stores `seq` to *flag (host memory too); the host spins on that word instead
+// of a D2H copy and the stream's completion event, which cost ~6 us of a
+// ~18 us round trip (tools/rt_floor.hip, profiles/r03_rt_floor_graph_flag.json).
 template <int D, bool BF16, int U>
 __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, const float* __restrict__ q,
     uint32_t k, int prep, uint64_t* __restrict__ out, uint64_t* __restrict__ part,
-    uint32_t* __restrict__ counter) {
+    uint32_t* __restrict__ counter, uint64_t* flag, uint64_t seq) {
   using S = GemvShape<D, BF16>;
   static_assert(D % 64 == 0 && D <= 64 * kQPrepMax, "query_prep_kernel's shapes only");
   const int lane = threadIdx.x & 63;
@@ -1087,6 +1100,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
       if (x0 && r0 < k) out[r0] = x0;
       if (x1 && r1 < k) out[r1] = x1;
       if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
+      if (flag) signal_host(flag, seq, lane);
     } else {
       // this workgroup's k keys (0-padded) -> part, agent-scope stores
       uint64_t* dst = part + (size_t)blockIdx.x * k;
@@ -1133,6 +1147,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
       if (x[i] && r[i] < k) out[r[i]] = x[i];
     if ((uint32_t)lane >= nz && (uint32_t)lane < k) out[lane] = 0;
     if (lane == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (flag) signal_host(flag, seq, lane);
   }
 }
 
@@ -1161,14 +1176,15 @@ uint32_t gemv_small_parts(uint32_t dim, bool bf16, uint32_t n_rows) {
 template <int D, bool BF16>
 static void gemv_small_launch(const void* X, uint32_t n_rows, uint32_t row_base,
                               const float* q_raw, int prep, uint32_t k, uint64_t* out,
-                              uint64_t* part, uint32_t* counter, hipStream_t st) {
+                              uint64_t* part, uint32_t* counter, uint64_t* flag, uint64_t seq,
+                              hipStream_t st) {
   // row groups per step: 4 (8 with the next step's loads issued ahead was
   // slower: 14.9 us against 12.6 at 221 rows), fewer past 3 chunks per lane
   constexpr int J = GemvShape<D, BF16>::J;
   constexpr int U = J <= 3 ? 4 : (12 / J > 0 ? 12 / J : 1);
   const uint32_t nwg = part ? gemv_small_parts(D, BF16, n_rows) : 1;
   hipLaunchKernelGGL((gemv_small_kernel<D, BF16, U>), dim3(nwg), dim3(kGemvThreads), 0, st, X,
-                     n_rows, row_base, q_raw, k, prep, out, part, counter);
+                     n_rows, row_base, q_raw, k, prep, out, part, counter, flag, seq);
 }
 
 bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
@@ -1181,7 +1197,8 @@ bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
 
 hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
-                             uint64_t* out, hipStream_t st, uint64_t* part, uint32_t* counter) {
+                             uint64_t* out, hipStream_t st, uint64_t* part, uint32_t* counter,
+                             uint64_t* flag, uint64_t seq) {
   if (!gemv_small_ok(dim, n_rows, k)) return hipErrorInvalidValue;
   if (!counter) part = nullptr;
   const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
@@ -1189,10 +1206,10 @@ hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_
   case DD:                                                                                  \
     if (bf16)                                                                               \
       gemv_small_launch<DD, true>(X, n_rows, row_base, q_raw, prep, k, out, part, counter,  \
-                                  st);                                                      \
+                                  flag, seq, st);                                           \
     else                                                                                    \
       gemv_small_launch<DD, false>(X, n_rows, row_base, q_raw, prep, k, out, part, counter, \
-                                   st);                                                     \
+                                   flag, seq, st);                                          \
     break;
   switch (dim) {
     VS_SMALL_CASE(128)

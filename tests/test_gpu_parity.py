@@ -521,3 +521,84 @@ def test_small_collection_one_launch(pkg, orc, dim, dtype, metric):
                     bad = orc.check_topk(s, r, c, s64, rr, cc, orc.rescore(X, Qp, r, c, base), 1e-5)
                     assert not bad, (rows, k, bad[:3])
             eng.drop_collection(name)
+
+
+_SMALL_COMPLETION = r"""
+import json, sys
+import torch                      # first: the library then binds torch's HIP runtime
+import numpy as np
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge
+pkg = ge.load_package()
+rng = np.random.default_rng(11)
+V = rng.standard_normal((221, 768)).astype(np.float32)
+Q = rng.standard_normal((40, 768)).astype(np.float32)
+out = []
+with pkg.VectorEngine(device=0) as eng:
+    eng.create_collection("c1", 768, 0, 0)
+    eng.upsert("c1", list(range(221)), V)
+    for i in range(40):
+        s, r, c = eng.search("c1", Q[i:i + 1], 5)
+        out.append([s.view(np.uint32).tolist(), r.tolist(), c.tolist()])
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("env", [{"VS_SPIN_US": "0"}, {"VS_DIRECT_COMPLETION": "0"}])
+def test_small_completion_word_fallbacks(pkg, env):
+    """The one-launch small path publishes its keys through a completion word in
+    mapped host memory (HostDirect). Forty calls on one staging slot (the word's
+    sequence advancing) must give the same bits as with the word read only after
+    the stream's event (VS_SPIN_US=0: no spin, event then word check) and as the
+    D2H copy path (VS_DIRECT_COMPLETION=0)."""
+    import os
+    base = _run_py(_SMALL_COMPLETION)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        other = _run_py(_SMALL_COMPLETION)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert base == other
+
+
+def test_small_completion_concurrent(pkg, orc):
+    """Threads searching small collections at once: each call on its own staging
+    slot and completion word (contexts and slots shared); every reply equals
+    the serial one, bit for bit."""
+    import threading
+    rng = np.random.default_rng(5)
+    with pkg.VectorEngine(device=0) as eng:
+        names = []
+        for i, rows in enumerate((221, 64, 200)):
+            n = f"cc{i}"
+            eng.create_collection(n, 768, 0, i % 2)
+            eng.upsert(n, list(range(rows)), rng.standard_normal((rows, 768)).astype(np.float32))
+            names.append(n)
+        Q = rng.standard_normal((96, 768)).astype(np.float32)
+        jobs = [(names[i % 3], i, 1 + i % 16) for i in range(96)]
+        want = {j: eng.search(n, Q[j:j + 1], k) for n, j, k in jobs}
+        got, errs = {}, []
+
+        def worker(part):
+            try:
+                for _ in range(5):
+                    for n, j, k in part:
+                        got[j] = eng.search(n, Q[j:j + 1], k)
+                        w = want[j]
+                        if not (np.array_equal(got[j][0].view(np.uint32), w[0].view(np.uint32))
+                                and np.array_equal(got[j][1], w[1])):
+                            errs.append((n, j, k))
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(jobs[t::8],)) for t in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs[:5]
