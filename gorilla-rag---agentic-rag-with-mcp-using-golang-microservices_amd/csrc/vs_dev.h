@@ -282,8 +282,12 @@ struct HostDirect {
   uint64_t* keys = nullptr;  // device views of the mapped buffer
   uint64_t* flag = nullptr;
   uint64_t seq = 0;
+  const float* host_q = nullptr;  // raw query in host memory: sent in the kernel arguments
   bool used = false;
 };
+// search_core's one-launch small path takes this search (one query, no
+// filter, a small collection, k <= kGemvSmallMaxK)
+bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered);
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
                 const uint32_t* allow_list = nullptr, HostDirect* direct = nullptr);

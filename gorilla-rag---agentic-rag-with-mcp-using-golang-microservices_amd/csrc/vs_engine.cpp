@@ -475,6 +475,11 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   return VS_OK;
 }
 
+bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered) {
+  return nq == 1 && !filtered && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
+         vsk::gemv_small_ok(c.dim, (uint32_t)c.rows, k);
+}
+
 // Core search on device data. d_q: nq x dim fp32 on this device, ordered on
 // eng->stream. Writes nq x k keys to d_keys. work_mu and the collection's
 // reader lock are held by the caller.
@@ -492,7 +497,7 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
   // one query over a small collection (config C1): prep, scan and merge in
   // one launch (the same keys as the three launches below, bit for bit)
-  if (nq == 1 && !allow && vsk::gemv_small_ok(dim, (uint32_t)c.rows, k)) {
+  if (small_path(c, nq, k, allow != nullptr)) {
     constexpr size_t kPartBytes = (size_t)vsk::kGemvSmallMaxParts * vsk::kGemvSmallMaxK * 8;
     if (eng->small_part.bytes < kPartBytes + 64) {
       VS_HIP(hipStreamSynchronize(eng->stream), "sync");
@@ -504,7 +509,8 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                                   cosine, k, direct ? direct->keys : d_keys, eng->stream,
                                   eng->small_part.as<uint64_t>(),
                                   (uint32_t*)((char*)eng->small_part.p + kPartBytes),
-                                  direct ? direct->flag : nullptr, direct ? direct->seq : 0),
+                                  direct ? direct->flag : nullptr, direct ? direct->seq : 0,
+                                  direct ? direct->host_q : nullptr),
            "small scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     if (direct) direct->used = true;
@@ -1040,6 +1046,16 @@ bool direct_completion() {
   return v;
 }
 
+// The small path's query in the kernel arguments (on unless VS_QUERY_ARGS=0;
+// read once): no H2D copy for one-query calls on small collections.
+bool query_args() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_QUERY_ARGS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // A batched search of a large collection (the MFMA passes fill every CU for
 // milliseconds): such calls queue behind each other on the primary context,
 // so two of them never split the device and the batcher's pipelining (the
@@ -1111,7 +1127,12 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     hs = cx->host_slots.back().get();
   }
   VS_HIP(hs->ensure(qbytes, kbytes), "alloc pinned staging");
-  std::memcpy(hs->in, queries, qbytes);
+  // a call the one-launch small path takes writes its keys and a completion
+  // word straight to the slot's mapped buffer; its query travels in the
+  // kernel arguments (dim <= kGemvSmallArgDim: no H2D at all)
+  const bool direct = !abytes && !df && direct_completion() && small_path(*c, nq, k, false);
+  const bool qarg = direct && c->dim <= vsk::kGemvSmallArgDim && query_args();
+  if (!qarg) std::memcpy(hs->in, queries, qbytes);
   // busy from the first enqueue that reads the slot: a failure after it
   // drains the stream before the slot is released (a queued H2D may still
   // read hs->in, a queued D2H write hs->out)
@@ -1121,22 +1142,22 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     hs->busy = false;
     return rc;
   };
-  hipError_t e = hipMemcpyAsync(cx->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, cx->stream);
+  hipError_t e = hipSuccess;
+  if (!qarg) e = hipMemcpyAsync(cx->q_in.p, hs->in, qbytes, hipMemcpyHostToDevice, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "query H2D"));
   if (abytes) {  // pageable: HIP stages it (a shipped-bitmap call, not the batcher's path)
     e = hipMemcpyAsync(cx->allow.p, allow, abytes, hipMemcpyHostToDevice, cx->stream);
     if (e != hipSuccess) return abandon(fail_hip(e, "filter bitmap H2D"));
   }
-  // a one-query call may take the one-launch small path, which then writes
-  // its keys and a completion word straight to the slot's mapped buffer
   HostDirect hd;
   HostDirect* hdp = nullptr;
-  if (nq == 1 && !abytes && !df && k <= vsk::kGemvSmallMaxK && direct_completion()) {
+  if (direct) {
     e = hs->ensure_mapped(vsk::kGemvSmallMaxK + 1);
     if (e != hipSuccess) return abandon(fail_hip(e, "alloc mapped completion"));
     hd.keys = hs->mapped_dev;
     hd.flag = hs->mapped_dev + vsk::kGemvSmallMaxK;
     hd.seq = ++hs->seq;
+    hd.host_q = qarg ? queries : nullptr;
     hdp = &hd;
   }
   int rc;
@@ -1149,6 +1170,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
                      abytes ? cx->allow.as<uint64_t>() : nullptr,
                      abytes ? popcount_rows(allow, c->rows) : 0, nullptr, hdp);
   if (rc != VS_OK) return abandon(rc);
+  if (direct && !hd.used) return abandon(fail(VS_ERR_INTERNAL, "small path not taken"));
   if (!hd.used) e = hipMemcpyAsync(hs->out, cx->keys.p, kbytes, hipMemcpyDeviceToHost, cx->stream);
   if (e == hipSuccess) e = hipEventRecord(hs->done, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "keys D2H"));

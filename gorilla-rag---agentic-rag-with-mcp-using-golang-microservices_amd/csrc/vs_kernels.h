@@ -111,6 +111,9 @@ uint32_t compact_scratch_words(uint32_t n_rows);
 // With `flag`, `out` is mapped pinned host memory (k keys) and the kernel
 // stores `seq` to *flag (mapped host memory) after the keys are visible to
 // the host, which may then read them without waiting for the stream.
+// With `q_host` (dim <= kGemvSmallArgDim) the raw query is read from host
+// memory at launch and travels in the kernel arguments (q_raw unused).
+constexpr uint32_t kGemvSmallArgDim = 768;  // 3 KiB of fp32 in the argument segment
 constexpr uint32_t kGemvSmallMaxRows = 256;  // 32 rows per wave
 constexpr uint32_t kGemvSmallMaxK = 16;  // the workgroup merge is serial in k
 constexpr uint32_t kGemvSmallMaxParts = 16;
@@ -120,7 +123,7 @@ hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_
                              uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
                              uint64_t* out, hipStream_t st, uint64_t* part = nullptr,
                              uint32_t* counter = nullptr, uint64_t* flag = nullptr,
-                             uint64_t seq = 0);
+                             uint64_t seq = 0, const float* q_host = nullptr);
 
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);

@@ -17,6 +17,7 @@
 // Store side (upsert, Qdrant cosine preprocess) and the synthetic generator
 // are here too. Numerics contract: include/vsearch.h and DESIGN.md.
 #include <cstdlib>
+#include <cstring>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -967,7 +968,7 @@ __device__ __forceinline__ void signal_host(uint64_t* flag, uint64_t seq, int la
 // of a D2H copy and the stream's completion event, which cost ~6 us of a
 // ~18 us round trip (tools/rt_floor.hip, profiles/r03_rt_floor_graph_flag.json).
 template <int D, bool BF16, int U>
-__global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
+__device__ __forceinline__ void gemv_small_body(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, const float* __restrict__ q,
     uint32_t k, int prep, uint64_t* __restrict__ out, uint64_t* __restrict__ part,
     uint32_t* __restrict__ counter, uint64_t* flag, uint64_t seq) {
@@ -1151,6 +1152,31 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
   }
 }
 
+template <int D, bool BF16, int U>
+__global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
+    const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, const float* __restrict__ q,
+    uint32_t k, int prep, uint64_t* __restrict__ out, uint64_t* __restrict__ part,
+    uint32_t* __restrict__ counter, uint64_t* flag, uint64_t seq) {
+  gemv_small_body<D, BF16, U>(Xv, n_rows, row_base, q, k, prep, out, part, counter, flag, seq);
+}
+
+// The same search with the raw query in the kernel's argument segment (r03):
+// the dispatch carries it, so the call needs no H2D copy. QueryArg is the
+// first argument, so the query starts at the segment pointer.
+template <int D>
+struct QueryArg {
+  float v[D];
+};
+template <int D, bool BF16, int U>
+__global__ __launch_bounds__(kGemvThreads) void gemv_small_arg_kernel(
+    QueryArg<D> qa, const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, uint32_t k,
+    int prep, uint64_t* __restrict__ out, uint64_t* __restrict__ part,
+    uint32_t* __restrict__ counter, uint64_t* flag, uint64_t seq) {
+  const float* q = (const float*)(const __attribute__((address_space(4))) float*)
+      __builtin_amdgcn_kernarg_segment_ptr();
+  gemv_small_body<D, BF16, U>(Xv, n_rows, row_base, q, k, prep, out, part, counter, flag, seq);
+}
+
 uint32_t gemv_small_parts(uint32_t dim, bool bf16, uint32_t n_rows) {
   // one row-group step per wave: 8 waves x U groups x RB rows per workgroup
   const uint32_t epc = bf16 ? 8 : 4, cpr = dim / epc;
@@ -1177,12 +1203,21 @@ template <int D, bool BF16>
 static void gemv_small_launch(const void* X, uint32_t n_rows, uint32_t row_base,
                               const float* q_raw, int prep, uint32_t k, uint64_t* out,
                               uint64_t* part, uint32_t* counter, uint64_t* flag, uint64_t seq,
-                              hipStream_t st) {
+                              const float* q_host, hipStream_t st) {
   // row groups per step: 4 (8 with the next step's loads issued ahead was
   // slower: 14.9 us against 12.6 at 221 rows), fewer past 3 chunks per lane
   constexpr int J = GemvShape<D, BF16>::J;
   constexpr int U = J <= 3 ? 4 : (12 / J > 0 ? 12 / J : 1);
   const uint32_t nwg = part ? gemv_small_parts(D, BF16, n_rows) : 1;
+  if constexpr (D <= (int)kGemvSmallArgDim) {
+    if (q_host) {
+      QueryArg<D> qa;
+      std::memcpy(qa.v, q_host, sizeof(qa.v));
+      hipLaunchKernelGGL((gemv_small_arg_kernel<D, BF16, U>), dim3(nwg), dim3(kGemvThreads), 0,
+                         st, qa, X, n_rows, row_base, k, prep, out, part, counter, flag, seq);
+      return;
+    }
+  }
   hipLaunchKernelGGL((gemv_small_kernel<D, BF16, U>), dim3(nwg), dim3(kGemvThreads), 0, st, X,
                      n_rows, row_base, q_raw, k, prep, out, part, counter, flag, seq);
 }
@@ -1198,18 +1233,19 @@ bool gemv_small_ok(uint32_t dim, uint32_t n_rows, uint32_t k) {
 hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const float* q_raw, bool cosine, uint32_t k,
                              uint64_t* out, hipStream_t st, uint64_t* part, uint32_t* counter,
-                             uint64_t* flag, uint64_t seq) {
+                             uint64_t* flag, uint64_t seq, const float* q_host) {
   if (!gemv_small_ok(dim, n_rows, k)) return hipErrorInvalidValue;
+  if (q_host && dim > kGemvSmallArgDim) return hipErrorInvalidValue;
   if (!counter) part = nullptr;
   const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
 #define VS_SMALL_CASE(DD)                                                                   \
   case DD:                                                                                  \
     if (bf16)                                                                               \
       gemv_small_launch<DD, true>(X, n_rows, row_base, q_raw, prep, k, out, part, counter,  \
-                                  flag, seq, st);                                           \
+                                  flag, seq, q_host, st);                                   \
     else                                                                                    \
       gemv_small_launch<DD, false>(X, n_rows, row_base, q_raw, prep, k, out, part, counter, \
-                                   flag, seq, st);                                          \
+                                   flag, seq, q_host, st);                                  \
     break;
   switch (dim) {
     VS_SMALL_CASE(128)

@@ -544,13 +544,15 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env", [{"VS_SPIN_US": "0"}, {"VS_DIRECT_COMPLETION": "0"}])
+@pytest.mark.parametrize("env", [{"VS_SPIN_US": "0"}, {"VS_DIRECT_COMPLETION": "0"},
+                                 {"VS_QUERY_ARGS": "0"}])
 def test_small_completion_word_fallbacks(pkg, env):
     """The one-launch small path publishes its keys through a completion word in
     mapped host memory (HostDirect). Forty calls on one staging slot (the word's
     sequence advancing) must give the same bits as with the word read only after
-    the stream's event (VS_SPIN_US=0: no spin, event then word check) and as the
-    D2H copy path (VS_DIRECT_COMPLETION=0)."""
+    the stream's event (VS_SPIN_US=0: no spin, event then word check), as the
+    D2H copy path (VS_DIRECT_COMPLETION=0) and as the query copied to the
+    device instead of sent in the kernel arguments (VS_QUERY_ARGS=0)."""
     import os
     base = _run_py(_SMALL_COMPLETION)
     old = {k: os.environ.get(k) for k in env}

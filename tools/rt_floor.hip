@@ -14,6 +14,8 @@
 //   flag_map h2d + a kernel that writes its keys and then a sequence word to
 //            mapped pinned memory (system-scope fence between); the host
 //            spins on the word, no event (r03)
+//   arg_flag the query passed by value in the kernel arguments (3 KiB, no
+//            H2D copy) + flag_map's completion word (r03)
 //   vs_search  the engine's host API on config C1 (221 x 768 fp32 cosine,
 //            one query, k = 5): everything above plus the engine's own work
 //
@@ -57,6 +59,28 @@ __global__ void touch(const float* __restrict__ in, uint64_t* __restrict__ out, 
 // keys to mapped host memory, then (after a system-scope fence) the call's
 // sequence number: a host that sees the number sees the keys
 __global__ void touch_flag(const float* __restrict__ in, uint64_t* out, int n, uint64_t seq) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += in[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 256; ++i) t += red[i];
+    for (int i = 0; i < 5; ++i) out[i] = (uint64_t)__float_as_uint(t) + (uint64_t)i;
+    __threadfence_system();
+    __hip_atomic_store(out + 7, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// the query travels in the kernel's argument segment (read through the
+// segment pointer, vector loads: the struct is the first argument)
+struct QArg {
+  float v[768];
+};
+__global__ void touch_arg(QArg qa, uint64_t* out, int n, uint64_t seq) {
+  const __attribute__((address_space(4))) float* in =
+      (const __attribute__((address_space(4))) float*)__builtin_amdgcn_kernarg_segment_ptr();
   __shared__ float red[256];
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) s += in[i];
@@ -141,6 +165,16 @@ int main() {
          (void)hipMemcpyAsync(h_out, d_out, 40, hipMemcpyDeviceToHost, st);
        },
        0},
+      {"arg_flag",
+       [&] {
+         ++seq;
+         QArg qa;
+         std::memcpy(qa.v, h_in, sizeof(qa.v));
+         hipLaunchKernelGGL(touch_arg, dim3(1), dim3(256), 0, st, qa, m_out, n, seq);
+         while (__atomic_load_n((volatile uint64_t*)(m_out + 7), __ATOMIC_ACQUIRE) != seq) {
+         }
+       },
+       2},
       {"graph", [&] { (void)hipGraphLaunch(gexec, st); }, 0},
       {"flag_map",
        [&] {
