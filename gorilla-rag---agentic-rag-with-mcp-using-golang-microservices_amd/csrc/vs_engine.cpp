@@ -255,7 +255,13 @@ int device_checksum(DevEngine* eng, const Collection& c, uint64_t* out) {
 // workgroups, each over L / G lists, runs the merge in parallel. G divides
 // L and leaves >= 8 lists per group.
 uint32_t merge_groups(uint32_t L, uint32_t k) {
-  if (k <= 32 || (uint64_t)L * k <= 8192) return 1;
+  // VS_MERGE_TWO_STAGE=0 (read once): one workgroup always (ablation of the
+  // r03 sample-bound merge against the two stages)
+  static const bool two = [] {
+    const char* e = std::getenv("VS_MERGE_TWO_STAGE");
+    return !(e && e[0] == '0');
+  }();
+  if (!two || k <= 32 || (uint64_t)L * k <= 8192) return 1;
   for (uint32_t g = 64; g >= 4; --g)
     if (L % g == 0 && L / g >= 8) return g;
   return 1;

@@ -2921,6 +2921,83 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
     return;
   }
 
+  // Sample bound + list walk (r03). The lists are sorted descending without
+  // repeats, so the k-th largest DISTINCT key among the first m entries of
+  // every list (a subset of the keys) has at least k distinct keys at or
+  // above it: a lower bound on the k-th largest key overall. Each list is
+  // then read only down to that bound -- for a single-query GEMV merge a
+  // step or two per list instead of all L x kin keys (the filter below read
+  // every key and bitonic-sorted whatever passed max_l list_l[k-1], a weak
+  // bound: 175 us for 758 lists of 100 at 200k rows). Survivors past
+  // kMergeCap fall through to that filter with the sample bound.
+  uint64_t sthr = 0;
+  {
+    const uint32_t m0 = (2 * k + L - 1) / L;
+    const uint32_t m = m0 < 1 ? 1 : (m0 > kin ? kin : m0);
+    const uint64_t ns64 = (uint64_t)L * m;
+    const uint32_t ns = ns64 < (uint64_t)kMergeCap ? (uint32_t)ns64 : (uint32_t)kMergeCap;
+    int p2 = 1;
+    while ((uint32_t)p2 < ns) p2 <<= 1;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)p2; i += kMergeThreads) {
+      uint64_t x = 0;
+      if (i < ns) {
+        const uint32_t l = i / m, j = i - l * m;
+        x = lists[l * lstride + q * qstride + j];
+      }
+      buf[i] = x;
+    }
+    __syncthreads();
+    bitonic_sort_desc(buf, p2);
+    const uint32_t u = dedupe_sorted(buf, ns, cnt);
+    if (u >= k) {
+      sthr = buf[k - 1] - 1;  // survivors: keys >= the sample's k-th distinct key
+      __syncthreads();        // every thread has read buf[k - 1]
+      if (threadIdx.x == 0) cnt = 0;
+      __syncthreads();
+      // tpl threads per list (a power of two <= 64: lanes of one wave), each
+      // step reading 4 consecutive keys per thread; a list's walk ends at the
+      // first step whose last key is under the bound
+      uint32_t tpl = 1;
+      while (tpl < 64 && (uint64_t)L * tpl * 2 <= (uint64_t)kMergeThreads) tpl <<= 1;
+      const uint32_t gpb = kMergeThreads / tpl;
+      const uint32_t g = threadIdx.x / tpl, sl = threadIdx.x % tpl;
+      const int src = (lane & ~(int)(tpl - 1)) + (int)tpl - 1;
+      for (uint32_t l = g; l < L; l += gpb) {
+        const uint64_t* lp = lists + l * lstride + q * qstride;
+        for (uint32_t j0 = 0; j0 < kin; j0 += tpl * 4) {
+          uint64_t x[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const uint32_t j = j0 + sl * 4 + (uint32_t)v;
+            x[v] = j < kin ? lp[j] : 0ull;
+          }
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (x[v] > sthr) {
+              const uint32_t at = atomicAdd(&cnt, 1u);
+              if (at < (uint32_t)kMergeCap) buf[at] = x[v];
+            }
+          if (__shfl(x[3], src, 64) <= sthr) break;  // the group's last key
+        }
+      }
+      __syncthreads();
+      const uint32_t c = cnt;
+      if (c <= (uint32_t)kMergeCap) {
+        int p3 = 1;
+        while ((uint32_t)p3 < c) p3 <<= 1;
+        for (uint32_t i = c + threadIdx.x; i < (uint32_t)p3; i += kMergeThreads) buf[i] = 0;
+        __syncthreads();
+        bitonic_sort_desc(buf, p3);
+        const uint32_t u2 = dedupe_sorted(buf, c, cnt);
+        const uint32_t nR = u2 < k ? u2 : k;
+        for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads)
+          out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
+        return;
+      }
+      __syncthreads();  // overflow: the filter below, from the sample bound
+    }
+  }
+
   // initial bound (strict filter "key > thr")
   uint64_t b = 0;
   if (kin >= k)
@@ -2938,6 +3015,7 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   uint64_t bound = 0;
   for (int i = 0; i < kMergeThreads / 64; ++i) bound = red[i] > bound ? red[i] : bound;
   uint64_t thr = bound ? bound - 1 : 0;  // admit the bound itself
+  thr = sthr > thr ? sthr : thr;
 
   const uint64_t total = (uint64_t)L * kin;
   const uint32_t chunk = kMergeCap - k;

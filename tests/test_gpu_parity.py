@@ -459,7 +459,13 @@ bad = []
 for L, kin, k, nd in ((8, 10, 10, 6), (8, 10, 64, 30), (40, 100, 20, 15), (40, 100, 20, 300),
                       (12, 100, 100, 50), (12, 100, 100, 700), (100, 100, 100, 2000),
                       (4, 2000, 3000, 5000), (3, 1500, 1500, 2000), (8, 10, 2000, 50),
-                      (5, 1200, 1100, 900)):
+                      (5, 1200, 1100, 900),
+                      # r03 sample bound + list walk (k > 32 or many keys): many
+                      # lists, heavy overlap (survivors past the LDS buffer:
+                      # the filter fallback), two long lists, kin < k
+                      (758, 100, 100, 20000), (758, 100, 100, 400), (1000, 100, 100, 3000),
+                      (2, 1024, 1024, 3000), (1500, 16, 100, 8000), (64, 128, 128, 10000),
+                      (33, 50, 40, 5000), (5000, 8, 64, 30000)):
     nq = 3
     pool = np.unique(rng.integers(1 << 40, 1 << 62, size=nd * 2, dtype=np.uint64))[:nd]
     lists = np.zeros((L, nq, kin), np.uint64)
