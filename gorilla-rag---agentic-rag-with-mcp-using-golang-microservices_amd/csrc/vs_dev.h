@@ -93,8 +93,8 @@ struct HostSlot {
   size_t in_bytes = 0, out_bytes = 0;
   hipEvent_t done = nullptr;
   bool busy = false;  // between its enqueue and the end of its decode
-  // small-path completion (r03): kGemvSmallMaxK keys + the sequence word, in
-  // coherent mapped pinned memory the kernel writes directly (HostDirect)
+  // one-query completion (r03): up to kMaxK keys + the sequence word, in
+  // coherent mapped pinned memory the last kernel writes directly (HostDirect)
   uint64_t* mapped = nullptr;
   uint64_t* mapped_dev = nullptr;  // the same memory as the device sees it
   uint64_t seq = 0;
@@ -275,9 +275,11 @@ hipError_t wait_event(hipEvent_t ev);
 // eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and
 // the collection's reader lock held by the caller. Asynchronous: nothing
 // waits on the device unless a scratch buffer has to grow.
-// With `direct`, a search that takes the one-launch small path writes its
-// keys to direct->keys (mapped pinned host memory) and then direct->seq to
-// *direct->flag, and sets direct->used; d_keys is then not written.
+// With `direct` (one query), a search whose last kernel can publish to the
+// host -- the one-launch small path, or the GEMV list path's merge -- writes
+// its keys to direct->keys (mapped pinned host memory) and then direct->seq
+// to *direct->flag, and sets direct->used; d_keys is then not written. Other
+// paths leave direct->used false and write d_keys.
 struct HostDirect {
   uint64_t* keys = nullptr;  // device views of the mapped buffer
   uint64_t* flag = nullptr;

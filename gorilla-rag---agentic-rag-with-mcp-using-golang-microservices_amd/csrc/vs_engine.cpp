@@ -255,11 +255,13 @@ int device_checksum(DevEngine* eng, const Collection& c, uint64_t* out) {
 // workgroups, each over L / G lists, runs the merge in parallel. G divides
 // L and leaves >= 8 lists per group.
 uint32_t merge_groups(uint32_t L, uint32_t k) {
-  // VS_MERGE_TWO_STAGE=0 (read once): one workgroup always (ablation of the
-  // r03 sample-bound merge against the two stages)
+  // r03: off unless VS_MERGE_TWO_STAGE=1 (read once). With the sample-bound
+  // merge one workgroup is as fast or faster at every size measured (bf16,
+  // one query: 2k rows k = 100 89.7 -> 47.6 us, 20k 71.3 -> 63.5, 12.5M
+  // 2962 -> 2953; profiles/r03_merge_two_stage_ab.jsonl)
   static const bool two = [] {
     const char* e = std::getenv("VS_MERGE_TWO_STAGE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (!two || k <= 32 || (uint64_t)L * k <= 8192) return 1;
   for (uint32_t g = 64; g >= 4; --g)
@@ -269,7 +271,8 @@ uint32_t merge_groups(uint32_t L, uint32_t k) {
 
 int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t n, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr,
-                const uint32_t* gather = nullptr, uint32_t n_gather = 0) {
+                const uint32_t* gather = nullptr, uint32_t n_gather = 0,
+                HostDirect* direct = nullptr) {
   const uint32_t dim = c.dim;
   const bool bf16 = c.dtype == VS_DTYPE_BF16;
   const uint32_t n_rows = gather ? n_gather : (uint32_t)c.rows;
@@ -302,6 +305,11 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
       VS_HIP(vsk::launch_merge(eng->merge_tmp.as<uint64_t>(), G, k, 0, 1, k, k,
                                d_keys + (size_t)(i - q0) * k, eng->stream),
              "merge");
+    } else if (direct && n == 1) {  // the keys and the completion word to the host
+      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k, direct->keys,
+                               eng->stream, direct->flag, direct->seq),
+             "merge");
+      direct->used = true;
     } else {
       VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
                                d_keys + (size_t)(i - q0) * k, eng->stream),
@@ -593,7 +601,7 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     }
     return search_gemv(eng, c, qp, 0, nq, k, d_keys, nullptr, allow_list, (uint32_t)allowed);
   }
-  return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
+  return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow, nullptr, 0, direct);
 }
 
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
@@ -1136,8 +1144,9 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   // a call the one-launch small path takes writes its keys and a completion
   // word straight to the slot's mapped buffer; its query travels in the
   // kernel arguments (dim <= kGemvSmallArgDim: no H2D at all)
-  const bool direct = !abytes && !df && direct_completion() && small_path(*c, nq, k, false);
-  const bool qarg = direct && c->dim <= vsk::kGemvSmallArgDim && query_args();
+  const bool direct = nq == 1 && !abytes && !df && k <= vsk::kMaxK && direct_completion();
+  const bool qarg = direct && small_path(*c, nq, k, false) &&
+                    c->dim <= vsk::kGemvSmallArgDim && query_args();
   if (!qarg) std::memcpy(hs->in, queries, qbytes);
   // busy from the first enqueue that reads the slot: a failure after it
   // drains the stream before the slot is released (a queued H2D may still
@@ -1158,10 +1167,10 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   HostDirect hd;
   HostDirect* hdp = nullptr;
   if (direct) {
-    e = hs->ensure_mapped(vsk::kGemvSmallMaxK + 1);
+    e = hs->ensure_mapped(vsk::kMaxK + 1);
     if (e != hipSuccess) return abandon(fail_hip(e, "alloc mapped completion"));
     hd.keys = hs->mapped_dev;
-    hd.flag = hs->mapped_dev + vsk::kGemvSmallMaxK;
+    hd.flag = hs->mapped_dev + vsk::kMaxK;
     hd.seq = ++hs->seq;
     hd.host_q = qarg ? queries : nullptr;
     hdp = &hd;
@@ -1176,7 +1185,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
                      abytes ? cx->allow.as<uint64_t>() : nullptr,
                      abytes ? popcount_rows(allow, c->rows) : 0, nullptr, hdp);
   if (rc != VS_OK) return abandon(rc);
-  if (direct && !hd.used) return abandon(fail(VS_ERR_INTERNAL, "small path not taken"));
+  if (qarg && !hd.used) return abandon(fail(VS_ERR_INTERNAL, "small path not taken"));
   if (!hd.used) e = hipMemcpyAsync(hs->out, cx->keys.p, kbytes, hipMemcpyDeviceToHost, cx->stream);
   if (e == hipSuccess) e = hipEventRecord(hs->done, cx->stream);
   if (e != hipSuccess) return abandon(fail_hip(e, "keys D2H"));
@@ -1188,7 +1197,7 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     // the kernel's completion word: its keys are in place once it reads seq
     // (the H2D that read hs->in ran before the kernel; nothing after the
     // kernel touches the slot). Past the spin limit, the stream's event.
-    const uint64_t* word = hs->mapped + vsk::kGemvSmallMaxK;
+    const uint64_t* word = hs->mapped + vsk::kMaxK;
     if (!wait_word(word, hd.seq)) {
       we = hipEventSynchronize(hs->done);
       if (we == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != hd.seq)

@@ -191,9 +191,13 @@ void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);
 
 // Merge L sorted key lists per query -> out [nq][k] (global top-k by key).
 // List l of query q starts at lists[l * lstride + q * qstride], kin entries.
+// With `flag` (nq == 1; out and flag in mapped pinned host memory) every
+// writer fences at system scope, then `seq` is stored to *flag: the host may
+// read out once it sees seq (as launch_gemv_small's completion word).
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k,
-                        uint64_t* out, hipStream_t st);
+                        uint64_t* out, hipStream_t st, uint64_t* flag = nullptr,
+                        uint64_t seq = 0);
 
 // Convert fp32 queries (nq x dim) to bf16 (after preprocessing).
 hipError_t launch_to_bf16(const float* in, uint64_t n, uint16_t* out,

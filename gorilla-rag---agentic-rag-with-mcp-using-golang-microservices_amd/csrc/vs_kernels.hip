@@ -465,26 +465,48 @@ __device__ __forceinline__ float chunk_dot(const uint4& c, const float* qv) {
 template <int KPL>
 __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint32_t k,
                                           int lane, int w, uint64_t* __restrict__ out) {
+  (void)theta;
   if constexpr (KPL <= 2) {
+    // r03: by rank, not by serial inserts. Each wave list is sorted, distinct
+    // (distinct rows) and 0 past its keys, so a key's place in the
+    // workgroup's list is its index in its own list plus, for each other
+    // wave, the number of that wave's keys above it (a binary search over
+    // sm[ow][0, k)); every lane places its keys at once. The serial form had
+    // wave 0 insert the other 7 lists one key at a time: at k = 100 over 33
+    // rows per wave, 231 dependent inserts at the end of every workgroup.
     __shared__ uint64_t sm[kGemvWaves][64 * KPL];
+    __shared__ uint32_t nzw[kGemvWaves];
+    uint32_t nz = 0;
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) sm[w][i * 64 + lane] = L.e[i];
+    for (int i = 0; i < KPL; ++i) {
+      sm[w][i * 64 + lane] = L.e[i];
+      nz += (uint32_t)__popcll(__ballot(L.e[i] != 0));
+    }
+    if (lane == 0) nzw[w] = nz;
     __syncthreads();
-    if (w == 0) {
-      for (int ow = 1; ow < kGemvWaves; ++ow) {
-        for (uint32_t j = 0; j < k; ++j) {
-          const uint64_t x = sm[ow][j];  // uniform LDS broadcast
-          if (x <= theta) break;         // lists are sorted: the rest cannot enter
-          L.insert(x, k, lane);
-          theta = L.kth(k);
-        }
-      }
+    uint32_t tot = 0;
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) {
-        const uint32_t idx = (uint32_t)(i * 64 + lane);
-        if (idx < k) out[(size_t)blockIdx.x * k + idx] = L.e[i];
+    for (int ow = 0; ow < kGemvWaves; ++ow) tot += nzw[ow];
+    uint32_t top = 1;  // highest power of two <= k
+    while (top * 2 <= k) top *= 2;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const uint32_t e = (uint32_t)(i * 64 + lane);
+      const uint64_t x = L.e[i];
+      if (e < k && x != 0) {
+        uint32_t r = e;
+#pragma unroll
+        for (int ow = 0; ow < kGemvWaves; ++ow) {
+          if (ow == w) continue;
+          uint32_t pos = 0;  // entries of sm[ow][0, k) above x
+          for (uint32_t st = top; st > 0; st >>= 1)
+            if (pos + st <= k && sm[ow][pos + st - 1] > x) pos += st;
+          r += pos;
+        }
+        if (r < k) out[(size_t)blockIdx.x * k + r] = x;
       }
     }
+    for (uint32_t r = tot + threadIdx.x; r < k; r += kGemvThreads) out[(size_t)blockIdx.x * k + r] = 0;
   } else {
     const size_t li = (size_t)blockIdx.x * kGemvWaves + w;
 #pragma unroll
@@ -2814,7 +2836,8 @@ __device__ __forceinline__ uint32_t dedupe_sorted(uint64_t* buf, uint32_t c, uin
 __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, uint32_t L,
                                             uint64_t lstride, uint64_t qstride, uint32_t kin,
                                             uint32_t k, uint32_t q, uint64_t* __restrict__ out,
-                                            uint64_t* buf, uint64_t* red, uint32_t& cnt) {
+                                            uint64_t* buf, uint64_t* red, uint32_t& cnt,
+                                            bool tourney = true) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 
   // Fast path (single-query GEMV merges and shard merges at k <= 32): all
@@ -2856,7 +2879,10 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
     for (uint32_t r = nz + t; r < k; r += kMergeThreads) out[(size_t)q * k + r] = 0;
     return;
   }
-  if (total0 <= (uint64_t)kMergeThreads * kMergeHeld && k <= 32) {
+  // (r03: only for many lists and k <= 10 -- elsewhere the sample-bound path
+  // below is as fast or faster: one query at 2k rows, k = 32: 61.6 -> 34.7
+  // us; profiles/r03_merge_tourney_ab.jsonl)
+  if (tourney && L >= 256 && k <= 10 && total0 <= (uint64_t)kMergeThreads * kMergeHeld) {
     uint64_t x[kMergeHeld];
     // every load issued unconditionally (clamped index), all in flight at
     // once; a conditional load per key compiled to one round trip each
@@ -2922,36 +2948,61 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   }
 
   // Sample bound + list walk (r03). The lists are sorted descending without
-  // repeats, so the k-th largest DISTINCT key among the first m entries of
-  // every list (a subset of the keys) has at least k distinct keys at or
-  // above it: a lower bound on the k-th largest key overall. Each list is
-  // then read only down to that bound -- for a single-query GEMV merge a
-  // step or two per list instead of all L x kin keys (the filter below read
-  // every key and bitonic-sorted whatever passed max_l list_l[k-1], a weak
-  // bound: 175 us for 758 lists of 100 at 200k rows). Survivors past
-  // kMergeCap fall through to that filter with the sample bound.
+  // repeats, so the k-th largest key among the first m entries of every list
+  // (a subset of the keys) has at least k keys at or above it -- k DISTINCT
+  // keys unless lists share keys (replicated shards), which the walk's result
+  // reveals (fewer than k distinct survivors: the filter below runs instead).
+  // That key bounds the k-th largest key overall from below, so each list is
+  // read only down to it: for a single-query GEMV merge a step or two per
+  // list instead of all L x kin keys (the filter below read every key and
+  // bitonic-sorted whatever passed max_l list_l[k-1], a weak bound: 175 us for
+  // 758 lists of 100 at 200k rows). The sample (<= 512 keys: one per thread,
+  // so a weaker bound for many lists) is ranked, not sorted, and so are the
+  // survivors when they are <= 512: no sort on the common path.
   uint64_t sthr = 0;
   {
+    constexpr uint32_t kSample = kMergeThreads;  // one sampled key per thread
     const uint32_t m0 = (2 * k + L - 1) / L;
     const uint32_t m = m0 < 1 ? 1 : (m0 > kin ? kin : m0);
     const uint64_t ns64 = (uint64_t)L * m;
-    const uint32_t ns = ns64 < (uint64_t)kMergeCap ? (uint32_t)ns64 : (uint32_t)kMergeCap;
-    int p2 = 1;
-    while ((uint32_t)p2 < ns) p2 <<= 1;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)p2; i += kMergeThreads) {
-      uint64_t x = 0;
-      if (i < ns) {
-        const uint32_t l = i / m, j = i - l * m;
-        x = lists[l * lstride + q * qstride + j];
-      }
-      buf[i] = x;
+    const uint32_t ns = ns64 < (uint64_t)kSample ? (uint32_t)ns64 : kSample;
+    uint64_t x = 0;
+    if (threadIdx.x < ns) {
+      const uint32_t l = threadIdx.x / m, j = threadIdx.x - l * m;
+      x = lists[l * lstride + q * qstride + j];
+    }
+    buf[threadIdx.x] = x;
+    __syncthreads();
+    // the smallest sampled key with at most k - 1 sampled keys above it (the
+    // sample's k-th largest); none if fewer than k sampled keys are non-zero
+    uint64_t cand = ~0ull;
+    uint32_t nzc = x != 0 ? 1u : 0u;
+    if (x != 0) {
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < ns; ++j) r += buf[j] > x ? 1u : 0u;
+      if (r < k) cand = x;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint64_t y = __shfl_xor(cand, o, 64);
+      cand = y < cand ? y : cand;
+      nzc += __shfl_xor(nzc, o, 64);
+    }
+    __syncthreads();  // buf reads done
+    if (lane == 0) {
+      red[w] = cand;
+      buf[w] = nzc;
     }
     __syncthreads();
-    bitonic_sort_desc(buf, p2);
-    const uint32_t u = dedupe_sorted(buf, ns, cnt);
-    if (u >= k) {
-      sthr = buf[k - 1] - 1;  // survivors: keys >= the sample's k-th distinct key
-      __syncthreads();        // every thread has read buf[k - 1]
+    uint64_t sb = ~0ull;
+    uint32_t nz = 0;
+    for (int i = 0; i < kMergeThreads / 64; ++i) {
+      sb = red[i] < sb ? red[i] : sb;
+      nz += (uint32_t)buf[i];
+    }
+    __syncthreads();  // red / buf reads done
+    if (nz >= k && sb != ~0ull) {
+      sthr = sb - 1;  // survivors: keys >= sb
       if (threadIdx.x == 0) cnt = 0;
       __syncthreads();
       // tpl threads per list (a power of two <= 64: lanes of one wave), each
@@ -2982,19 +3033,40 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
       }
       __syncthreads();
       const uint32_t c = cnt;
-      if (c <= (uint32_t)kMergeCap) {
+      if (c <= (uint32_t)kMergeThreads) {
+        // rank placement, as the few-keys path above: a repeated key counts at
+        // its first position only
+        const uint32_t t = threadIdx.x;
+        const uint64_t x = t < c ? buf[t] : 0ull;
+        bool first = x != 0;
+        for (uint32_t i = 0; first && i < t; ++i) first = buf[i] != x;
+        buf[kMergeThreads + t] = first ? x : 0ull;
+        const uint32_t u2 = (uint32_t)__syncthreads_count(first);
+        if (u2 >= k) {
+          if (first) {
+            uint32_t rank = 0;
+            for (uint32_t i = 0; i < c; ++i) rank += buf[kMergeThreads + i] > x ? 1u : 0u;
+            if (rank < k) out[(size_t)q * k + rank] = x;
+          }
+          return;
+        }
+      } else if (c <= (uint32_t)kMergeCap) {
         int p3 = 1;
         while ((uint32_t)p3 < c) p3 <<= 1;
         for (uint32_t i = c + threadIdx.x; i < (uint32_t)p3; i += kMergeThreads) buf[i] = 0;
         __syncthreads();
         bitonic_sort_desc(buf, p3);
         const uint32_t u2 = dedupe_sorted(buf, c, cnt);
-        const uint32_t nR = u2 < k ? u2 : k;
-        for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads)
-          out[(size_t)q * k + j] = j < nR ? buf[j] : 0;
-        return;
+        if (u2 >= k) {
+          for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads) out[(size_t)q * k + j] = buf[j];
+          return;
+        }
       }
-      __syncthreads();  // overflow: the filter below, from the sample bound
+      // fewer than k distinct survivors (lists sharing keys inflated the
+      // sample's ranks), or more survivors than the buffer holds (whose
+      // distinct count is unknown): the filter below, without the sample bound
+      sthr = 0;
+      __syncthreads();
     }
   }
 
@@ -3015,7 +3087,6 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   uint64_t bound = 0;
   for (int i = 0; i < kMergeThreads / 64; ++i) bound = red[i] > bound ? red[i] : bound;
   uint64_t thr = bound ? bound - 1 : 0;  // admit the bound itself
-  thr = sthr > thr ? sthr : thr;
 
   const uint64_t total = (uint64_t)L * kin;
   const uint32_t chunk = kMergeCap - k;
@@ -3063,19 +3134,36 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
 
 __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
     const uint64_t* __restrict__ lists, uint32_t L, uint64_t lstride, uint64_t qstride,
-    uint32_t kin, uint32_t k, uint64_t* __restrict__ out) {
+    uint32_t kin, uint32_t k, uint64_t* __restrict__ out, int tourney, uint64_t* flag,
+    uint64_t seq) {
   __shared__ uint64_t buf[kMergeCap];
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t cnt;
-  merge_query(lists, L, lstride, qstride, kin, k, blockIdx.x, out, buf, red, cnt);
+  merge_query(lists, L, lstride, qstride, kin, k, blockIdx.x, out, buf, red, cnt, tourney != 0);
+  if (flag) {  // merge_query returns on block-uniform paths: every thread is here
+    __threadfence_system();  // this thread's key stores, host-visible
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// VS_MERGE_TOURNEY=0 (read once; ablation): k <= 32 merges of up to 8192
+// keys take the sample-bound path instead of the register tournament
+static int merge_tourney() {
+  static const int v = [] {
+    const char* e = getenv("VS_MERGE_TOURNEY");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
 }
 
 hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
                         uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out,
-                        hipStream_t st) {
+                        hipStream_t st, uint64_t* flag, uint64_t seq) {
   if (k == 0 || k > kMaxK || nq == 0 || L == 0 || kin == 0) return hipErrorInvalidValue;
+  if (flag && nq != 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(merge_keys_kernel, dim3(nq), dim3(kMergeThreads), 0, st, lists, L,
-                     lstride, qstride, kin, k, out);
+                     lstride, qstride, kin, k, out, merge_tourney(), flag, seq);
   return hipGetLastError();
 }
 

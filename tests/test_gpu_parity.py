@@ -486,6 +486,27 @@ for L, kin, k, nd in ((8, 10, 10, 6), (8, 10, 64, 30), (40, 100, 20, 15), (40, 1
         want[:min(k, u.size)] = u[:k]
         if not np.array_equal(got[q], want):
             bad.append([L, kin, k, nd, q, got[q][:8].tolist(), want[:8].tolist()])
+# replicated lists (every list the same keys): the sample's ranks count each
+# key L times, so its bound overshoots; the merge must notice and fall back
+for L, kin, k, nd in ((5000, 64, 100, 64), (600, 100, 100, 100), (40, 100, 64, 70)):
+    nq = 2
+    one = np.zeros((nq, kin), np.uint64)
+    for q in range(nq):
+        pool = np.unique(rng.integers(1 << 40, 1 << 62, size=nd * 2, dtype=np.uint64))[:nd]
+        one[q, :min(kin, nd)] = np.sort(pool)[::-1][:kin]
+    lists = np.ascontiguousarray(np.broadcast_to(one, (L, nq, kin)))
+    d = torch.from_numpy(lists.view(np.int64)).cuda()
+    out = torch.full((nq, k), 12345, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    eng.merge_keys(d.data_ptr(), L, nq, kin, k, out.data_ptr(), st)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    for q in range(nq):
+        u = np.unique(one[q][one[q] != 0])[::-1]
+        want = np.zeros(k, np.uint64)
+        want[:min(k, u.size)] = u[:k]
+        if not np.array_equal(got[q], want):
+            bad.append(["replicated", L, kin, k, q, got[q][:8].tolist(), want[:8].tolist()])
 print(json.dumps({"bad": bad[:5]}))
 """
 
