@@ -489,6 +489,8 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   return VS_OK;
 }
 
+int gemv_one();
+
 bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered) {
   return nq == 1 && !filtered && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
          vsk::gemv_small_ok(c.dim, (uint32_t)c.rows, k);
@@ -511,13 +513,20 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
     return fail(VS_ERR_INVALID_ARG, "collection exceeds 2^32-1 rows");
   // one query over a small collection (config C1): prep, scan and merge in
   // one launch (the same keys as the three launches below, bit for bit)
-  if (small_path(c, nq, k, allow != nullptr)) {
-    constexpr size_t kPartBytes = (size_t)vsk::kGemvSmallMaxParts * vsk::kGemvSmallMaxK * 8;
+  constexpr size_t kPartBytes = (size_t)vsk::kGemvSmallMaxParts * vsk::kGemvSmallMaxK * 8;
+  // the small path's parts + counter, and the one-launch GEMV's counter (the
+  // word after it): zeroed once, left zero by the kernels
+  auto ensure_counters = [&]() -> int {
     if (eng->small_part.bytes < kPartBytes + 64) {
       VS_HIP(hipStreamSynchronize(eng->stream), "sync");
       VS_HIP(eng->small_part.ensure(kPartBytes + 64), "alloc small-scan parts");
       VS_HIP(hipMemsetAsync(eng->small_part.p, 0, eng->small_part.bytes, eng->stream), "zero");
     }
+    return VS_OK;
+  };
+  if (small_path(c, nq, k, allow != nullptr)) {
+    const int rc0 = ensure_counters();
+    if (rc0 != VS_OK) return rc0;
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_gemv_small(c.data, bf16, dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q,
                                   cosine, k, direct ? direct->keys : d_keys, eng->stream,
@@ -557,6 +566,39 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                       (!use_mfma || (double)nq * (double)(allowed * rbytes + kGatherCallBytes) <=
                                         (double)c.rows * (double)rbytes);
   if (gather) use_mfma = false;
+  // one query on the GEMV list path: query prep, scan and merge in one launch
+  // (the last workgroup merges), the answer straight to the host with `direct`
+  if (nq == 1 && !use_mfma && !gather && k < large_k_from() && gemv_one() != 0 &&
+      vsk::gemv_one_ok(dim, k)) {
+    const int rc0 = ensure_counters();
+    if (rc0 != VS_OK) return rc0;
+    const uint32_t maxl = vsk::gemv_max_lists(dim, bf16, (uint32_t)c.rows, k);
+    if (eng->lists.bytes < (size_t)maxl * k * 8) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->lists.ensure((size_t)maxl * k * 8), "alloc list scratch");
+    }
+    const bool fused_merge = gemv_one() == 1;
+    uint32_t L = 0;
+    VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    VS_HIP(vsk::launch_gemv_one(
+               c.data, bf16, dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q, cosine, allow, k,
+               eng->lists.as<uint64_t>(), maxl,
+               fused_merge ? (uint32_t*)((char*)eng->small_part.p + kPartBytes + 4) : nullptr,
+               direct ? direct->keys : d_keys, eng->stream,
+               fused_merge && direct ? direct->flag : nullptr, direct ? direct->seq : 0, &L),
+           "gemv scan (one launch)");
+    VS_HIP(ev_end(eng, eng->scan_ev), "event");
+    if (!fused_merge) {  // the workgroup lists -> launch_merge (two launches)
+      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      VS_HIP(vsk::launch_merge(eng->lists.as<uint64_t>(), L, k, 0, 1, k, k,
+                               direct ? direct->keys : d_keys, eng->stream,
+                               direct ? direct->flag : nullptr, direct ? direct->seq : 0),
+             "merge");
+      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+    }
+    if (direct) direct->used = true;
+    return VS_OK;
+  }
   // the bf16 MFMA path reads a bf16 copy, 256 queries per pass (rows past nq
   // are padding: finite, and masked by the kernels)
   uint16_t* qb = nullptr;
@@ -1056,6 +1098,18 @@ bool direct_completion() {
   static const bool v = [] {
     const char* e = std::getenv("VS_DIRECT_COMPLETION");
     return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// One-query GEMV searches with the query prep fused into the scan
+// (VS_GEMV_ONE, read once): 2 (default) = prep + scan in one launch, then
+// the merge; 1 = the merge too, by the last workgroup; 0 = prep, scan and
+// merge as three launches.
+int gemv_one() {
+  static const int v = [] {
+    const char* e = std::getenv("VS_GEMV_ONE");
+    return e ? std::atoi(e) : 2;
   }();
   return v;
 }

@@ -403,11 +403,53 @@ hipError_t launch_round_bf16(const float* in, uint64_t n, float* out, hipStream_
   return hipGetLastError();
 }
 
+// merge of sorted key lists (merge_query, defined with merge_keys_kernel
+// below; the one-launch GEMV's last workgroup runs it too)
+constexpr int kMergeThreads = 512;
+constexpr int kMergeCap = 4096;
+constexpr int kMergeHeld = 16;  // fast path: keys per thread held in registers
+__device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, uint32_t L,
+                                            uint64_t lstride, uint64_t qstride, uint32_t kin,
+                                            uint32_t k, uint32_t q, uint64_t* __restrict__ out,
+                                            uint64_t* buf, uint64_t* red, uint32_t& cnt,
+                                            bool tourney);
+
 // ---------------------------------------------------------------------------
 // single-query scan (GEMV) + per-wave top-k
 // ---------------------------------------------------------------------------
 constexpr int kGemvThreads = 512;
 constexpr int kGemvWaves = kGemvThreads / 64;
+static_assert(kGemvThreads == kMergeThreads, "the one-launch GEMV merges in its last workgroup");
+
+// Wave 0's query preprocessing into LDS, as query_prep_kernel does it (the
+// same fp64 norm in the same order, so the same bits): prep bit 0 = cosine
+// normalise, bit 1 = round to bf16 values. The caller syncs.
+template <int D>
+__device__ __forceinline__ void prep_query_wave(const float* __restrict__ q, int prep, float* qs,
+                                                int lane) {
+  constexpr int PJ = D / 64;
+  float v[PJ];
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) v[j] = q[lane + 64 * j];
+  bool keep = true;
+  double nrm = 1.0;
+  if (prep & 1) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const double t = (double)v[j];
+      s = s + t * t;
+    }
+    s = wave_sum_f64(s);
+    keep = vs::cosine_keep(s);
+    nrm = sqrt(s);
+  }
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const float y = keep ? v[j] : (float)((double)v[j] / nrm);
+    qs[lane + 64 * j] = (prep & 2) ? vs::bf16_to_f32(vs::f32_to_bf16(y)) : y;
+  }
+}
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 // non-temporal loads: 75.5% -> 81-86% of 8 TB/s on 10M x 768 bf16 and
@@ -527,12 +569,70 @@ __device__ __forceinline__ void gemv_emit(WaveList<KPL>& L, uint64_t theta, uint
 // score leaves as its order-preserving 32-bit image (the key's high word, 0
 // for a masked row) in sc[row], and the top 11 bits of each unmasked image
 // are counted into hist[2048] (the first digit of the radix select).
-template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar>
+// After a workgroup's stores to mapped host memory: every storing wave drains
+// them, the workgroup meets, one lane releases at system scope and stores
+// `seq` to *flag (the host spins on it, then reads the stores).
+__device__ __forceinline__ void publish_host(uint64_t* flag, uint64_t seq) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ONE (r03, one query, KPL <= 2, no gather): `q` is the RAW query, which
+// wave 0 of every workgroup preprocesses into LDS (prep bits as
+// query_prep_kernel), `out` receives the per-workgroup lists, and the last
+// workgroup to finish (an agent-scope counter) merges them with merge_query
+// into `dst` -- then, with `flag`, publishes `seq` there for the host. One
+// launch instead of query prep + scan + merge.
+template <int KPL>
+__device__ __forceinline__ void gemv_one_finish(const uint64_t* lists, uint32_t k,
+                                                uint32_t* counter, uint64_t* dst,
+                                                uint64_t* flag, uint64_t seq) {
+  __shared__ uint64_t buf[kMergeCap];
+  __shared__ uint64_t red[kMergeThreads / 64];
+  __shared__ uint32_t cnt;
+  __shared__ int last;
+  // hand-off (MI355X_MICROARCH.md, valid producer / consumer forms): every
+  // storing wave drains its list stores, the workgroup meets, ONE lane
+  // releases at agent scope and adds to the counter; the last adder acquires
+  // once, then the whole workgroup reads with plain loads. (A __threadfence()
+  // per thread -- an L2 write-back and an L1 invalidate per wave in every
+  // workgroup -- made a 20k-row search 3x slower.)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t prev =
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // the sample-bound path only (a constant: the tournament's registers would
+  // raise the scan's VGPR count)
+  merge_query(lists, gridDim.x, k, 0, k, k, 0, dst, buf, red, cnt, false);
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (flag) publish_host(flag, seq);
+}
+
+template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar, bool ONE = false>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
     uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr) {
+    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr,
+    int prep = 0, uint32_t* counter = nullptr, uint64_t* dst = nullptr, uint64_t* flag = nullptr,
+    uint64_t seq = 0) {
+  static_assert(!ONE || (KPL >= 1 && KPL <= 2 && !GATHER), "one-launch: list scans, no gather");
   using S = GemvShape<D, BF16>;
   constexpr bool kScores = KPL == 0;
   __shared__ uint32_t lhist[kScores ? kRselBins : 1];
@@ -559,13 +659,20 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   int rowsel[S::J];
   int coff[S::J];  // chunk index within its row
   float qv[S::J][S::EPC];
+  const float* qsrc = q;
+  if constexpr (ONE) {
+    __shared__ float qs[D];
+    if (w == 0) prep_query_wave<D>(q, prep, qs, lane);
+    __syncthreads();
+    qsrc = qs;
+  }
 #pragma unroll
   for (int j = 0; j < S::J; ++j) {
     const int c = lane + 64 * j;
     rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
     coff[j] = c % S::CPR;
 #pragma unroll
-    for (int e = 0; e < S::EPC; ++e) qv[j][e] = q[coff[j] * S::EPC + e];
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qsrc[coff[j] * S::EPC + e];
   }
 
   WaveList<kScores ? 1 : KPL> L;
@@ -678,6 +785,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
       if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
   } else {
     gemv_emit<KPL>(L, theta, k, lane, w, out);
+    if constexpr (ONE) {
+      if (counter) gemv_one_finish<KPL>(out, k, counter, dst, flag, seq);
+    }
   }
 }
 
@@ -830,6 +940,61 @@ static hipError_t gemv_dispatch_kpl(const void* X, uint32_t n_rows, uint32_t row
     gemv_launch_kpl<D, BF16, false>(kpl, grid, block, st, X, n_rows, row_base, q, allow, k,
                                     g.rows_per_wave, out, nullptr);
   return hipGetLastError();
+}
+
+template <int D, bool BF16>
+static hipError_t gemv_one_d(const void* X, uint32_t n_rows, uint32_t row_base, const float* q_raw,
+                             int prep, const uint64_t* allow, uint32_t k, uint64_t* lists,
+                             uint32_t max_lists, uint32_t* counter, uint64_t* dst, uint64_t* flag,
+                             uint64_t seq, hipStream_t st, uint32_t* nlists) {
+  using S = GemvShape<D, BF16>;
+  const GemvGrid g = gemv_grid(n_rows, S::RB);
+  if (g.nwg > max_lists) return hipErrorInvalidValue;
+  if (nlists) *nlists = g.nwg;
+  if (gemv_kpl(k) == 1)
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1, false, kGemvVar, true>), dim3(g.nwg),
+                       dim3(kGemvThreads), 0, st, X, n_rows, row_base, q_raw, allow, k,
+                       g.rows_per_wave, lists, nullptr, nullptr, prep, counter, dst, flag, seq);
+  else
+    hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 2, false, kGemvVar, true>), dim3(g.nwg),
+                       dim3(kGemvThreads), 0, st, X, n_rows, row_base, q_raw, allow, k,
+                       g.rows_per_wave, lists, nullptr, nullptr, prep, counter, dst, flag, seq);
+  return hipGetLastError();
+}
+
+bool gemv_one_ok(uint32_t dim, uint32_t k) {
+  if (k == 0 || k > 128) return false;
+  switch (dim) {
+    case 128: case 256: case 384: case 512: case 768: case 1024: case 1536: return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
+                           uint32_t row_base, const float* q_raw, bool cosine,
+                           const uint64_t* allow, uint32_t k, uint64_t* lists, uint32_t max_lists,
+                           uint32_t* counter, uint64_t* dst, hipStream_t st, uint64_t* flag,
+                           uint64_t seq, uint32_t* nlists) {
+  if (!gemv_one_ok(dim, k) || n_rows == 0 || (counter && !dst)) return hipErrorInvalidValue;
+  const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
+#define VS_ONE_CASE(DD)                                                                      \
+  case DD:                                                                                   \
+    return bf16 ? gemv_one_d<DD, true>(X, n_rows, row_base, q_raw, prep, allow, k, lists,    \
+                                       max_lists, counter, dst, flag, seq, st, nlists)       \
+                : gemv_one_d<DD, false>(X, n_rows, row_base, q_raw, prep, allow, k, lists,   \
+                                        max_lists, counter, dst, flag, seq, st, nlists);
+  switch (dim) {
+    VS_ONE_CASE(128)
+    VS_ONE_CASE(256)
+    VS_ONE_CASE(384)
+    VS_ONE_CASE(512)
+    VS_ONE_CASE(768)
+    VS_ONE_CASE(1024)
+    VS_ONE_CASE(1536)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef VS_ONE_CASE
 }
 
 template <bool BF16, bool GATHER>
@@ -1027,30 +1192,7 @@ __device__ __forceinline__ void gemv_small_body(
   };
   if (gfirst < n_groups) load_step(gfirst);
   __shared__ float qs[D];
-  if (w == 0) {
-    constexpr int PJ = D / 64;
-    float v[PJ];
-#pragma unroll
-    for (int j = 0; j < PJ; ++j) v[j] = q[lane + 64 * j];
-    bool keep = true;
-    double nrm = 1.0;
-    if (prep & 1) {
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < PJ; ++j) {
-        const double t = (double)v[j];
-        s = s + t * t;
-      }
-      s = wave_sum_f64(s);
-      keep = vs::cosine_keep(s);
-      nrm = sqrt(s);
-    }
-#pragma unroll
-    for (int j = 0; j < PJ; ++j) {
-      const float y = keep ? v[j] : (float)((double)v[j] / nrm);
-      qs[lane + 64 * j] = (prep & 2) ? vs::bf16_to_f32(vs::f32_to_bf16(y)) : y;
-    }
-  }
+  if (w == 0) prep_query_wave<D>(q, prep, qs, lane);
   __syncthreads();
   float qv[S::J][S::EPC];
 #pragma unroll
@@ -2782,10 +2924,6 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // candidates are streamed in chunks; survivors are appended to an LDS buffer
 // that also holds the running top-k, which is re-sorted (bitonic) only when a
 // chunk added something. Correct for any input; fast when the bound is good.
-constexpr int kMergeThreads = 512;
-constexpr int kMergeCap = 4096;
-constexpr int kMergeHeld = 16;  // fast path: keys per thread held in registers
-
 __device__ __forceinline__ void bitonic_sort_desc(uint64_t* buf, int n_pow2) {
   for (int size = 2; size <= n_pow2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -2830,6 +2968,94 @@ __device__ __forceinline__ uint32_t dedupe_sorted(uint64_t* buf, uint32_t c, uin
   return cnt_sh;
 }
 
+// A key of buf[0, ns) with at least k sampled keys at or above it: for
+// ns <= 256 the smallest with at most k - 1 above it (by rank), through nz the
+// non-zero sampled keys; past 256 the k-th distinct key after a sort, nz the
+// distinct ones. ~0 if none. ns <= kMergeThreads, red holds kMergeThreads / 64
+// words. Ends with buf free for reuse.
+__device__ __forceinline__ uint64_t sample_kth(uint64_t* buf, uint32_t ns, uint32_t k,
+                                               uint64_t* red, uint32_t& nz) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (ns > 256) {
+    // ranking every key against all ns is LDS-bandwidth bound past a few
+    // hundred keys (each broadcast read still returns a KiB per wave): sort
+    // instead, then the k-th distinct key (exactly k distinct keys >= it)
+    int p2 = 1;
+    while ((uint32_t)p2 < ns) p2 <<= 1;
+    for (uint32_t i = ns + threadIdx.x; i < (uint32_t)p2; i += kMergeThreads) buf[i] = 0;
+    __syncthreads();
+    bitonic_sort_desc(buf, p2);
+    __shared__ uint32_t u_sh;
+    const uint32_t u = dedupe_sorted(buf, ns, u_sh);
+    nz = u;
+    const uint64_t sb = u >= k ? buf[k - 1] : ~0ull;
+    __syncthreads();  // buf reads done
+    return sb;
+  }
+  const uint64_t x = threadIdx.x < ns ? buf[threadIdx.x] : 0ull;
+  uint64_t cand = ~0ull;
+  uint32_t nzc = x != 0 ? 1u : 0u;
+  if (x != 0) {
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < ns; ++j) r += buf[j] > x ? 1u : 0u;
+    if (r < k) cand = x;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t y = __shfl_xor(cand, o, 64);
+    cand = y < cand ? y : cand;
+    nzc += __shfl_xor(nzc, o, 64);
+  }
+  __syncthreads();  // buf reads done
+  if (lane == 0) {
+    red[w] = cand;
+    buf[w] = nzc;
+  }
+  __syncthreads();
+  uint64_t sb = ~0ull;
+  nz = 0;
+  for (int i = 0; i < kMergeThreads / 64; ++i) {
+    sb = red[i] < sb ? red[i] : sb;
+    nz += (uint32_t)buf[i];
+  }
+  __syncthreads();  // red / buf reads done
+  return sb;
+}
+
+// The c survivors buf[0, c) (every key at or above a sample bound) -> the
+// top k of their distinct keys in out[0, k): by rank when c <= 512 (a
+// repeated key counts at its first position only), else bitonic sort +
+// dedupe. False (nothing written) when they hold fewer than k distinct keys
+// or c > kMergeCap. cnt_sh: shared scratch.
+__device__ __forceinline__ bool place_survivors(uint64_t* buf, uint32_t c, uint32_t k,
+                                                uint64_t* __restrict__ out, uint32_t& cnt_sh) {
+  if (c <= 64) {  // rank is O(c^2) LDS broadcast reads: a sort past a few dozen
+    const uint32_t t = threadIdx.x;
+    const uint64_t x = t < c ? buf[t] : 0ull;
+    bool first = x != 0;
+    for (uint32_t i = 0; first && i < t; ++i) first = buf[i] != x;
+    buf[kMergeThreads + t] = first ? x : 0ull;
+    const uint32_t u2 = (uint32_t)__syncthreads_count(first);
+    if (u2 < k) return false;
+    if (first) {
+      uint32_t rank = 0;
+      for (uint32_t i = 0; i < c; ++i) rank += buf[kMergeThreads + i] > x ? 1u : 0u;
+      if (rank < k) out[rank] = x;
+    }
+    return true;
+  }
+  if (c > (uint32_t)kMergeCap) return false;
+  int p3 = 1;
+  while ((uint32_t)p3 < c) p3 <<= 1;
+  for (uint32_t i = c + threadIdx.x; i < (uint32_t)p3; i += kMergeThreads) buf[i] = 0;
+  __syncthreads();
+  bitonic_sort_desc(buf, p3);
+  const uint32_t u2 = dedupe_sorted(buf, c, cnt_sh);
+  if (u2 < k) return false;
+  for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads) out[j] = buf[j];
+  return true;
+}
+
 // Top-k of query q over L lists (merge_keys_kernel; also select_slab_kernel's
 // overflow fallback). buf holds >= kMergeCap keys; red / cnt are the
 // caller's shared scratch. One workgroup of kMergeThreads threads.
@@ -2837,7 +3063,7 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
                                             uint64_t lstride, uint64_t qstride, uint32_t kin,
                                             uint32_t k, uint32_t q, uint64_t* __restrict__ out,
                                             uint64_t* buf, uint64_t* red, uint32_t& cnt,
-                                            bool tourney = true) {
+                                            bool tourney) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 
   // Fast path (single-query GEMV merges and shard merges at k <= 32): all
@@ -2879,9 +3105,8 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
     for (uint32_t r = nz + t; r < k; r += kMergeThreads) out[(size_t)q * k + r] = 0;
     return;
   }
-  // (r03: only for many lists and k <= 10 -- elsewhere the sample-bound path
-  // below is as fast or faster: one query at 2k rows, k = 32: 61.6 -> 34.7
-  // us; profiles/r03_merge_tourney_ab.jsonl)
+  // (r03: off unless VS_MERGE_TOURNEY=1 -- the sample-bound path below is
+  // faster; profiles/r03_merge_tourney_ab.jsonl, r03_merge_lat.jsonl)
   if (tourney && L >= 256 && k <= 10 && total0 <= (uint64_t)kMergeThreads * kMergeHeld) {
     uint64_t x[kMergeHeld];
     // every load issued unconditionally (clamped index), all in flight at
@@ -2959,50 +3184,77 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   // 758 lists of 100 at 200k rows). The sample (<= 512 keys: one per thread,
   // so a weaker bound for many lists) is ranked, not sorted, and so are the
   // survivors when they are <= 512: no sort on the common path.
-  uint64_t sthr = 0;
-  {
+  // Lists held in registers (the common single-query merge: one list per
+  // scan workgroup, L >= 2k / 4): each thread loads the first 4 entries of
+  // lists t and t + 512 at once, so the sample and the walk's first step are
+  // one memory round trip; only a list whose 4th key still passes the bound
+  // is read further.
+  if (L <= 2u * kMergeThreads && 4ull * L >= 2ull * k) {
+    const uint32_t m0 = (2 * k + L - 1) / L;
+    const uint32_t m = m0 < 1 ? 1 : (m0 > kin ? kin : (m0 > 4 ? 4 : m0));
+    uint64_t h[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const uint32_t l = threadIdx.x + (uint32_t)a * kMergeThreads;
+      const uint64_t* lp = lists + (size_t)(l < L ? l : 0) * lstride + q * qstride;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) h[a][v] = (l < L && (uint32_t)v < kin) ? lp[v] : 0ull;
+    }
+    const uint32_t cap = k * 8 < 128 ? 128 : (k * 8 > (uint32_t)kMergeThreads ? kMergeThreads : k * 8);
+    const uint32_t ns = L * m < cap ? L * m : cap;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const uint32_t l = threadIdx.x + (uint32_t)a * kMergeThreads;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if ((uint32_t)v < m && l * m + (uint32_t)v < ns) buf[l * m + v] = h[a][v];
+    }
+    __syncthreads();
+    uint32_t nz;
+    const uint64_t sb = sample_kth(buf, ns, k, red, nz);
+    if (nz >= k && sb != ~0ull) {
+      const uint64_t thr = sb - 1;
+      if (threadIdx.x == 0) cnt = 0;
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const uint32_t l = threadIdx.x + (uint32_t)a * kMergeThreads;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (h[a][v] > thr) {
+            const uint32_t at = atomicAdd(&cnt, 1u);
+            if (at < (uint32_t)kMergeCap) buf[at] = h[a][v];
+          }
+        if (l < L && h[a][3] > thr) {  // the rest of this list, one thread
+          const uint64_t* lp = lists + (size_t)l * lstride + q * qstride;
+          for (uint32_t j = 4; j < kin; ++j) {
+            const uint64_t x = lp[j];
+            if (x <= thr) break;
+            const uint32_t at = atomicAdd(&cnt, 1u);
+            if (at < (uint32_t)kMergeCap) buf[at] = x;
+          }
+        }
+      }
+      __syncthreads();
+      if (place_survivors(buf, cnt, k, out + (size_t)q * k, cnt)) return;
+    }
+  } else {
+    // Sample bound + list walk over global memory (few lists, or very many)
     constexpr uint32_t kSample = kMergeThreads;  // one sampled key per thread
     const uint32_t m0 = (2 * k + L - 1) / L;
     const uint32_t m = m0 < 1 ? 1 : (m0 > kin ? kin : m0);
     const uint64_t ns64 = (uint64_t)L * m;
     const uint32_t ns = ns64 < (uint64_t)kSample ? (uint32_t)ns64 : kSample;
-    uint64_t x = 0;
+    (void)ns64;
     if (threadIdx.x < ns) {
       const uint32_t l = threadIdx.x / m, j = threadIdx.x - l * m;
-      x = lists[l * lstride + q * qstride + j];
-    }
-    buf[threadIdx.x] = x;
-    __syncthreads();
-    // the smallest sampled key with at most k - 1 sampled keys above it (the
-    // sample's k-th largest); none if fewer than k sampled keys are non-zero
-    uint64_t cand = ~0ull;
-    uint32_t nzc = x != 0 ? 1u : 0u;
-    if (x != 0) {
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < ns; ++j) r += buf[j] > x ? 1u : 0u;
-      if (r < k) cand = x;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const uint64_t y = __shfl_xor(cand, o, 64);
-      cand = y < cand ? y : cand;
-      nzc += __shfl_xor(nzc, o, 64);
-    }
-    __syncthreads();  // buf reads done
-    if (lane == 0) {
-      red[w] = cand;
-      buf[w] = nzc;
+      buf[threadIdx.x] = lists[l * lstride + q * qstride + j];
     }
     __syncthreads();
-    uint64_t sb = ~0ull;
-    uint32_t nz = 0;
-    for (int i = 0; i < kMergeThreads / 64; ++i) {
-      sb = red[i] < sb ? red[i] : sb;
-      nz += (uint32_t)buf[i];
-    }
-    __syncthreads();  // red / buf reads done
+    uint32_t nz;
+    const uint64_t sb = sample_kth(buf, ns, k, red, nz);
     if (nz >= k && sb != ~0ull) {
-      sthr = sb - 1;  // survivors: keys >= sb
+      const uint64_t sthr = sb - 1;  // survivors: keys >= sb
       if (threadIdx.x == 0) cnt = 0;
       __syncthreads();
       // tpl threads per list (a power of two <= 64: lanes of one wave), each
@@ -3032,43 +3284,13 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
         }
       }
       __syncthreads();
-      const uint32_t c = cnt;
-      if (c <= (uint32_t)kMergeThreads) {
-        // rank placement, as the few-keys path above: a repeated key counts at
-        // its first position only
-        const uint32_t t = threadIdx.x;
-        const uint64_t x = t < c ? buf[t] : 0ull;
-        bool first = x != 0;
-        for (uint32_t i = 0; first && i < t; ++i) first = buf[i] != x;
-        buf[kMergeThreads + t] = first ? x : 0ull;
-        const uint32_t u2 = (uint32_t)__syncthreads_count(first);
-        if (u2 >= k) {
-          if (first) {
-            uint32_t rank = 0;
-            for (uint32_t i = 0; i < c; ++i) rank += buf[kMergeThreads + i] > x ? 1u : 0u;
-            if (rank < k) out[(size_t)q * k + rank] = x;
-          }
-          return;
-        }
-      } else if (c <= (uint32_t)kMergeCap) {
-        int p3 = 1;
-        while ((uint32_t)p3 < c) p3 <<= 1;
-        for (uint32_t i = c + threadIdx.x; i < (uint32_t)p3; i += kMergeThreads) buf[i] = 0;
-        __syncthreads();
-        bitonic_sort_desc(buf, p3);
-        const uint32_t u2 = dedupe_sorted(buf, c, cnt);
-        if (u2 >= k) {
-          for (uint32_t j = threadIdx.x; j < k; j += kMergeThreads) out[(size_t)q * k + j] = buf[j];
-          return;
-        }
-      }
-      // fewer than k distinct survivors (lists sharing keys inflated the
-      // sample's ranks), or more survivors than the buffer holds (whose
-      // distinct count is unknown): the filter below, without the sample bound
-      sthr = 0;
-      __syncthreads();
+      if (place_survivors(buf, cnt, k, out + (size_t)q * k, cnt)) return;
     }
   }
+  // fewer than k distinct survivors (lists sharing keys inflated the sample's
+  // ranks), or more survivors than the buffer holds (whose distinct count is
+  // unknown): the filter below, without the sample bound
+  __syncthreads();
 
   // initial bound (strict filter "key > thr")
   uint64_t b = 0;
@@ -3140,19 +3362,18 @@ __global__ __launch_bounds__(kMergeThreads) void merge_keys_kernel(
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t cnt;
   merge_query(lists, L, lstride, qstride, kin, k, blockIdx.x, out, buf, red, cnt, tourney != 0);
-  if (flag) {  // merge_query returns on block-uniform paths: every thread is here
-    __threadfence_system();  // this thread's key stores, host-visible
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (flag) publish_host(flag, seq);  // merge_query returns on block-uniform paths
 }
 
-// VS_MERGE_TOURNEY=0 (read once; ablation): k <= 32 merges of up to 8192
-// keys take the sample-bound path instead of the register tournament
+// VS_MERGE_TOURNEY=1 (read once; ablation) gives back the register
+// tournament for k <= 10 over >= 256 lists. Off by default since r03: the
+// sample-bound path with register-held list prefixes is faster at every shape
+// measured (one query, 768 lists x 10: 10.2 against 14.2 us;
+// profiles/r03_merge_lat.jsonl)
 static int merge_tourney() {
   static const int v = [] {
     const char* e = getenv("VS_MERGE_TOURNEY");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
   }();
   return v;
 }

@@ -631,3 +631,50 @@ def test_small_completion_concurrent(pkg, orc):
         for t in th:
             t.join()
         assert not errs, errs[:5]
+
+
+_GEMV_ONE = r"""
+import json, sys
+import torch                      # first: the library then binds torch's HIP runtime
+import numpy as np
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge
+pkg = ge.load_package()
+out = {}
+with pkg.VectorEngine(device=0) as eng:
+    for dim, dtype, metric, rows in ((768, 0, 0, 300), (768, 1, 1, 5000), (1024, 1, 0, 70000),
+                                     (128, 0, 1, 20000), (1536, 0, 0, 4000), (768, 0, 0, 200000)):
+        name = f"g{dim}_{dtype}_{metric}_{rows}"
+        eng.create_collection(name, dim, metric, dtype, 0, 1000)
+        eng.generate(name, rows, 77)
+        rng = np.random.default_rng(dim + rows)
+        Q = (rng.standard_normal((6, dim)) * 3).astype(np.float32)
+        allow = rng.random(rows) < 0.6
+        for k in (1, 10, 17, 64, 65, 100, 128):
+            for i in range(Q.shape[0]):
+                s, r, c = eng.search(name, Q[i:i + 1], k)
+                out[f"{name}/{k}/{i}"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+            s, r, c = eng.search_filtered(name, Q[:1], k, allow)
+            out[f"{name}/{k}/f"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+        eng.drop_collection(name)
+print(json.dumps(out))
+"""
+
+
+def test_gemv_one_launch_equals_three_launches(pkg):
+    """One query on the GEMV list path runs as ONE launch (every workgroup
+    preprocesses the raw query, the last one merges the workgroup lists) and,
+    through the host API, hands its keys over by the completion word. Its
+    answers must be bit-identical to query prep + scan + merge (VS_GEMV_ONE=0)
+    over dims 128..1536, both dtypes and metrics, 300..200k rows, k 1..128
+    (KPL 1 and 2), with a row_base and with a shipped filter bitmap."""
+    import os
+    base = _run_py(_GEMV_ONE)
+    os.environ["VS_GEMV_ONE"] = "0"
+    try:
+        other = _run_py(_GEMV_ONE)
+    finally:
+        os.environ.pop("VS_GEMV_ONE", None)
+    assert base.keys() == other.keys()
+    bad = [key for key in base if base[key] != other[key]]
+    assert not bad, bad[:5]
