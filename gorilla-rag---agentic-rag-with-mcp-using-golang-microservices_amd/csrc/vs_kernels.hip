@@ -3080,7 +3080,9 @@ __device__ __forceinline__ void merge_query(const uint64_t* __restrict__ lists, 
   // thread, and each key's output slot is its rank, the number of keys above
   // it among the distinct keys (a loop of LDS broadcast reads; 0 = empty). No
   // shuffle rounds: P = 8, k = 10 was 10 + 10 dependent wave-max rounds.
-  if (total0 <= (uint64_t)kMergeThreads) {
+  // (r03: up to 128 keys -- the rank loops are O(keys^2) LDS broadcast reads,
+  // 448 keys took ~10 us more than the sample-bound path below)
+  if (total0 <= 128) {
     const uint32_t t = threadIdx.x, tot = (uint32_t)total0;
     uint64_t x = 0;
     if (t < tot) {
