@@ -133,7 +133,7 @@ hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_
 // `counter`: one u32, zero between launches (the kernel leaves it zero), of
 // this stream only; NULL = no merge (the lists are left for launch_merge). With `flag` (dst and flag mapped pinned host memory)
 // `seq` is stored to *flag once dst is host-visible. gemv_one_ok: the GEMV
-// table's dims up to 1536 and k <= 128 (register lists merged per workgroup).
+// table's dims up to 1024 and k <= 128 (register lists merged per workgroup).
 bool gemv_one_ok(uint32_t dim, uint32_t k);
 hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_rows,
                            uint32_t row_base, const float* q_raw, bool cosine,

@@ -658,21 +658,11 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
 
   int rowsel[S::J];
   int coff[S::J];  // chunk index within its row
-  float qv[S::J][S::EPC];
-  const float* qsrc = q;
-  if constexpr (ONE) {
-    __shared__ float qs[D];
-    if (w == 0) prep_query_wave<D>(q, prep, qs, lane);
-    __syncthreads();
-    qsrc = qs;
-  }
 #pragma unroll
   for (int j = 0; j < S::J; ++j) {
     const int c = lane + 64 * j;
     rowsel[j] = (S::RB == 1) ? 0 : c / S::CPR;
     coff[j] = c % S::CPR;
-#pragma unroll
-    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qsrc[coff[j] * S::EPC + e];
   }
 
   WaveList<kScores ? 1 : KPL> L;
@@ -692,44 +682,67 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   };
   (void)flush_scores;
 
-  if (lo < hi) {
-    constexpr bool kNT = (VAR & 1) != 0, kDpp = (VAR & 2) != 0;
-    constexpr int DEPTH = (VAR & 4) ? 2 : 1;
-    uint4 buf[DEPTH + 1][S::J];
-    uint32_t ixn[S::J];  // GATHER: rows of the next position to load
-    auto fetch_ix = [&](uint32_t r0) {
+  constexpr bool kNT = (VAR & 1) != 0, kDpp = (VAR & 2) != 0;
+  constexpr int DEPTH = (VAR & 4) ? 2 : 1;
+  uint4 buf[DEPTH + 1][S::J];
+  uint32_t ixn[S::J];  // GATHER: rows of the next position to load
+  auto fetch_ix = [&](uint32_t r0) {
 #pragma unroll
-      for (int j = 0; j < S::J; ++j) {
-        const uint32_t pos = r0 + rowsel[j];
-        ixn[j] = rows[pos < hi ? pos : hi - 1];
-      }
-    };
-    auto load = [&](uint4* dst, uint32_t r0) {
-#pragma unroll
-      for (int j = 0; j < S::J; ++j) {
-        uint32_t row;
-        if constexpr (GATHER) {
-          row = ixn[j];
-        } else {
-          row = r0 + rowsel[j];
-          row = row < hi ? row : hi - 1;
-        }
-        const char* p = X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16;
-        if constexpr (kNT) {
-          const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
-          dst[j] = uint4{v[0], v[1], v[2], v[3]};
-        } else {
-          dst[j] = *(const uint4*)p;
-        }
-      }
-    };
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const uint32_t r0 = lo + d * stride;
-      if constexpr (GATHER) fetch_ix(r0 < hi ? r0 : lo);
-      load(buf[d], r0 < hi ? r0 : lo);
+    for (int j = 0; j < S::J; ++j) {
+      const uint32_t pos = r0 + rowsel[j];
+      ixn[j] = rows[pos < hi ? pos : hi - 1];
     }
-    if constexpr (GATHER) fetch_ix(lo + DEPTH * stride);
+  };
+  auto load = [&](uint4* dst, uint32_t r0) {
+#pragma unroll
+    for (int j = 0; j < S::J; ++j) {
+      uint32_t row;
+      if constexpr (GATHER) {
+        row = ixn[j];
+      } else {
+        row = r0 + rowsel[j];
+        row = row < hi ? row : hi - 1;
+      }
+      const char* p = X + (size_t)row * S::RBYTES + (size_t)coff[j] * 16;
+      if constexpr (kNT) {
+        const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+        dst[j] = uint4{v[0], v[1], v[2], v[3]};
+      } else {
+        dst[j] = *(const uint4*)p;
+      }
+    }
+  };
+  // the first rows' loads go out before the query is read (r03: in the
+  // one-launch form, before wave 0's query preprocessing and its barrier),
+  // except where holding them across the preprocessing would take the
+  // one-launch kernel past 80 VGPRs (3 workgroups per CU): 4 chunks per lane
+  auto prologue = [&]() {
+    if (lo < hi) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        const uint32_t r0 = lo + d * stride;
+        if constexpr (GATHER) fetch_ix(r0 < hi ? r0 : lo);
+        load(buf[d], r0 < hi ? r0 : lo);
+      }
+      if constexpr (GATHER) fetch_ix(lo + DEPTH * stride);
+    }
+  };
+  constexpr bool kEarly = !ONE || S::J <= 3;
+  if constexpr (kEarly) prologue();
+  float qv[S::J][S::EPC];
+  const float* qsrc = q;
+  if constexpr (ONE) {
+    __shared__ float qs[D];
+    if (w == 0) prep_query_wave<D>(q, prep, qs, lane);
+    __syncthreads();
+    qsrc = qs;
+  }
+#pragma unroll
+  for (int j = 0; j < S::J; ++j)
+#pragma unroll
+    for (int e = 0; e < S::EPC; ++e) qv[j][e] = qsrc[coff[j] * S::EPC + e];
+  if constexpr (!kEarly) prologue();
+  if (lo < hi) {
     for (uint32_t r = lo; r < hi; r += stride) {
       const uint32_t rn = r + DEPTH * stride;
       load(buf[DEPTH], rn < hi ? rn : r);
@@ -964,8 +977,10 @@ static hipError_t gemv_one_d(const void* X, uint32_t n_rows, uint32_t row_base, 
 
 bool gemv_one_ok(uint32_t dim, uint32_t k) {
   if (k == 0 || k > 128) return false;
+  // not 1536: the wave-0 preprocessing of 24 values per lane takes that scan
+  // to 88-106 VGPRs (63-85 without it), below 3 workgroups per CU
   switch (dim) {
-    case 128: case 256: case 384: case 512: case 768: case 1024: case 1536: return true;
+    case 128: case 256: case 384: case 512: case 768: case 1024: return true;
     default: return false;
   }
 }
@@ -990,7 +1005,6 @@ hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_ro
     VS_ONE_CASE(512)
     VS_ONE_CASE(768)
     VS_ONE_CASE(1024)
-    VS_ONE_CASE(1536)
     default:
       return hipErrorInvalidValue;
   }

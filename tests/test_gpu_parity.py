@@ -666,7 +666,8 @@ def test_gemv_one_launch_equals_three_launches(pkg):
     preprocesses the raw query, the last one merges the workgroup lists) and,
     through the host API, hands its keys over by the completion word. Its
     answers must be bit-identical to query prep + scan + merge (VS_GEMV_ONE=0)
-    over dims 128..1536, both dtypes and metrics, 300..200k rows, k 1..128
+    over dims 128..1024 (1536: the three launches in both runs), both dtypes and
+    metrics, 300..200k rows, k 1..128
     (KPL 1 and 2), with a row_base and with a shipped filter bitmap."""
     import os
     base = _run_py(_GEMV_ONE)
