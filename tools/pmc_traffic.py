@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCAN = {"c3": "mfma_topk_kernel<768, 0,", "c3b1": "gemv_topk_kernel<768, true, 1",
         "c2": "gemv_topk_kernel<768, false, 1", "c4": "mfma_topk_kernel<768, 0,",
-        "c4b1": "gemv_topk_kernel<768, true, 16", "c5b256": "mfma_topk_kernel<1024, 0,"}
+        "c4b1": "gemv_topk_kernel<768, true, 2", "c5b256": "mfma_topk_kernel<1024, 0,"}
 
 
 def main():
