@@ -107,8 +107,16 @@ struct HostSlot {
     if (done) (void)hipEventDestroy(done);
     if (mapped) (void)hipHostFree(mapped);
   }
+  size_t mapped_words = 0;
+  // grows the mapped completion buffer (the slot is idle); zero-filled, so a
+  // fresh word never equals a sequence number (they start at 1)
   hipError_t ensure_mapped(size_t words) {
-    if (mapped) return hipSuccess;
+    if (mapped && words <= mapped_words) return hipSuccess;
+    if (mapped) {
+      (void)hipHostFree(mapped);
+      mapped = mapped_dev = nullptr;
+      mapped_words = 0;
+    }
     void* p = nullptr;
     const hipError_t e = hipHostMalloc(&p, words * 8, hipHostMallocCoherent | hipHostMallocMapped);
     if (e != hipSuccess) return e;
@@ -121,6 +129,7 @@ struct HostSlot {
     }
     mapped = (uint64_t*)p;
     mapped_dev = (uint64_t*)d;
+    mapped_words = words;
     return hipSuccess;
   }
   // grows the pinned buffers (the slot is idle: nothing in flight uses them)
