@@ -203,6 +203,7 @@ struct DevEngine {
   // zeroed between uses), select state, the selected keys, sort scratch;
   // large merges (vs_merge_keys / shard merges at k > kMaxK)
   DevBuf lk_sc, lk_hist, lk_state, lk_sel, lk_sort, merge_big;
+  DevBuf lk_cand, lk_ctr;  // fused selection: boundary-bucket keys, 3 counters
   // small-collection search spread over workgroups: their keys + the
   // completion counter (zeroed at allocation; each launch leaves it zero)
   DevBuf small_part;

@@ -333,6 +333,16 @@ int search_gemv(DevEngine* eng, Collection& c, float* qp, uint32_t q0, uint32_t 
 // took 3.30 / 4.15 / 8.12 ms at k = 129 / 256 / 1024 on the list path
 // against 2.63-2.66 ms for any k on the large-k path (2.34-2.49 ms for the
 // list path at k <= 128; profiles/r03_large_k_threshold.jsonl).
+// The large-k selection in two launches (on unless VS_RSEL_FUSED=0; read
+// once): rsel_f1/f2 instead of the 12-launch digit chain.
+bool rsel_fused() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_RSEL_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 uint32_t large_k_from() {
   static const uint32_t v = [] {
     const char* e = std::getenv("VS_LARGE_K_FROM");
@@ -363,6 +373,15 @@ int search_large_k(DevEngine* eng, Collection& c, const float* qp, uint32_t nq, 
     VS_HIP(eng->lk_sel.ensure((size_t)keff * 8), "alloc selected keys");
     VS_HIP(eng->lk_sort.ensure(sort_bytes), "alloc sort scratch");
   }
+  const bool fused = rsel_fused();
+  constexpr size_t kCtrBytes = 16 + vsk::kRselBins * 4;  // 3 counters (+pad), hist1
+  if (fused && (eng->lk_cand.bytes < (size_t)n_rows * 8 || eng->lk_ctr.bytes < kCtrBytes)) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    VS_HIP(eng->lk_cand.ensure((size_t)n_rows * 8), "alloc boundary-bucket keys");
+    const bool fresh = eng->lk_ctr.bytes < kCtrBytes;
+    VS_HIP(eng->lk_ctr.ensure(kCtrBytes), "alloc select counters");
+    if (fresh) VS_HIP(hipMemsetAsync(eng->lk_ctr.p, 0, kCtrBytes, eng->stream), "zero");
+  }
   uint32_t* sc = eng->lk_sc.as<uint32_t>();
   uint32_t* hist = eng->lk_hist.as<uint32_t>();
   for (uint32_t i = 0; i < nq; ++i) {
@@ -372,10 +391,17 @@ int search_large_k(DevEngine* eng, Collection& c, const float* qp, uint32_t nq, 
            "score pass");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-    VS_HIP(vsk::launch_rsel(sc, n_rows, (uint32_t)c.row_base, keff, hist,
-                            eng->lk_state.as<vsk::RselState>(), eng->lk_sel.as<uint64_t>(),
-                            eng->stream),
-           "radix select");
+    if (fused)
+      VS_HIP(vsk::launch_rsel_fused(sc, n_rows, (uint32_t)c.row_base, keff, hist,
+                                    (uint32_t*)((char*)eng->lk_ctr.p + 16),
+                                    eng->lk_ctr.as<uint32_t>(), eng->lk_sel.as<uint64_t>(),
+                                    eng->lk_cand.as<uint64_t>(), eng->stream),
+             "radix select (two launches)");
+    else
+      VS_HIP(vsk::launch_rsel(sc, n_rows, (uint32_t)c.row_base, keff, hist,
+                              eng->lk_state.as<vsk::RselState>(), eng->lk_sel.as<uint64_t>(),
+                              eng->stream),
+             "radix select");
     VS_HIP(vsk::launch_sort_keys_desc(eng->lk_sel.as<uint64_t>(), d_keys + (size_t)i * k, keff,
                                       eng->lk_sort.p, eng->lk_sort.bytes, eng->stream),
            "sort selected keys");

@@ -40,6 +40,12 @@ hipError_t launch_gemv_scores(const void* X, bool bf16, uint32_t dim, uint32_t n
                               hipStream_t st);
 // hist (kRselBins u32, the first digit's counts from launch_gemv_scores) is
 // left zeroed; `keff` = min(k, unmasked rows) keys land in sel (unordered).
+// The same selection in two launches (r03): hist1 = kRselBins u32 and ctr =
+// 3 u32 (zero between calls, left zero), cand = n_rows keys of scratch; keff
+// keys land in sel (unordered), hist is left zeroed.
+hipError_t launch_rsel_fused(const uint32_t* sc, uint32_t n_rows, uint32_t row_base,
+                             uint32_t keff, uint32_t* hist, uint32_t* hist1, uint32_t* ctr,
+                             uint64_t* sel, uint64_t* cand, hipStream_t st);
 hipError_t launch_rsel(const uint32_t* sc, uint32_t n_rows, uint32_t row_base, uint32_t keff,
                        uint32_t* hist, RselState* state, uint64_t* sel, hipStream_t st);
 // Descending sort of n 64-bit keys (rocPRIM radix sort); temp / temp_bytes

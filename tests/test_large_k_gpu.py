@@ -223,3 +223,56 @@ def test_search_handler_large_top_k(pkg, orc, n):
     finally:
         s.close()
         eng.close()
+
+
+_RSEL_AB = r"""
+import json, sys
+import torch                      # first: the library then binds torch's HIP runtime
+import numpy as np
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+out = {}
+with pkg.VectorEngine(device=0) as eng:
+    eng.create_collection("r", 768, 1, 1, 0, 5)
+    eng.generate("r", 200_000, orc.SEED_CORPUS)
+    Q = orc.generate(orc.SEED_QUERY, 0, 3, 768)
+    for k in (129, 4000, 5000, 50_000):
+        s, r, c = eng.search("r", Q, k)
+        out[f"r/{k}"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+    # identical rows: the boundary bucket holds thousands of equal scores
+    base = orc.generate(11, 0, 5, 256)
+    V = base[np.arange(30_000) % 5]
+    eng.create_collection("t", 256, 1, 0, 0, 9)
+    eng.upsert("t", np.arange(V.shape[0]), V)
+    for k in (3000, 12_345, 29_999):
+        s, r, c = eng.search("t", base[:2] + 0.001, k)
+        out[f"t/{k}"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+print(json.dumps(out))
+"""
+
+
+def test_fused_selection_equals_digit_chain():
+    """The one-launch selection (rsel_fused_kernel: first digit from the score
+    pass's histogram, one compaction pass, the last workgroup finishing the
+    boundary bucket by an LDS sort or radix passes) must return the same bits
+    as the 12-launch digit chain (VS_RSEL_FUSED=0): random rows at k = 129 ..
+    50,000 and 30,000 rows of 5 repeated vectors (ties across the k-th key)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(env_extra):
+        env = dict(os.environ, **env_extra)
+        res = subprocess.run([sys.executable, "-c", f"ROOT={root!r}\n" + _RSEL_AB],
+                             capture_output=True, text=True, timeout=300, env=env)
+        assert res.returncode == 0, res.stderr[-3000:]
+        return json.loads(res.stdout.strip().splitlines()[-1])
+
+    a = run({})
+    b = run({"VS_RSEL_FUSED": "0"})
+    assert a.keys() == b.keys()
+    bad = [key for key in a if a[key] != b[key]]
+    assert not bad, bad
