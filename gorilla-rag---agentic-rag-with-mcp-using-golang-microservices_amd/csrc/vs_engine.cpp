@@ -516,10 +516,19 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 }
 
 int gemv_one();
+uint32_t large_k_from();
 
 bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered) {
   return nq == 1 && !filtered && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
          vsk::gemv_small_ok(c.dim, (uint32_t)c.rows, k);
+}
+
+// search_core's one-launch GEMV form takes this unfiltered search (and the
+// small path does not): its query may then travel in the kernel arguments
+bool gemv_one_path(const Collection& c, uint32_t nq, uint32_t k) {
+  return nq == 1 && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
+         !small_path(c, nq, k, false) && k < large_k_from() && gemv_one() == 2 &&
+         vsk::gemv_one_ok(c.dim, k);
 }
 
 // Core search on device data. d_q: nq x dim fp32 on this device, ordered on
@@ -611,7 +620,8 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                eng->lists.as<uint64_t>(), maxl,
                fused_merge ? (uint32_t*)((char*)eng->small_part.p + kPartBytes + 4) : nullptr,
                direct ? direct->keys : d_keys, eng->stream,
-               fused_merge && direct ? direct->flag : nullptr, direct ? direct->seq : 0, &L),
+               fused_merge && direct ? direct->flag : nullptr, direct ? direct->seq : 0, &L,
+               !fused_merge && direct ? direct->host_q : nullptr),
            "gemv scan (one launch)");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     if (!fused_merge) {  // the workgroup lists -> launch_merge (two launches)
@@ -1150,6 +1160,16 @@ bool query_args() {
   return v;
 }
 
+// The same for the one-launch GEMV form (VS_QUERY_ARGS_GEMV, read once;
+// default off until measured on the device).
+bool query_args_gemv() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_QUERY_ARGS_GEMV");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // A batched search of a large collection (the MFMA passes fill every CU for
 // milliseconds): such calls queue behind each other on the primary context,
 // so two of them never split the device and the batcher's pipelining (the
@@ -1225,7 +1245,8 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
   // word straight to the slot's mapped buffer; its query travels in the
   // kernel arguments (dim <= kGemvSmallArgDim: no H2D at all)
   const bool direct = nq == 1 && !abytes && !df && k <= vsk::kMaxK && direct_completion();
-  const bool qarg = direct && small_path(*c, nq, k, false) &&
+  const bool qarg = direct &&
+                    (small_path(*c, nq, k, false) || (query_args_gemv() && gemv_one_path(*c, nq, k))) &&
                     c->dim <= vsk::kGemvSmallArgDim && query_args();
   if (!qarg) std::memcpy(hs->in, queries, qbytes);
   // busy from the first enqueue that reads the slot: a failure after it

@@ -137,7 +137,9 @@ hipError_t launch_gemv_small(const void* X, bool bf16, uint32_t dim, uint32_t n_
 // entries of k keys), and the last workgroup merges them into dst[0, k) --
 // the same keys as query prep + launch_gemv + launch_merge, bit for bit.
 // `counter`: one u32, zero between launches (the kernel leaves it zero), of
-// this stream only; NULL = no merge (the lists are left for launch_merge). With `flag` (dst and flag mapped pinned host memory)
+// this stream only; NULL = no merge (the lists are left for launch_merge).
+// q_host (no merge, dim <= kGemvSmallArgDim): the raw query is read from host
+// memory at launch and travels in the kernel arguments (q_raw unused). With `flag` (dst and flag mapped pinned host memory)
 // `seq` is stored to *flag once dst is host-visible. gemv_one_ok: the GEMV
 // table's dims up to 1024 and k <= 128 (register lists merged per workgroup).
 bool gemv_one_ok(uint32_t dim, uint32_t k);
@@ -146,7 +148,7 @@ hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_ro
                            const uint64_t* allow, uint32_t k, uint64_t* lists, uint32_t max_lists,
                            uint32_t* counter, uint64_t* dst, hipStream_t st,
                            uint64_t* flag = nullptr, uint64_t seq = 0,
-                           uint32_t* nlists = nullptr);
+                           uint32_t* nlists = nullptr, const float* q_host = nullptr);
 
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);

@@ -624,14 +624,13 @@ __device__ __forceinline__ void gemv_one_finish(const uint64_t* lists, uint32_t 
   if (flag) publish_host(flag, seq);
 }
 
-template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar, bool ONE = false>
-__global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
+template <int D, bool BF16, int KPL, bool GATHER, int VAR, bool ONE>
+__device__ __forceinline__ void gemv_topk_body(
     const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
     const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
-    uint32_t rows_per_wave, uint64_t* __restrict__ out,
-    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr,
-    int prep = 0, uint32_t* counter = nullptr, uint64_t* dst = nullptr, uint64_t* flag = nullptr,
-    uint64_t seq = 0) {
+    uint32_t rows_per_wave, uint64_t* __restrict__ out, const uint32_t* __restrict__ rows,
+    uint32_t* __restrict__ hist, int prep, uint32_t* counter, uint64_t* dst, uint64_t* flag,
+    uint64_t seq) {
   static_assert(!ONE || (KPL >= 1 && KPL <= 2 && !GATHER), "one-launch: list scans, no gather");
   using S = GemvShape<D, BF16>;
   constexpr bool kScores = KPL == 0;
@@ -804,6 +803,37 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
   }
 }
 
+template <int D, bool BF16, int KPL, bool GATHER = false, int VAR = kGemvVar, bool ONE = false>
+__global__ __launch_bounds__(kGemvThreads) void gemv_topk_kernel(
+    const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
+    const float* __restrict__ q, const uint64_t* __restrict__ allow, uint32_t k,
+    uint32_t rows_per_wave, uint64_t* __restrict__ out,
+    const uint32_t* __restrict__ rows = nullptr, uint32_t* __restrict__ hist = nullptr,
+    int prep = 0, uint32_t* counter = nullptr, uint64_t* dst = nullptr, uint64_t* flag = nullptr,
+    uint64_t seq = 0) {
+  gemv_topk_body<D, BF16, KPL, GATHER, VAR, ONE>(Xv, n_rows, row_base, q, allow, k,
+                                                 rows_per_wave, out, rows, hist, prep, counter,
+                                                 dst, flag, seq);
+}
+
+// The raw query travels in the kernel's argument segment (r03): QueryArg is
+// the first argument, so the query starts at the segment pointer; no H2D.
+template <int D>
+struct QueryArg {
+  float v[D];
+};
+template <int D, bool BF16, int KPL>
+__global__ __launch_bounds__(kGemvThreads) void gemv_one_arg_kernel(
+    QueryArg<D> qa, const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base,
+    const uint64_t* __restrict__ allow, uint32_t k, uint32_t rows_per_wave,
+    uint64_t* __restrict__ out, int prep) {
+  const float* q = (const float*)(const __attribute__((address_space(4))) float*)
+      __builtin_amdgcn_kernarg_segment_ptr();
+  gemv_topk_body<D, BF16, KPL, false, kGemvVar, true>(Xv, n_rows, row_base, q, allow, k,
+                                                       rows_per_wave, out, nullptr, nullptr, prep,
+                                                       nullptr, nullptr, nullptr, 0);
+}
+
 // Any dimension: one row per wave step, lane-strided scalar loads.
 template <bool BF16, int KPL, bool GATHER = false>
 __global__ __launch_bounds__(kGemvThreads) void gemv_topk_generic_kernel(
@@ -959,11 +989,24 @@ template <int D, bool BF16>
 static hipError_t gemv_one_d(const void* X, uint32_t n_rows, uint32_t row_base, const float* q_raw,
                              int prep, const uint64_t* allow, uint32_t k, uint64_t* lists,
                              uint32_t max_lists, uint32_t* counter, uint64_t* dst, uint64_t* flag,
-                             uint64_t seq, hipStream_t st, uint32_t* nlists) {
+                             uint64_t seq, hipStream_t st, uint32_t* nlists, const float* q_host) {
   using S = GemvShape<D, BF16>;
   const GemvGrid g = gemv_grid(n_rows, S::RB);
   if (g.nwg > max_lists) return hipErrorInvalidValue;
   if (nlists) *nlists = g.nwg;
+  if constexpr (D <= (int)kGemvSmallArgDim) {
+    if (q_host) {  // no merge in the kernel (counter unused): the lists, then launch_merge
+      QueryArg<D> qa;
+      std::memcpy(qa.v, q_host, sizeof(qa.v));
+      if (gemv_kpl(k) == 1)
+        hipLaunchKernelGGL((gemv_one_arg_kernel<D, BF16, 1>), dim3(g.nwg), dim3(kGemvThreads), 0,
+                           st, qa, X, n_rows, row_base, allow, k, g.rows_per_wave, lists, prep);
+      else
+        hipLaunchKernelGGL((gemv_one_arg_kernel<D, BF16, 2>), dim3(g.nwg), dim3(kGemvThreads), 0,
+                           st, qa, X, n_rows, row_base, allow, k, g.rows_per_wave, lists, prep);
+      return hipGetLastError();
+    }
+  }
   if (gemv_kpl(k) == 1)
     hipLaunchKernelGGL((gemv_topk_kernel<D, BF16, 1, false, kGemvVar, true>), dim3(g.nwg),
                        dim3(kGemvThreads), 0, st, X, n_rows, row_base, q_raw, allow, k,
@@ -989,15 +1032,18 @@ hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_ro
                            uint32_t row_base, const float* q_raw, bool cosine,
                            const uint64_t* allow, uint32_t k, uint64_t* lists, uint32_t max_lists,
                            uint32_t* counter, uint64_t* dst, hipStream_t st, uint64_t* flag,
-                           uint64_t seq, uint32_t* nlists) {
+                           uint64_t seq, uint32_t* nlists, const float* q_host) {
   if (!gemv_one_ok(dim, k) || n_rows == 0 || (counter && !dst)) return hipErrorInvalidValue;
+  if (q_host && (counter || dim > kGemvSmallArgDim)) return hipErrorInvalidValue;
   const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
 #define VS_ONE_CASE(DD)                                                                      \
   case DD:                                                                                   \
     return bf16 ? gemv_one_d<DD, true>(X, n_rows, row_base, q_raw, prep, allow, k, lists,    \
-                                       max_lists, counter, dst, flag, seq, st, nlists)       \
+                                       max_lists, counter, dst, flag, seq, st, nlists,       \
+                                       q_host)                                               \
                 : gemv_one_d<DD, false>(X, n_rows, row_base, q_raw, prep, allow, k, lists,   \
-                                        max_lists, counter, dst, flag, seq, st, nlists);
+                                        max_lists, counter, dst, flag, seq, st, nlists,      \
+                                        q_host);
   switch (dim) {
     VS_ONE_CASE(128)
     VS_ONE_CASE(256)
@@ -1341,10 +1387,6 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_small_kernel(
 // The same search with the raw query in the kernel's argument segment (r03):
 // the dispatch carries it, so the call needs no H2D copy. QueryArg is the
 // first argument, so the query starts at the segment pointer.
-template <int D>
-struct QueryArg {
-  float v[D];
-};
 template <int D, bool BF16, int U>
 __global__ __launch_bounds__(kGemvThreads) void gemv_small_arg_kernel(
     QueryArg<D> qa, const void* __restrict__ Xv, uint32_t n_rows, uint32_t row_base, uint32_t k,
