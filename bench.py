@@ -138,7 +138,10 @@ def pmc_traffic(workload):
 
 
 def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_fn, row0):
-    """Times `steps` searches of one batch; returns (max elapsed s over ranks, scan/merge ms)."""
+    """Times `steps` searches of one batch; returns (max elapsed s over ranks,
+    scan/merge ms, every timed step's result tensor). The result tensors
+    rotate over at least `steps` buffers (shard.engine_callables ring), so
+    each step's answer is still intact after the timed region."""
     import torch.distributed as dist
 
     q = torch.empty((batch, dim), dtype=torch.float32, device="cuda")
@@ -151,9 +154,9 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = None
+    outs = []
     for _ in range(steps):
-        out = sharded.search(q, k)
+        outs.append(sharded.search(q, k))
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -164,7 +167,47 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     tm = eng.timing(reset=True)
-    return el, tm, out
+    return el, tm, outs
+
+
+def verify_steps(pkg, outs, k, n_rows):
+    """After the timed region: every timed step's answer is identical to the
+    first one (the same batch each step), full (min(k, rows) keys per query)
+    and sorted. Raises on any violation; returns the checked count."""
+    first = outs[0].cpu().numpy()
+    for i, o in enumerate(outs[1:], 1):
+        if not np.array_equal(o.cpu().numpy(), first):
+            raise AssertionError(f"timed step {i} returned a different answer than step 0")
+    s, r, c = pkg.keys_decode(first.view(np.uint64))
+    if int(c.min()) != min(k, n_rows):
+        raise AssertionError("incomplete result lists")
+    if not np.all(np.diff(s, axis=1) <= 0):
+        raise AssertionError("unsorted results")
+    return len(outs)
+
+
+def oracle_parity(pkg, cfg, n_full, keys, pick=(0, 85, 170, 255)):
+    """Part of the CPU-baseline leg (rank 0, N = 1): `pick` queries of the
+    timed batch checked against the streaming fp64 oracle over the whole
+    generated corpus (the north_star rule, oracle.check_topk). Test
+    infrastructure only: called after the timed region, never timed."""
+    from oracle import oracle
+
+    rows, dim, dtype, metric, batch, k, _ = cfg
+    bf16 = dtype == "bf16"
+    idx = [i for i in pick if i < keys.shape[0]]
+    Q = oracle.generate(oracle.SEED_QUERY, 0, keys.shape[0], dim)[idx]
+    Qp = oracle.preprocess(Q, metric == "cosine", bf16)
+    s, r, c = pkg.keys_decode(keys[idx])
+    t0 = time.perf_counter()
+    s64, rr, cc = oracle.search_generated(oracle.SEED_CORPUS, 0, n_full, Qp, k, bf16)
+    resc = oracle.rescore_generated(oracle.SEED_CORPUS, Qp, r, c, bf16)
+    bad = oracle.check_topk(s, r, c, s64, rr, cc, resc, score_rtol=1e-5)
+    return {"queries_checked": len(idx), "query_ids": idx, "violations": len(bad),
+            "first_violations": bad[:3], "rule": "north_star: ids exact except exact-score "
+            "near-ties < 1e-5 rel; scores within 1e-5 rel of the fp64 score",
+            "oracle": "oracle.search_generated (fp64, full corpus regenerated)",
+            "oracle_s": round(time.perf_counter() - t0, 2)}
 
 
 def cgroup_cpu_quota():
@@ -310,7 +353,9 @@ def main():
         f"{time.perf_counter() - t0:.2f}s on {torch.cuda.get_device_name(local)}")
 
     stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
-    ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True)
+    # every timed step keeps its own result buffer (checked after the timer)
+    ring = max(args.steps, 20, 1)
+    ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True, ring=ring)
     sharded = shard.ShardedSearch(ls, mg, always_gather=force_dist)
     # the data-path exchange: the engine's own RCCL communicator (all-gather +
     # merge on the search's stream) unless VS_COLLECTIVE=torch; gloo runs
@@ -338,14 +383,17 @@ def main():
             flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if int(flag.item()) == 1:
-                sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True)
+                sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True,
+                                                                 ring=ring)
                 sharded.world_size = world
             else:
                 log("[bench] torch.distributed exchange instead of the engine communicator")
                 collective = "torch"
 
-    el, tm, out = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
-                            stream_fn, 0)
+    el, tm, outs = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
+                             stream_fn, 0)
+    out = outs[-1]
+    steps_verified = verify_steps(pkg, outs, k, n_full)
     elem = 2 if dtype == "bf16" else 4
     bound = "mfma" if batch > 1 else "hbm"
     qpp = 256 if (dtype == "bf16" and dim <= 768) or (dtype == "f32" and dim <= 384) else 128
@@ -372,33 +420,35 @@ def main():
                    "rows_per_gpu": hi - lo, "collective": collective,
                    "build_id": pkg.build_id()},
         "roofline": roof,
+        "steps_verified": steps_verified,
     }
 
     # secondary: the single-query GEMV line on the same resident corpus
     if not args.no_secondary and batch > 1:
-        el1, tm1, _ = run_phase(eng, sharded, coll, dim, 1, k, max(20, args.steps), 3, dist_on,
-                                stream_fn, 1000)
         steps1 = max(20, args.steps)
+        el1, tm1, outs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 3, dist_on,
+                                    stream_fn, 1000)
         r1 = kernel_roofline(hi - lo, dim, elem, 1, k, tm1["scan_ms"], "hbm")
         result["secondary"] = {"workload": "same corpus, single query (GEMV path)",
                                "value": round(steps1 / el1, 2), "unit": "queries/s",
-                               "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1}
+                               "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1,
+                               "steps_verified": verify_steps(pkg, outs1, k, n_full)}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(cfg, args, n_full)
         except Exception as e:  # the baseline never decides the run
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
+        # the same leg checks the timed batch against the oracle (outside the timer)
+        try:
+            result["parity"] = oracle_parity(pkg, cfg, n_full, out.cpu().numpy().view(np.uint64))
+        except Exception as e:  # reported, never silent
+            result["parity"] = {"queries_checked": 0, "error": repr(e)}
     elif rank == 0:
         result["cpu_baseline"] = None
 
-    # sanity: the last step's results are well-formed (full k, sorted)
-    if rank == 0 and out is not None:
-        s, r, c = pkg.keys_decode(out.cpu().numpy().view(np.uint64))
-        assert int(c.min()) == min(k, n_full), "incomplete result lists"
-        assert np.all(np.diff(s, axis=1) <= 0), "unsorted results"
-        if args.dump_keys:
-            np.save(args.dump_keys, out.cpu().numpy().view(np.uint64))
+    if rank == 0 and args.dump_keys:
+        np.save(args.dump_keys, out.cpu().numpy().view(np.uint64))
 
     if rank == 0:
         print(json.dumps(result), flush=True)

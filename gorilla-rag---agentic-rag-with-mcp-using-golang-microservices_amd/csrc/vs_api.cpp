@@ -67,6 +67,11 @@ struct SColl {
   std::vector<std::string> iname;  // shard s -> its collection's name on its device
   int home = -1;          // placed engines: index of the device holding the whole collection
   uint64_t reserved = 0;  // placed: bytes counted against its device at creation
+  // false while vs_collection_create / vs_restore is still making it on the
+  // devices: the name is taken (a second create fails EXISTS) but every
+  // other call, vs_collection_drop included, sees "not found", so only the
+  // creating call can take it back out (and return its reservation, once)
+  std::atomic<bool> ready{false};
 };
 
 // A device-resident filter of a multi-shard engine: one per shard.
@@ -112,6 +117,16 @@ struct vs_engine {
     std::atomic<int> inflight{0};
   };
   std::vector<std::unique_ptr<CtxSet>> sets;
+  // Striped engines: every set's all-gather is enqueued under coll_mu and
+  // waits, on each device, for the previous one (coll_ev[d], recorded after
+  // it), so the collectives of different sets' communicators execute in ONE
+  // order on every device. Without it two sets' collectives over the same
+  // GPUs could start in opposite orders on two devices, each kernel waiting
+  // for a peer that runs the other: RCCL's documented deadlock for
+  // concurrent communicators.
+  std::mutex coll_mu;
+  std::vector<hipEvent_t> coll_ev;  // per device index; armed after the first collective
+  bool coll_armed = false;
   // VS_FLAG_PLACE_COLLECTIONS: whole collections per device; bytes reserved
   // and collections per device (the placement balance), guarded by map_mu
   bool placed = false;
@@ -130,7 +145,8 @@ namespace {
 std::shared_ptr<SColl> find_scoll(vs_engine* E, const char* name) {
   std::lock_guard<std::mutex> g(E->map_mu);
   auto it = E->colls.find(name ? name : "");
-  return it == E->colls.end() ? nullptr : it->second;
+  return it == E->colls.end() || !it->second->ready.load(std::memory_order_acquire) ? nullptr
+                                                                                    : it->second;
 }
 
 DevEngine* shard_eng(vs_engine* E, uint32_t s) { return E->dev[E->shard_dev[s]]; }
@@ -317,19 +333,33 @@ int sharded_search(vs_engine* E, CtxSet& cx, SColl& sc, const float* h_q, const 
       send[d] = sc_d.keys.as<uint64_t>();
     }
   }
-  // 3. one all-gather of the devices' lists over RCCL, merged on dev 0
-  ncclResult_t r = ncclGroupStart();
-  if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
-  for (uint32_t d = 0; d < D; ++d) {
-    r = ncclAllGather(send[d], cx.scr[d].gather.p, (size_t)nq * k, ncclUint64, cx.comm[d],
-                      cx.dev[d]->stream);
-    if (r != ncclSuccess) {
-      (void)ncclGroupEnd();
-      return nccl_fail(r, "ncclAllGather");
+  // 3. one all-gather of the devices' lists over RCCL, merged on dev 0; in
+  //    the engine's one collective order (coll_mu / coll_ev)
+  {
+    std::lock_guard<std::mutex> cg(E->coll_mu);
+    if (E->coll_armed)
+      for (uint32_t d = 0; d < D; ++d) {
+        VS_HIP(vsd::set_dev(cx.dev[d]), "hipSetDevice");
+        VS_HIP(hipStreamWaitEvent(cx.dev[d]->stream, E->coll_ev[d], 0), "collective order");
+      }
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    for (uint32_t d = 0; d < D; ++d) {
+      r = ncclAllGather(send[d], cx.scr[d].gather.p, (size_t)nq * k, ncclUint64, cx.comm[d],
+                        cx.dev[d]->stream);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(r, "ncclAllGather");
+      }
     }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    for (uint32_t d = 0; d < D; ++d) {
+      VS_HIP(vsd::set_dev(cx.dev[d]), "hipSetDevice");
+      VS_HIP(hipEventRecord(E->coll_ev[d], cx.dev[d]->stream), "collective order");
+    }
+    E->coll_armed = true;
   }
-  r = ncclGroupEnd();
-  if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
   DevEngine* d0 = cx.dev[0];
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
   return vsd::merge_any(d0, cx.scr[0].gather.as<uint64_t>(), D, (uint64_t)nq * k, k, nq, k, k,
@@ -374,6 +404,9 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
   if (filter_id && (f.coll_gen != sc->gen || f.rows != sc->rows))
     return fail(VS_ERR_INVALID_ARG, "filter " + std::to_string(filter_id) +
                                         " was built for another collection state");
+  // min(k, rows) searched and sized; the outputs keep stride k (vs_engine.cpp search_host)
+  const uint32_t ko = k;
+  k = (uint32_t)std::min<uint64_t>(k, std::max<uint64_t>(sc->rows, 1));
   const size_t qbytes = (size_t)nq * dim * 4, kbytes = (size_t)nq * k * 8;
   std::vector<std::vector<uint64_t>> bits_keep;  // alive until the wait below
   std::vector<std::shared_ptr<vsd::DevFilter>> fkeep;  // likewise
@@ -432,7 +465,7 @@ int sharded_search_host(vs_engine* E, const char* coll, const float* queries, ui
   // every device (all scratch is ordered by the devices' streams)
   aw.locks.clear();
   const hipError_t we = vsd::wait_event(hs->done);
-  if (we == hipSuccess) vsd::decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+  if (we == hipSuccess) vsd::decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count, ko);
   {
     std::lock_guard<std::mutex> g(d0->work_mu);
     hs->busy = false;
@@ -700,22 +733,17 @@ int sharded_create(vs_engine* E, const char* name, uint32_t dim, int metric, int
       E->dev_colls[best] += 1;
       E->colls[name] = sc;
     }
-    if (restore_path) {
-      const int rc = vsd::restore(home_eng(E, *sc), sc->iname[0].c_str(), restore_path);
-      if (rc != VS_OK) {
-        const std::string msg = vsd::last_error();
-        unplace(E, *sc);
-        return fail(rc, msg);
-      }
-      return VS_OK;
-    }
-    const int rc = vsd::collection_create(home_eng(E, *sc), sc->iname[0].c_str(), dim, metric,
-                                          dtype, capacity_hint, row_base);
+    const int rc =
+        restore_path
+            ? vsd::restore(home_eng(E, *sc), sc->iname[0].c_str(), restore_path)
+            : vsd::collection_create(home_eng(E, *sc), sc->iname[0].c_str(), dim, metric, dtype,
+                                     capacity_hint, row_base);
     if (rc != VS_OK) {
       const std::string msg = vsd::last_error();
       unplace(E, *sc);
       return fail(rc, msg);
     }
+    sc->ready.store(true, std::memory_order_release);
     return VS_OK;
   }
   if (row_base != 0)
@@ -740,6 +768,7 @@ int sharded_create(vs_engine* E, const char* name, uint32_t dim, int metric, int
       return fail(rc, msg);
     }
   }
+  sc->ready.store(true, std::memory_order_release);
   return VS_OK;
 }
 
@@ -748,7 +777,8 @@ int sharded_drop(vs_engine* E, const char* name) {
   {
     std::lock_guard<std::mutex> g(E->map_mu);
     auto it = E->colls.find(name ? name : "");
-    if (it == E->colls.end()) return not_found(name);
+    if (it == E->colls.end() || !it->second->ready.load(std::memory_order_acquire))
+      return not_found(name);  // absent, or still being made by its creating call
     sc = it->second;
     E->colls.erase(it);
   }
@@ -911,6 +941,11 @@ void destroy(vs_engine* E) {
     }
   }
   E->sets.clear();
+  for (size_t d = 0; d < E->coll_ev.size(); ++d)
+    if (E->coll_ev[d]) {
+      (void)hipSetDevice(E->dev[d]->device);
+      (void)hipEventDestroy(E->coll_ev[d]);
+    }
   if (!E->dev.empty() && E->dev[0]) {
     (void)hipSetDevice(E->dev[0]->device);
     (void)hipStreamSynchronize(E->dev[0]->stream);
@@ -938,6 +973,8 @@ size_t vs_copy_last_error(char* buf, size_t len) {
   }
   return n;
 }
+
+int vs_runtime_check(void) { return vsd::one_hip_runtime(); }
 
 int vs_device_count(void) {
   int n = 0;
@@ -976,9 +1013,11 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out) {
   auto* E = new vs_engine();
   E->sharded = cfg->n_shards > 1;
   E->placed = E->sharded && (cfg->flags & VS_FLAG_PLACE_COLLECTIONS);
+  // VS_FLAG_ENGINE_PER_SHARD: a device engine per entry, repeated ordinals included
+  const bool per_shard = E->placed && (cfg->flags & VS_FLAG_ENGINE_PER_SHARD);
   std::vector<int> devlist;
   for (uint32_t s = 0; s < cfg->n_shards; ++s) {
-    auto it = std::find(devlist.begin(), devlist.end(), ord[s]);
+    auto it = per_shard ? devlist.end() : std::find(devlist.begin(), devlist.end(), ord[s]);
     uint32_t d = (uint32_t)(it - devlist.begin());
     if (it == devlist.end()) {
       DevEngine* de = nullptr;
@@ -998,6 +1037,16 @@ int vs_open_multi(const vs_config_multi* cfg, vs_engine** out) {
   if (E->sharded) {
     E->dev_bytes.assign(E->dev.size(), 0);
     E->dev_colls.assign(E->dev.size(), 0);
+    if (!E->placed) {
+      E->coll_ev.assign(E->dev.size(), nullptr);
+      for (size_t d = 0; d < E->dev.size(); ++d) {
+        (void)hipSetDevice(E->dev[d]->device);
+        if (hipEventCreateWithFlags(&E->coll_ev[d], hipEventDisableTiming) != hipSuccess) {
+          destroy(E);
+          return fail(VS_ERR_DEVICE, "event");
+        }
+      }
+    }
     // context set j = search context j of every device
     size_t nsets = SIZE_MAX;
     for (DevEngine* de : E->dev) nsets = std::min(nsets, de->store->ctx.size());
@@ -1107,6 +1156,7 @@ int vs_generate(vs_engine* eng, const char* coll, uint64_t n, uint64_t seed) {
 int vs_generate_vectors(vs_engine* eng, uint64_t seed, uint64_t row0, uint64_t n, uint32_t dim,
                         float* d_out, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (const int rt = vsd::one_hip_runtime()) return rt;
   return vsd::generate_vectors(eng->dev[0], seed, row0, n, dim, d_out, stream);
 }
 
@@ -1174,6 +1224,7 @@ int vs_search_filter_id(vs_engine* eng, const char* coll, const float* queries, 
 int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uint32_t nq,
                    uint32_t dim, uint32_t k, uint64_t* d_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (const int rt = vsd::one_hip_runtime()) return rt;
   if (!eng->sharded)
     return vsd::search_keys(eng->dev[0], coll, d_queries, nq, dim, k, d_keys, stream);
   if (k == 0) return fail(VS_ERR_INVALID_ARG, "k must be at least 1");
@@ -1211,6 +1262,7 @@ int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries, uin
 int vs_merge_keys(vs_engine* eng, const uint64_t* d_lists, uint32_t n_lists, uint32_t nq,
                   uint32_t k_in, uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (const int rt = vsd::one_hip_runtime()) return rt;
   return vsd::merge_keys(eng->dev[0], d_lists, n_lists, nq, k_in, k, d_out_keys, stream);
 }
 
@@ -1249,6 +1301,7 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
                          uint32_t k, uint64_t* d_out_keys, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   if (!eng->pcomm) return fail(VS_ERR_INVALID_ARG, "vs_comm_init has not been called");
+  if (const int rt = vsd::one_hip_runtime()) return rt;
   if (k == 0 || k_in == 0) return fail(VS_ERR_INVALID_ARG, "bad merge shape");
   if (nq == 0) return VS_OK;
   if (!d_local || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
@@ -1273,6 +1326,7 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
                    float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
+  if (const int rt = vsd::one_hip_runtime()) return rt;
   return vsd::decode_keys(eng->dev[0], d_keys, nq, k, out_scores, out_rows, out_count, stream);
 }
 

@@ -269,8 +269,10 @@ int merge_any(DevEngine* eng, const uint64_t* lists, uint32_t L, uint64_t lstrid
               uint64_t qstride, uint32_t nq, uint32_t kin, uint32_t k, uint64_t* out);
 int decode_keys(DevEngine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,
                 float* out_scores, uint64_t* out_rows, uint32_t* out_count, void* stream);
+// keys [nq][k] -> outputs of row stride ko >= k (slots k .. ko-1 zeroed: a
+// search clamped to the collection's rows answers into the caller's stride)
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores, uint64_t* rows,
-                 uint32_t* count);
+                 uint32_t* count, uint32_t ko = 0);
 int checksum(DevEngine* eng, const char* coll, uint64_t* out);
 int snapshot(DevEngine* eng, const char* coll, const char* path);
 int restore(DevEngine* eng, const char* coll, const char* path);
@@ -280,6 +282,10 @@ int timing(DevEngine* eng, double* scan_ms_sum, uint64_t* scan_count, double* me
 uint64_t popcount_rows(const uint64_t* allow, uint64_t rows);
 // Waits for ev: a short spin on hipEventQuery, then hipEventSynchronize.
 hipError_t wait_event(hipEvent_t ev);
+// VS_OK when this process maps one HIP runtime; else VS_ERR_DEVICE with both
+// paths in the message. Entry points that take the caller's device pointers
+// and stream call it first ("one HIP runtime per process").
+int one_hip_runtime();
 
 // Search of device queries d_q (nq x dim fp32 on this device, ordered on
 // eng->stream) -> keys d_keys [nq][k] in local rows + row_base; work_mu and

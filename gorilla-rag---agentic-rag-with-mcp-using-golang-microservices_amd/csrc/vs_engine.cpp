@@ -7,6 +7,7 @@
 // guarded by reader/writer locks (search = reader, upsert = writer), which is
 // what net/http's goroutine-per-request handlers (main.go:77) need.
 #include <hip/hip_runtime.h>
+#include <link.h>
 
 #include <algorithm>
 #include <atomic>
@@ -683,19 +684,20 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
 }
 
 void decode_host(const uint64_t* keys, uint32_t nq, uint32_t k, float* scores,
-                 uint64_t* rows, uint32_t* count) {
+                 uint64_t* rows, uint32_t* count, uint32_t ko) {
+  if (ko < k) ko = k;
   for (uint32_t i = 0; i < nq; ++i) {
     uint32_t c = 0;
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint64_t key = keys[(size_t)i * k + j];
+    for (uint32_t j = 0; j < ko; ++j) {
+      const uint64_t key = j < k ? keys[(size_t)i * k + j] : 0ull;
       if (key == 0) {
-        if (scores) scores[(size_t)i * k + j] = 0.f;
-        if (rows) rows[(size_t)i * k + j] = 0;
+        if (scores) scores[(size_t)i * ko + j] = 0.f;
+        if (rows) rows[(size_t)i * ko + j] = 0;
         continue;
       }
       ++c;
-      if (scores) scores[(size_t)i * k + j] = vs::key_score(key);
-      if (rows) rows[(size_t)i * k + j] = vs::key_row(key);
+      if (scores) scores[(size_t)i * ko + j] = vs::key_score(key);
+      if (rows) rows[(size_t)i * ko + j] = vs::key_row(key);
     }
     if (count) count[i] = c;
   }
@@ -1115,6 +1117,61 @@ hipError_t wait_event(hipEvent_t ev) {
   return hipEventSynchronize(ev);
 }
 
+// One HIP runtime per process (r04). torch's ROCm wheel ships its own
+// libamdhip64.so and links it by file name, while this library links
+// libamdhip64.so.7 by soname: when this library is loaded first, importing
+// torch later maps a SECOND runtime (and HSA runtime) into the process. The
+// two have separate null streams and queues with no ordering between them, so
+// a device-pointer search on "torch's stream" is not ordered with torch's own
+// work at all: the round-3 driver run read a query's keys before the select
+// kernel had written them (tests/test_placement_gpu.py). Device-pointer entry
+// points refuse to run in such a process instead of racing. The scan is a
+// dl_iterate_phdr walk, repeated only when the loader's add/remove counters
+// moved since the last one.
+namespace {
+struct RtScan {
+  unsigned long long adds = 0, subs = 0;
+  bool probe = true;  // the first callback only reads the loader's counters
+  std::vector<std::string> paths;
+};
+int rt_visit(struct dl_phdr_info* info, size_t, void* p) {
+  RtScan& s = *(RtScan*)p;
+  if (s.probe) {
+    s.adds = info->dlpi_adds;
+    s.subs = info->dlpi_subs;
+    return 1;
+  }
+  const char* n = info->dlpi_name ? info->dlpi_name : "";
+  const char* b = std::strrchr(n, '/');
+  b = b ? b + 1 : n;
+  if (std::strncmp(b, "libamdhip64.so", 14) == 0) s.paths.emplace_back(n);
+  return 0;
+}
+}  // namespace
+
+int one_hip_runtime() {
+  static std::mutex mu;
+  static unsigned long long seen_adds = ~0ull, seen_subs = ~0ull;
+  static std::string problem;
+  RtScan s;
+  dl_iterate_phdr(rt_visit, &s);
+  std::lock_guard<std::mutex> g(mu);
+  if (s.adds != seen_adds || s.subs != seen_subs) {
+    RtScan full;
+    full.probe = false;
+    dl_iterate_phdr(rt_visit, &full);
+    problem.clear();
+    if (full.paths.size() > 1)
+      problem = "two HIP runtimes are loaded in this process (" + full.paths[0] + " and " +
+                full.paths[1] +
+                "): device pointers and streams of one are not ordered with the other's work; "
+                "load one runtime (import torch before libvsearch, engine.load_library does)";
+    seen_adds = s.adds;
+    seen_subs = s.subs;
+  }
+  return problem.empty() ? VS_OK : fail(VS_ERR_DEVICE, problem);
+}
+
 // Spins on a completion word in mapped host memory for up to spin_us(): true
 // once it holds seq.
 bool wait_word(const uint64_t* w, uint64_t seq) {
@@ -1200,6 +1257,11 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
     return fail(VS_ERR_INVALID_ARG, "filter bitmap has " + std::to_string(allow_words) +
                                         " words, the collection needs " +
                                         std::to_string((c->rows + 63) / 64));
+  // a limit past the collection returns every row, as Qdrant does: search
+  // (and size the keys, staging and sort scratch) for min(k, rows); the
+  // caller's outputs keep their stride k, zero past the rows
+  const uint32_t ko = k;
+  k = (uint32_t)std::min<uint64_t>(k, std::max<uint64_t>(c->rows, 1));
   // the filter stays referenced until the device is done with it (a
   // concurrent vs_filter_drop only unlinks it)
   std::shared_ptr<DevFilter> df;
@@ -1305,10 +1367,10 @@ int search_host(DevEngine* eng, const char* coll, const float* queries, uint32_t
       if (we == hipSuccess && __atomic_load_n(word, __ATOMIC_ACQUIRE) != hd.seq)
         we = hipErrorLaunchFailure;  // the stream completed without the word
     }
-    if (we == hipSuccess) decode_host(hs->mapped, nq, k, out_scores, out_rows, out_count);
+    if (we == hipSuccess) decode_host(hs->mapped, nq, k, out_scores, out_rows, out_count, ko);
   } else {
     we = wait_event(hs->done);
-    if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count);
+    if (we == hipSuccess) decode_host((const uint64_t*)hs->out, nq, k, out_scores, out_rows, out_count, ko);
   }
   g.lock();
   hs->busy = false;

@@ -37,6 +37,7 @@ FLAG_TIMING = 1
 FLAG_TIMING_MERGE = 2
 FLAG_TIMING_SAMPLE = 4
 FLAG_PLACE_COLLECTIONS = 8
+FLAG_ENGINE_PER_SHARD = 16
 
 # Every function include/vsearch.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -48,7 +49,7 @@ EXPORTS = (
     "vs_snapshot", "vs_restore", "vs_checksum", "vs_search_filtered",
     "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
     "vs_engine_layout", "vs_comm_unique_id", "vs_comm_init", "vs_gather_merge_keys",
-    "vs_copy_last_error", "vs_build_id", "vs_collection_placement",
+    "vs_copy_last_error", "vs_build_id", "vs_collection_placement", "vs_runtime_check",
 )
 COMM_ID_BYTES = 128
 
@@ -72,6 +73,37 @@ class _ConfigMulti(ctypes.Structure):
 _lib = None
 
 
+def _torch_runtime_first():
+    """Imports torch (when installed) before libvsearch is loaded, so the
+    process holds ONE HIP runtime. torch's ROCm wheel bundles its own
+    libamdhip64.so and links it by file name; libvsearch links
+    libamdhip64.so.7 by soname. torch first: libvsearch binds to the runtime
+    torch loaded (same soname). libvsearch first: a later torch import maps a
+    second runtime, whose null stream and queues are unordered with ours --
+    a vs_search_keys on torch's stream then races torch's own work (the
+    round-3 driver failure). VS_TORCH_FIRST=0 skips this."""
+    if os.environ.get("VS_TORCH_FIRST", "1") == "0":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def hip_runtimes() -> list:
+    """Paths of the libamdhip64 runtimes mapped into this process."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if len(line.split()) >= 6 else ""
+                if os.path.basename(p).startswith("libamdhip64.so") and p not in out:
+                    out.append(p)
+    except OSError:
+        pass
+    return out
+
+
 def load_library(path: str = LIB_PATH):
     """Loads libvsearch.so (built by __graft_entry__.build()). Raises if absent."""
     global _lib
@@ -80,6 +112,7 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: build the HIP library first "
                           "(python -c 'import __graft_entry__ as g; g.build()')")
+    _torch_runtime_first()
     L = ctypes.CDLL(path)
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     cp = ctypes.c_char_p
@@ -108,6 +141,7 @@ def load_library(path: str = LIB_PATH):
         "vs_last_error": ([], ctypes.c_char_p),
         "vs_copy_last_error": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_size_t),
         "vs_build_id": ([], ctypes.c_char_p),
+        "vs_runtime_check": ([], i32),
         "vs_timing": ([vp, vp, vp, vp, vp, i32], i32),
         "vs_snapshot": ([vp, cp, cp], i32),
         "vs_restore": ([vp, cp, cp], i32),
@@ -174,16 +208,19 @@ class VectorEngine:
     are then row-striped over the shards and searched with one RCCL
     all-gather per call (include/vsearch.h "multi-GPU engine"), or with
     ``place_collections`` each placed whole on one device
-    (VS_FLAG_PLACE_COLLECTIONS)."""
+    (VS_FLAG_PLACE_COLLECTIONS); ``engine_per_shard`` then gives every entry
+    of ``shards`` its own device engine even where ordinals repeat
+    (VS_FLAG_ENGINE_PER_SHARD)."""
 
     def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False,
                  timing_sample: bool = False, shards: Optional[Sequence[int]] = None,
-                 place_collections: bool = False):
+                 place_collections: bool = False, engine_per_shard: bool = False):
         L = load_library()
         flags = ((FLAG_TIMING if timing else 0) |
                  (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
                  (FLAG_TIMING_SAMPLE if timing and timing_sample else 0) |
-                 (FLAG_PLACE_COLLECTIONS if place_collections else 0))
+                 (FLAG_PLACE_COLLECTIONS if place_collections else 0) |
+                 (FLAG_ENGINE_PER_SHARD if engine_per_shard else 0))
         h = ctypes.c_void_p()
         if shards is None:
             cfg = _Config(device, flags)

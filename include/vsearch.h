@@ -98,6 +98,14 @@ typedef struct vs_config {
  * collections from concurrent handlers, main.go:77, :80-119). Row-striping
  * stays the layout for one collection larger than one device. */
 #define VS_FLAG_PLACE_COLLECTIONS 8u
+/* With VS_FLAG_PLACE_COLLECTIONS: one device engine (its own store, search
+ * contexts and streams) per entry of `devices`, even where ordinals repeat,
+ * so {0, 0} holds two placement slots on device 0. Collections placed on the
+ * second slot take the cross-device path of vs_search_keys (query and key
+ * copies ordered by events on the caller's stream) on a one-GPU host, where
+ * it is otherwise only reachable with two GPUs. Ignored without placement:
+ * RCCL holds one rank per device. */
+#define VS_FLAG_ENGINE_PER_SHARD 16u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 
@@ -235,7 +243,15 @@ int vs_search_filter_id(vs_engine* eng, const char* coll, const float* queries, 
  * `d_keys` (nq x k uint64) are device pointers on this engine's device;
  * `stream` is a hipStream_t (NULL = the null stream). The work is ordered
  * after prior work on `stream`, and later work on `stream` sees the result.
- * Each result is a 64-bit key (see below); unused slots hold 0. */
+ * Each result is a 64-bit key (see below); unused slots hold 0.
+ * The stream and the pointers must come from the HIP runtime this library
+ * is linked to: in a process that maps two libamdhip64 runtimes (e.g.
+ * torch's bundled copy next to /opt/rocm's) this call and every other one
+ * taking caller device pointers (vs_merge_keys, vs_gather_merge_keys,
+ * vs_decode_keys, vs_generate_vectors) fail with VS_ERR_DEVICE rather than
+ * run unordered with the caller's work. vs_runtime_check() runs that test
+ * alone (no device needed): VS_OK, or VS_ERR_DEVICE naming both runtimes. */
+int vs_runtime_check(void);
 int vs_search_keys(vs_engine* eng, const char* coll, const float* d_queries,
                    uint32_t nq, uint32_t dim, uint32_t k, uint64_t* d_keys,
                    void* stream);

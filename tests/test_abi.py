@@ -131,3 +131,39 @@ def test_copy_last_error_is_the_same_call_message(pkg):
     assert L.vs_copy_last_error(small, 5) == len(full)
     assert small.value == full[:4]
     assert L.vs_copy_last_error(None, 0) == len(full)
+
+
+_RT_PROBE = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+import __graft_entry__ as ge
+pkg = ge.load_package()
+L = pkg.load_library()
+import torch  # noqa: F401  (after the library: a second runtime unless load_library imported it first)
+from importlib import import_module
+eng = import_module(pkg.__name__ + ".engine")
+rc = L.vs_runtime_check()
+print(json.dumps({{"rc": rc, "msg": L.vs_last_error().decode() if rc else "",
+                  "runtimes": eng.hip_runtimes()}}))
+"""
+
+
+@pytest.mark.parametrize("torch_first", ["1", "0"])
+def test_one_hip_runtime_per_process(torch_first):
+    """Regression for the round-3 driver failure: torch's
+    wheel bundles its own libamdhip64.so, so loading libvsearch before torch
+    mapped two HIP runtimes whose streams are unordered with each other.
+    load_library now imports torch first (one runtime); with that disabled
+    the library's own check refuses device-pointer calls (VS_ERR_DEVICE)."""
+    import json
+    env = dict(os.environ, VS_TORCH_FIRST=torch_first)
+    out = subprocess.run([os.sys.executable, "-c", _RT_PROBE.format(root=ROOT)], env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    if torch_first == "1":
+        assert len(r["runtimes"]) == 1, r
+        assert r["rc"] == 0
+    else:
+        assert len(r["runtimes"]) == 2, r
+        assert r["rc"] == -5 and "two HIP runtimes" in r["msg"], r

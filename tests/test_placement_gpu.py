@@ -74,11 +74,15 @@ def test_placed_equals_single_device(placed, engine, orc, pkg, dtype, tmp_path):
         # device-pointer search on the engine's first device
         import torch
         dq = torch.from_numpy(Q[:8]).cuda()
-        dk = torch.zeros((8, 10), dtype=torch.int64, device="cuda")
+        # all-ones sentinel: a slot the search never wrote reads as ~0, not as
+        # an empty key (0), so a stream-ordering hole and an empty answer differ
+        dk = torch.full((8, 10), -1, dtype=torch.int64, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
         placed.search_keys(name, dq.data_ptr(), 8, dim, 10, dk.data_ptr(), st)
         torch.cuda.synchronize()
-        s, r, c = pkg.keys_decode(dk.cpu().numpy().view(np.uint64))
+        got = dk.cpu().numpy().view(np.uint64)
+        assert not np.any(got == np.uint64(0xFFFFFFFFFFFFFFFF)), "keys never written"
+        s, r, c = pkg.keys_decode(got)
         want = engine.search(name, Q[:8], 10)
         assert np.array_equal(r, want[1]) and np.array_equal(s, want[0])
         # snapshot of a placed collection restores anywhere, and back
@@ -151,3 +155,70 @@ def test_service_over_placed_engine(pkg, orc):
         s.close()
         eng.close()
         ref.close()
+
+
+def test_one_hip_runtime(pkg):
+    """The process holds one HIP runtime, torch's and the library's alike
+    (engine.load_library imports torch first): the round-3 failure above was
+    a second runtime whose null stream is not torch's."""
+    import torch  # noqa: F401
+    from importlib import import_module
+    eng_mod = import_module(pkg.__name__ + ".engine")
+    assert len(eng_mod.hip_runtimes()) == 1, eng_mod.hip_runtimes()
+    assert pkg.load_library().vs_runtime_check() == 0
+
+
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_placed_off_first_device(engine, orc, pkg, dtype):
+    """VS_FLAG_ENGINE_PER_SHARD: shards [0, 0] are two device engines on the
+    one GPU, so a collection lands on engine index 1 and vs_search_keys takes
+    placed_search_keys (vs_api.cpp: the queries copied from the caller's
+    device to the home device after an event on the caller's stream, the keys
+    copied back and the caller's stream made to wait on them) -- the path a
+    multi-GPU node runs for C5's collections, otherwise unreachable here.
+    Checked against a single-device engine and the streaming oracle, on
+    torch's null stream and on a side stream. Anchor: three collections
+    served concurrently, rag/vector-service/main.go:77, :80-119."""
+    import torch
+    dim, n = 768, 60_000
+    eng2 = pkg.VectorEngine(shards=[0, 0], place_collections=True, engine_per_shard=True)
+    name = f"off{dtype}"
+    try:
+        assert eng2.layout() == (2, 2)
+        eng2.create_collection("first", 128, 0, dtype, 0)  # engine 0
+        eng2.create_collection(name, dim, 0, dtype, 0)     # engine 1 (fewest collections)
+        h = json.loads(eng2.health())
+        assert [d["collections"] for d in h["devices"]] == [1, 1], h
+        assert eng2.placement(name) == 0  # the device ordinal: both engines are on GPU 0
+        eng2.generate(name, n, orc.SEED_CORPUS)
+        engine.create_collection(name, dim, 0, dtype, n)
+        engine.generate(name, n, orc.SEED_CORPUS)
+        Q = orc.generate(orc.SEED_QUERY, 21, 40, dim)
+        Qp = orc.preprocess(Q, cosine=True, bf16=bool(dtype))
+        for nq, k in ((1, 10), (8, 10), (40, 50), (3, 200)):
+            a = eng2.search(name, Q[:nq], k)
+            b = engine.search(name, Q[:nq], k)
+            assert all(np.array_equal(x, y) for x, y in zip(a, b)), (nq, k)
+        side = torch.cuda.Stream()
+        for st in (torch.cuda.default_stream(), side):
+            with torch.cuda.stream(st):
+                for nq, k in ((8, 10), (40, 100), (1, 5)):
+                    dq = torch.from_numpy(Q[:nq]).cuda()
+                    dk = torch.full((nq, k), -1, dtype=torch.int64, device="cuda")
+                    eng2.search_keys(name, dq.data_ptr(), nq, dim, k, dk.data_ptr(), st.cuda_stream)
+                    got = dk.cpu().numpy().view(np.uint64)  # ordered on st (torch's copy)
+                    assert not np.any(got == np.uint64(0xFFFFFFFFFFFFFFFF)), "keys never written"
+                    s, r, c = pkg.keys_decode(got)
+                    want = engine.search(name, Q[:nq], k)
+                    assert np.array_equal(r, want[1]) and np.array_equal(s, want[0]), (nq, k)
+                    s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp[:nq], k, bool(dtype))
+                    resc = orc.rescore_generated(orc.SEED_CORPUS, Qp[:nq], r, c, bool(dtype))
+                    bad = orc.check_topk(s, r, c, s64, rr, cc, resc, score_rtol=1e-5)
+                    assert not bad, bad[:4]
+        torch.cuda.synchronize()
+    finally:
+        eng2.close()
+        try:
+            engine.drop_collection(name)
+        except pkg.VSError:
+            pass

@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box session helper (run through gpurun). Every GPU step has its own
 # time limit; a step that crashes/hangs stops the script (no retries).
-#   tools/gpu_session.sh [tests] [testsel TAG FILES.. --] [bench TAG ARGS.. --] [prof TAG ARGS.. --]
+#   tools/gpu_session.sh [tests] [smoke] [testsel TAG FILES.. --] [bench TAG ARGS.. --]
+#                        [prof TAG ARGS.. --] [pmc TAG CTRS ARGS.. --] [tool TAG SECONDS CMD.. --]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
@@ -44,6 +45,11 @@ while [ $# -gt 0 ]; do
       timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$PWD/gpurun_out/pmc_$tag" -o run \
         --output-format csv -- python bench.py "${args[@]}" > "gpurun_out/pmc_$tag.log" 2>&1
       rc=$?; echo "pmc_${tag}_rc=$rc"; stop_if_bad $rc pmc ;;
+    tool)  # tool TAG SECONDS CMD... --   (a python tool under its own limit; stdout -> gpurun_out/tool_TAG.out)
+      shift; tag="$1"; shift; lim="$1"; shift; args=()
+      while [ $# -gt 0 ] && [ "$1" != "--" ]; do args+=("$1"); shift; done; [ $# -gt 0 ] && shift
+      timeout -k 10 "$lim" python -u "${args[@]}" > "gpurun_out/tool_$tag.out" 2> "gpurun_out/tool_$tag.err"
+      rc=$?; echo "tool_${tag}_rc=$rc"; tail -3 "gpurun_out/tool_$tag.out"; stop_if_bad $rc "tool $tag" ;;
     *) echo "unknown step $1"; exit 2 ;;
   esac
 done
