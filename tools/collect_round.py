@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Copies a measure_round.sh batch from gpurun_out/ into profiles/ (tracked):
+the bench lines, the rocprofv3 kernel stats and the main-pass per-launch
+trace named with the benched binary's build id, C1 and the concurrency
+trials; prints the bench's kernel_ms beside the trace's post-warmup mean.
+
+    python tools/collect_round.py TAG
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "gpurun_out")
+P = os.path.join(ROOT, "profiles")
+
+
+def main():
+    tag = sys.argv[1]
+    b = json.load(open(os.path.join(G, f"{tag}_bench_c3.json")))
+    bid = b["config"]["build_id"]
+    shutil.copy(os.path.join(G, f"{tag}_bench_c3.json"), os.path.join(P, f"{tag}_c3_{bid}_bench.json"))
+    shutil.copy(os.path.join(G, f"{tag}_prof_c3.json"),
+                os.path.join(P, f"{tag}_c3_{bid}_bench_under_rocprof.json"))
+    d = os.path.join(G, f"{tag}_prof_c3")
+    shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(P, f"{tag}_c3_{bid}_kernel_stats.csv"))
+    rows = [r for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv")))
+            if "mfma_topk_kernel<768, 0" in r["Kernel_Name"]]
+    with open(os.path.join(P, f"{tag}_c3_{bid}_main_pass_trace.csv"), "w") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Duration_ns"])
+        for r in rows:
+            w.writerow([r["Kernel_Name"], r["Start_Timestamp"], r["End_Timestamp"],
+                        int(r["End_Timestamp"]) - int(r["Start_Timestamp"])])
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    pr = json.load(open(os.path.join(G, f"{tag}_prof_c3.json")))
+    print(f"build {bid}: bench kernel_ms {b['roofline']['kernel_ms']} (frac {b['roofline']['frac']}); "
+          f"under rocprof {pr['roofline']['kernel_ms']}; trace mean after 10 launches "
+          f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10}")
+    for src, dst in ((f"{tag}_c1_http.jsonl", f"{tag}_c1_http_both_backends.jsonl"),
+                     (f"{tag}_rt_floor.json", f"{tag}_c1_rt_floor.json"),
+                     (f"{tag}_concurrency_overlap.json", f"{tag}_concurrency_overlap.json")):
+        if os.path.exists(os.path.join(G, src)):
+            shutil.copy(os.path.join(G, src), os.path.join(P, dst))
+    for fn in sorted(os.listdir(G)):
+        if fn.startswith(f"{tag}_bench_") and fn.endswith(".json") and fn != f"{tag}_bench_c3.json":
+            shutil.copy(os.path.join(G, fn), os.path.join(P, fn.replace("_bench_", "_") + ""))
+
+
+if __name__ == "__main__":
+    main()
