@@ -428,6 +428,17 @@ int merge_any(DevEngine* eng, const uint64_t* lists, uint32_t L, uint64_t lstrid
   return VS_OK;
 }
 
+// The main pass records each candidate quarter's largest score and the
+// select reads only the quarters that can hold a top-k key (r04; default on,
+// VS_SELECT_QMAX=0 gives back the select that re-reads every slab; read once).
+bool select_qmax() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_SELECT_QMAX");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
 // queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
 //  1. sample pass over 1/128 of every workgroup's tiles -> tile maxima ->
@@ -458,7 +469,8 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const size_t slots = (size_t)maxl * PS * cap;
   const size_t cbytes = slots * 36;
   const size_t scbytes = (size_t)maxl * st * PS * 4;  // tile maxima, [query][wg * st]
-  const size_t nbytes = (size_t)maxl * PS * 4 * 4;
+  // counts [maxl][PS][4], then (select_qmax) the quarters' maxima, same shape
+  const size_t nbytes = (size_t)maxl * PS * 4 * 4 * 2;
   if (eng->lists.bytes < lbytes || eng->sample_bound.bytes < sbytes || eng->cand.bytes < cbytes ||
       eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
@@ -502,14 +514,15 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     VS_HIP(vsk::launch_sample_bound(tmax, L * st, nv, k, bound, eng->stream), "sample bound");
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+    uint32_t* qmax = select_qmax() ? eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4 : nullptr;
     VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
                                  slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl,
-                                 &L, eng->stream, allow),
+                                 &L, eng->stream, allow, qmax),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
     VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                                    k, out, eng->stream, row_base, allow),
+                                    k, out, eng->stream, row_base, allow, qmax),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
   }

@@ -170,7 +170,10 @@ uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
 //    slab_tile[nlists][kMfmaQueries][cap] (cap % 4 == 0, cap >= 4 k:
 //    quarter j of a buffer is lane j's, counts in slabs
 //    cand_cnt[nlists][256][4]); a full quarter keeps its cap / 4 best slabs
-//    (exact for k <= cap / 4, never overflows);
+//    (exact for k <= cap / 4, never overflows); cand_max (nullable, same
+//    shape): each quarter's largest admitted score (vs::score_ord, 0 = no
+//    slab), which lets the select read only the few quarters that can hold
+//    a top-k key (r04);
 //    launch_select_slabs picks the top k;
 //  * lists pass (k <= kMfmaListMaxK): the main pass with per-query sorted
 //    lists in LDS (any input) -> lists[nlists][kMfmaQueries][k]; collections
@@ -192,7 +195,8 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
                             const float* init_score, float* slabs,
                             uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
-                            hipStream_t st, const uint64_t* allow = nullptr);
+                            hipStream_t st, const uint64_t* allow = nullptr,
+                            uint32_t* cand_max = nullptr);
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const float* init_score, uint64_t* lists,
@@ -205,7 +209,8 @@ hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_r
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,
-                               const uint64_t* allow = nullptr);
+                               const uint64_t* allow = nullptr,
+                               const uint32_t* cand_max = nullptr);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows, uint32_t dim = 768, bool f32 = false);

@@ -1644,6 +1644,8 @@ struct MfArgs {
                             // (32 B); quarter kq of a query's buffer belongs to its lane kq
   uint32_t* cand_tile;      // MODE 0: first global row of each slab's tile
   uint32_t* cand_cnt;       // MODE 0: [nwg][kMfmaQueries][4] slabs per quarter
+  uint32_t* cand_max;       // MODE 0, nullable: [nwg][kMfmaQueries][4] each quarter's largest
+                            // admitted score as vs::score_ord (0: no slab), for the select
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, cand_cap;
   const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
@@ -1762,6 +1764,22 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
       }
     }
   }
+}
+
+// Raises this lane's running quarter maximum (LDS word `base` + tid of the
+// main pass's counter area) to the slab maximum mx: a no-return ds_max_u32 on
+// the order-preserving image (-0 ranked as +0, as vs::make_key does). Rare
+// path; the thread id is taken opaque so no address is hoisted into the tile
+// loop, and nothing waits on the atomic (the write-out's LDS read is ordered
+// after it: one wave's LDS operations complete in order).
+template <typename P>
+__device__ __forceinline__ void mf_quarter_max(P cntl, uint32_t base, float mx) {
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+  lds_u32_t* w = (lds_u32_t*)(cntl + base + tid);
+  __hip_atomic_fetch_max(w, vs::score_ord(mx == 0.0f ? 0.0f : mx), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // A full quarter of a main-pass candidate buffer (slots [base, base + sub)):
@@ -1935,37 +1953,6 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   if constexpr (kLists)
     for (int i = threadIdx.x; i < (int)kMfmaQueries * kMfListLen; i += THREADS) lists[i] = 0;
 
-  // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
-  bf16x8_t qf[G][S::T];
-  uint32_t ql[G];
-  bool qvalid[G];
-  float th_s[G];     // admit rows whose score reaches th_s
-  // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
-  // query's buffer (candidate passes). The main pass keeps the counts and
-  // each lane's first slot in registers instead (no LDS round trip and no
-  // address rebuild in the append path; 256 VGPRs, no spill), and streams the
-  // corpus non-temporally: back to back, -2.0% at 1.25M rows and -1.2% at 10M
-  // against LDS counters and default-policy DMA (r01, 2 x 40 / 16 reps).
-  constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) == 0;
-  constexpr bool kNtDma = (MODE == 0) != ((VAR & 1024) != 0);
-  uint32_t cnt_r[G], slot0[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
-    if constexpr (kRegCnt) {
-      cnt_r[g] = 0u;
-      slot0[g] = (uint32_t)(((size_t)blockIdx.x * kMfmaQueries +
-                             (uint32_t)(w * QPW + g * 16 + col)) * a.cand_cap +
-                            (uint32_t)kq * (a.cand_cap >> 2));
-    }
-    ql[g] = (uint32_t)(w * QPW + g * 16 + col);
-    qvalid[g] = ql[g] < a.nq_valid;
-    const uint4* qrow = (const uint4*)((const unsigned char*)a.Q + (size_t)ql[g] * RBY);
-#pragma unroll
-    for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
-    th_s[g] = (a.init_score && qvalid[g]) ? a.init_score[ql[g]] : -INFINITY;
-  }
-
   // LDS-DMA source mapping: piece (s4l, rg) of a chunk holds rows rg*8 ..
   // rg*8+7, bytes [128*s4, 128*s4+128) of each; lane -> (row lane>>3,
   // 16-B position lane&7 holding chunk (lane&7) ^ swz). The per-lane part of
@@ -1973,12 +1960,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // is a scalar base advanced chunk by chunk (the chunk issued at step c is
   // c + AHEAD). Tiles past the last row read the collection's 32 rows of
   // allocation padding (vs_engine.cpp grow()) and are masked in the epilogue.
-  // VAR 8192: the prologue's loads drained and timed (ablation only)
-  uint64_t tclk1 = 0, tclk2 = 0;
-  if constexpr (kClock) {
-    __builtin_amdgcn_s_waitcnt(0);
-    tclk1 = wall_clock64();
-  }
+  constexpr bool kNtDma = (MODE == 0) != ((VAR & 1024) != 0);
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
   uint32_t loff[PPW];
 #pragma unroll
@@ -2040,6 +2022,53 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     }
     advance();
   };
+  // VAR 8388608 (r04): the ring's first AHEAD chunks are issued before the
+  // query-fragment prologue instead of after it, so the corpus fill (~5 us at
+  // ~25 GB/s per CU) overlaps the ~6 us of B-fragment loads from L2 that every
+  // launch starts with; the prologue's vmcnt(0) drain then covers both.
+  constexpr bool kEarlyFill = (VAR & 8388608) != 0;
+  if constexpr (kDma && kBF && kEarlyFill) {
+#pragma unroll
+    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
+  }
+  // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
+  bf16x8_t qf[G][S::T];
+  uint32_t ql[G];
+  bool qvalid[G];
+  float th_s[G];     // admit rows whose score reaches th_s
+  // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
+  // query's buffer (candidate passes). The main pass keeps the counts and
+  // each lane's first slot in registers instead (no LDS round trip and no
+  // address rebuild in the append path; 256 VGPRs, no spill), and streams the
+  // corpus non-temporally: back to back, -2.0% at 1.25M rows and -1.2% at 10M
+  // against LDS counters and default-policy DMA (r01, 2 x 40 / 16 reps).
+  constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) == 0;
+  uint32_t cnt_r[G], slot0[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    // (the register-count main pass keeps each lane's running quarter maximum
+    // here instead: score_ord of the largest admitted score, 0 = none)
+    if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
+    if constexpr (kRegCnt) {
+      cnt_r[g] = 0u;
+      slot0[g] = (uint32_t)(((size_t)blockIdx.x * kMfmaQueries +
+                             (uint32_t)(w * QPW + g * 16 + col)) * a.cand_cap +
+                            (uint32_t)kq * (a.cand_cap >> 2));
+    }
+    ql[g] = (uint32_t)(w * QPW + g * 16 + col);
+    qvalid[g] = ql[g] < a.nq_valid;
+    const uint4* qrow = (const uint4*)((const unsigned char*)a.Q + (size_t)ql[g] * RBY);
+#pragma unroll
+    for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
+    th_s[g] = (a.init_score && qvalid[g]) ? a.init_score[ql[g]] : -INFINITY;
+  }
+
+  // VAR 8192: the prologue's loads drained and timed (ablation only)
+  uint64_t tclk1 = 0, tclk2 = 0;
+  if constexpr (kClock) {
+    __builtin_amdgcn_s_waitcnt(0);
+    tclk1 = wall_clock64();
+  }
 
   // A operand read offsets: half hr (tile rows 16hr..16hr+15), lane reads row
   // 16hr + col, 16-B chunk 4*(t&1) + kq of piece t>>1.
@@ -2066,8 +2095,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   }
   __syncthreads();  // lists / counts initialised
   if constexpr (kDma && kBF) {
+    if constexpr (!kEarlyFill) {
 #pragma unroll
-    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
+      for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
+    }
     wait_vmcnt<PPW * (S::AHEAD - 1)>();
   } else {
     if constexpr (kDma)
@@ -2299,8 +2330,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             // can be in the top k (mfma_cand_cap gives sub >= k): exact, with
             // no re-run. Rare path: the slabs are read back from memory.
             // VAR 2097152 (ablation): drops the slab, inexact
-            if constexpr (kRegCnt && (VAR & 2097152) == 0)
+            if constexpr (kRegCnt && (VAR & 2097152) == 0) {
               mf_replace_min(a, slot0[g], sub, acc[0][g], acc[1][g], a.row_base + trow0, mx);
+              // the quarter's maximum never leaves it (a replacement evicts the
+              // smallest), so the running maximum stays exact
+              mf_quarter_max(cntl, g * THREADS, mx);
+            }
           } else if constexpr (kRegCnt) {
             // VAR 262144 (ablation): the appending wave runs at raised
             // priority, so it reaches the next chunk barrier sooner
@@ -2311,6 +2346,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
             cnt_r[g] = cg + 1;
+            mf_quarter_max(cntl, g * THREADS, mx);
             if constexpr ((VAR & 262144) != 0) __builtin_amdgcn_s_setprio(0);
           } else {
             // the address is rebuilt here from an opaque thread id, so none
@@ -2394,6 +2430,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     if constexpr (MODE == 0) {
       a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
           kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
+      if constexpr (kRegCnt)
+        if (a.cand_max)
+          a.cand_max[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
+              cntl[g * THREADS + threadIdx.x];
     } else if constexpr (MODE == 3) {
       // a workgroup with fewer tiles than max_tiles: the rest are empty
       for (uint32_t t = ntiles + kq; t < a.max_tiles; t += 4)
@@ -2537,7 +2577,7 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
                             const float* init_score, float* slabs,
                             uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
-                            hipStream_t st, const uint64_t* allow) {
+                            hipStream_t st, const uint64_t* allow, uint32_t* cand_max) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 * k || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
@@ -2545,7 +2585,7 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.init_score = init_score, a.cand = (uint64_t*)slabs;
-  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt;
+  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.cand_max = cand_max;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
   return mfma_launch_mode<0>(dim, f32, *nlists, a, st);
@@ -2692,8 +2732,8 @@ constexpr uint32_t kSelChunk = kSelHeld * kSelThreads;  // 2048 slabs
 template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
-    const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
-    uint64_t* __restrict__ out, SlabMask fm) {
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ cmax, uint32_t nwg,
+    uint32_t cap, uint32_t k, uint64_t* __restrict__ out, SlabMask fm) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -2704,18 +2744,52 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
   static_assert(4 * kMfmaMaxLists == 2 * kSelThreads, "two lists per thread");
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
-  // lists 2 tid, 2 tid + 1: counts (both loads in flight; past nl: 0)
+  // lists 2 tid, 2 tid + 1: counts and, with cmax, maxima (all loads in
+  // flight at once; past nl: 0)
   const uint32_t l0 = 2 * tid;
-  uint32_t c0 = 0, c1 = 0;
+  uint32_t c0 = 0, c1 = 0, x0 = 0, x1 = 0;
   {
     const uint32_t a0 = l0 < nl ? l0 : 0u, a1 = l0 + 1 < nl ? l0 + 1 : 0u;
-    const uint32_t r0 = cnt[((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3)];
-    const uint32_t r1 = cnt[((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3)];
+    const size_t i0 = ((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3);
+    const size_t i1 = ((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3);
+    const uint32_t r0 = cnt[i0], r1 = cnt[i1];
+    if (cmax) x0 = cmax[i0], x1 = cmax[i1];
     c0 = l0 < nl ? (r0 < sub ? r0 : sub) : 0u;
     c1 = l0 + 1 < nl ? (r1 < sub ? r1 : sub) : 0u;
+    x0 = c0 ? x0 : 0u;
+    x1 = c1 ? x1 : 0u;
   }
   if (tid < kMfmaMaxLists) lmax[tid] = 0;
-  // block exclusive prefix sum of the counts
+  if (tid == 0) fill = 0, spill = 0;
+  // the bound from lmax (per-buffer maxima as keys, row word 0): the k-th
+  // largest has k keys of k distinct rows at or above it. Admit keys > thr.
+  auto bound_from_lmax = [&]() -> uint64_t {
+    if (k <= 64) {
+      if (w == 0) {
+        const uint64_t b = sel_bound_wave(lmax, k, (int)lane);
+        if (lane == 0) thr_sh = b ? b - 1 : 0;
+      }
+      __syncthreads();
+      return thr_sh;
+    }
+    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+    return (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+  };
+  uint64_t thr = 0;
+  if (cmax) {
+    // r04: the main pass recorded each quarter's largest admitted score, so
+    // the per-buffer maxima (and the bound) come without reading a slab, and
+    // only quarters whose maximum passes the bound -- ~k of 4 nwg -- are read
+    // below (any key above the bound lies in one of them)
+    __syncthreads();  // lmax zeroed
+    if (x0) atomicMax((unsigned long long*)&lmax[l0 >> 2], (unsigned long long)x0 << 32);
+    if (x1) atomicMax((unsigned long long*)&lmax[(l0 + 1) >> 2], (unsigned long long)x1 << 32);
+    __syncthreads();
+    thr = bound_from_lmax();
+    if (((uint64_t)x0 << 32) <= thr) c0 = 0;
+    if (((uint64_t)x1 << 32) <= thr) c1 = 0;
+  }
+  // block exclusive prefix sum of the counts (with cmax: of the passing quarters)
   uint32_t incl = c0 + c1;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -2723,7 +2797,6 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     if ((int)lane >= d) incl += y;
   }
   if (lane == 63) wtot[w] = incl;
-  if (tid == 0) fill = 0, spill = 0;
   __syncthreads();
   uint32_t woff = 0, total = 0;
 #pragma unroll
@@ -2776,41 +2849,32 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     for (int u = 0; u < kSelHeld; ++u)
       if (bits[u]) bits[u] = slab_bits(fm, tl[u], ls[u] & 3);
   };
-  // pass 1: per buffer (workgroup) maximum admitted score
-  for (uint32_t base = 0; base < T; base += kSelChunk) {
-    load_chunk(base);
+  if (!cmax) {
+    // pass 1: per buffer (workgroup) maximum admitted score
+    for (uint32_t base = 0; base < T; base += kSelChunk) {
+      load_chunk(base);
 #pragma unroll
-    for (int u = 0; u < kSelHeld; ++u) {
-      float sv[8];
+      for (int u = 0; u < kSelHeld; ++u) {
+        float sv[8];
 #pragma unroll
-      for (int b = 0; b < 8; ++b) sv[b] = ((bits[u] >> b) & 1u) ? v[u][b >> 2][b & 3] : -INFINITY;
-      const float m = fmax3(fmax3(sv[0], sv[1], sv[2]), fmax3(sv[3], sv[4], sv[5]),
-                            fmax3(sv[6], sv[7], -INFINITY));
-      if (m != -INFINITY)
-        atomicMax((unsigned long long*)&lmax[ls[u] >> 2], (unsigned long long)make_key(m, 0xFFFFFFFFu));
-    }
-  }
-  __syncthreads();
-  if constexpr (SV == 1) return;
-  // admit keys > thr: every such key's score reaches thr_s
-  uint64_t thr;
-  if (k <= 64) {
-    if (w == 0) {
-      const uint64_t b = sel_bound_wave(lmax, k, (int)lane);
-      if (lane == 0) thr_sh = b ? b - 1 : 0;
+        for (int b = 0; b < 8; ++b) sv[b] = ((bits[u] >> b) & 1u) ? v[u][b >> 2][b & 3] : -INFINITY;
+        const float m = fmax3(fmax3(sv[0], sv[1], sv[2]), fmax3(sv[3], sv[4], sv[5]),
+                              fmax3(sv[6], sv[7], -INFINITY));
+        if (m != -INFINITY)
+          atomicMax((unsigned long long*)&lmax[ls[u] >> 2],
+                    (unsigned long long)make_key(m, 0xFFFFFFFFu));
+      }
     }
     __syncthreads();
-    thr = thr_sh;
-  } else {
-    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
-    thr = (k <= kMfmaMaxLists && lmax[k - 1] != 0) ? lmax[k - 1] - 1 : 0;
+    if constexpr (SV == 1) return;
+    thr = bound_from_lmax();
   }
   // the bound is a score with the smallest row key, so thr + 1 is its key
   const float thr_s = thr ? key_score(thr + 1) : -INFINITY;
   if constexpr (SV == 2) return;
   // pass 2: keys reaching the bound -> buf (held slabs when one chunk did it)
   for (uint32_t base = 0; base < T; base += kSelChunk) {
-    if (T > kSelChunk) load_chunk(base);
+    if (T > kSelChunk || cmax) load_chunk(base);  // else pass 1's registers hold them
 #pragma unroll
     for (int u = 0; u < kSelHeld; ++u)
 #pragma unroll
@@ -2964,10 +3028,10 @@ static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) 
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
-                               const uint64_t* allow) {
+                               const uint64_t* allow, const uint32_t* cand_max) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
-                     (const f32x4_t*)slabs, slab_tile, cand_cnt, nwg, cap, k, out,
+                     (const f32x4_t*)slabs, slab_tile, cand_cnt, cand_max, nwg, cap, k, out,
                      SlabMask{allow, row_base});
   return hipGetLastError();
 }

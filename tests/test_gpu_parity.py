@@ -679,3 +679,58 @@ def test_gemv_one_launch_equals_three_launches(pkg):
     assert base.keys() == other.keys()
     bad = [key for key in base if base[key] != other[key]]
     assert not bad, bad[:5]
+
+
+_QMAX = r"""
+import json, sys
+import torch                      # first: the library then binds torch's HIP runtime
+import numpy as np
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge
+pkg = ge.load_package()
+out = {}
+with pkg.VectorEngine(device=0) as eng:
+    # candidate MFMA path shapes: 8+ tiles per workgroup (>= 65k rows), both
+    # dtypes, D = 768 / 1024 / 128, k 1 .. 128, filters, a row_base, and
+    # 200k identical rows (every quarter full: the replacement path)
+    for dim, dtype, metric, rows, base in ((768, 1, 1, 1_000_000, 0), (768, 0, 0, 300_000, 0),
+                                           (1024, 1, 0, 400_000, 7000), (128, 1, 1, 2_000_000, 0)):
+        name = f"q{dim}_{dtype}_{rows}"
+        eng.create_collection(name, dim, metric, dtype, rows, base)
+        eng.generate(name, rows, 5)
+        rng = np.random.default_rng(dim + rows)
+        Q = rng.standard_normal((300, dim)).astype(np.float32)
+        allow = rng.random(rows) < 0.3
+        for nq, k in ((256, 10), (300, 1), (64, 50), (200, 100), (33, 128), (2, 10)):
+            s, r, c = eng.search(name, Q[:nq], k)
+            out[f"{name}/{nq}/{k}"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+        s, r, c = eng.search_filtered(name, Q[:128], 20, allow)
+        out[f"{name}/f"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+        eng.drop_collection(name)
+    eng.create_collection("same", 128, 0, 1, 200_000)
+    v = np.random.default_rng(1).standard_normal((1, 128)).astype(np.float32)
+    eng.upsert("same", np.arange(200_000), np.repeat(v, 200_000, axis=0))
+    Q = np.concatenate([v, np.random.default_rng(2).standard_normal((40, 128)).astype(np.float32)])
+    for k in (10, 64, 128):
+        s, r, c = eng.search("same", Q, k)
+        out[f"same/{k}"] = [s.view(np.uint32).tolist(), r.tolist(), c.tolist()]
+print(json.dumps(out))
+"""
+
+
+def test_select_quarter_maxima_equals_full_select(pkg):
+    """r04: the main pass records every candidate quarter's largest score and
+    the slab select reads only the quarters that can hold a top-k key. Its
+    answers must be bit-identical to the select that re-reads every slab
+    (VS_SELECT_QMAX=0): both dtypes, D 128 / 768 / 1024, k 1 .. 128, filters,
+    a row_base, and full quarters (200k identical rows)."""
+    import os
+    base = _run_py(_QMAX)
+    os.environ["VS_SELECT_QMAX"] = "0"
+    try:
+        other = _run_py(_QMAX)
+    finally:
+        os.environ.pop("VS_SELECT_QMAX", None)
+    assert base.keys() == other.keys()
+    bad = [key for key in base if base[key] != other[key]]
+    assert not bad, bad[:5]

@@ -222,3 +222,83 @@ def test_placed_off_first_device(engine, orc, pkg, dtype):
             engine.drop_collection(name)
         except pkg.VSError:
             pass
+
+
+def test_placed_create_drop_race_keeps_balance(pkg):
+    """Concurrent create / drop of the same names on a placed engine (ADVICE
+    r03): a collection is published only once it exists on its device, and
+    only its creating call can withdraw it, so no drop ever takes a
+    half-made one, no orphan stays on a device and the per-device
+    reservation counters never underflow. After the storm every device holds
+    nothing and a fresh create lands by the balance rule."""
+    import threading
+    eng = pkg.VectorEngine(shards=[0, 0], place_collections=True, engine_per_shard=True)
+    errors = []
+
+    def worker(t):
+        for i in range(60):
+            nm = f"race{(t + i) % 3}"
+            try:
+                eng.create_collection(nm, 64, 0, 1, 1000)
+            except pkg.VSError as e:
+                if e.code != -6:  # EXISTS
+                    errors.append(("create", e.code, e.msg))
+            try:
+                eng.drop_collection(nm)
+            except pkg.VSError as e:
+                if e.code != -2:  # NOT_FOUND
+                    errors.append(("drop", e.code, e.msg))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:4]
+        for nm in ("race0", "race1", "race2"):
+            try:
+                eng.drop_collection(nm)
+            except pkg.VSError:
+                pass
+        h = json.loads(eng.health())
+        assert [d["collections"] for d in h["devices"]] == [0, 0], h
+        eng.create_collection("a", 64, 0, 1, 1000)
+        eng.create_collection("b", 64, 0, 1, 1000)
+        h = json.loads(eng.health())
+        assert [d["collections"] for d in h["devices"]] == [1, 1], h
+    finally:
+        eng.close()
+
+
+def test_limit_past_rows_sizes_by_rows(engine, pkg, orc):
+    """A limit far past the collection: the host search sizes its
+    buffers by min(k, rows) and returns every row, zero past them, in the
+    caller's stride k -- no gigabyte allocations for a 300-row collection."""
+    dim, n = 128, 300
+    engine.create_collection("kclamp", dim, 0, 0)
+    try:
+        engine.generate("kclamp", n, orc.SEED_CORPUS)
+        Q = orc.generate(orc.SEED_QUERY, 0, 2, dim)
+        big = 50_000_000  # unclamped: 400 MB of device keys and pinned staging for one query
+        k = 400
+        s, r, c = engine.search("kclamp", Q, k)
+        assert list(c) == [n, n]
+        assert np.all(r[:, n:] == 0) and np.all(s[:, n:] == 0)
+        want = engine.search("kclamp", Q, n)
+        assert np.array_equal(r[:, :n], want[1]) and np.array_equal(s[:, :n], want[0])
+        import ctypes
+        L = pkg.load_library()
+        # one query with a huge k through the C-ABI: the caller's outputs are
+        # sized by k (600 MB on the host); the device side must not scale with it
+        s1 = np.zeros(big, np.float32)
+        r1 = np.zeros(big, np.uint64)
+        c1 = np.zeros(1, np.uint32)
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        q = np.ascontiguousarray(Q[:1], np.float32)
+        rc = L.vs_search(engine.handle, b"kclamp", p(q), 1, dim, big, p(s1), p(r1), p(c1))
+        assert rc == 0, L.vs_last_error()
+        assert int(c1[0]) == n
+        assert np.array_equal(r1[:n], want[1][0]) and not np.any(r1[n:n + 1000])
+    finally:
+        engine.drop_collection("kclamp")

@@ -27,6 +27,8 @@ struct Ctx {
   uint32_t* wgt;
   uint32_t nwg;
   hipEvent_t a, b;
+  float* tmax;  // sample-pass arms
+  uint32_t st;
 };
 
 template <int MODE, int VAR, int G = 2>
@@ -43,6 +45,33 @@ static float run(const Ctx& c, bool bound) {
   for (int i = 0; i < burst; ++i)
     hipLaunchKernelGGL((mfma_topk_kernel<768, MODE, VAR, G>), dim3(c.nwg), dim3(64 * mf_waves(G)),
                        0, 0, a);
+  hipEventRecord(c.b, 0);
+  hipEventSynchronize(c.b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.a, c.b);
+  return ms / burst;
+}
+
+// run() without the main pass's quarter-maxima writes (cand_max = null)
+template <int MODE, int VAR, int G = 2>
+static float run_nq(const Ctx& c, bool bound) {
+  Ctx c2 = c;
+  c2.args.cand_max = nullptr;
+  return run<MODE, VAR, G>(c2, bound);
+}
+
+// the sample pass (MODE 3) over the first st tiles of every workgroup, same
+// burst rule as run(); its arguments are built from the main pass's
+template <int VAR>
+static float run_sample(const Ctx& c, bool) {
+  MfArgs a{};
+  a.X = c.args.X, a.Q = c.args.Q, a.tmax = c.tmax;
+  a.max_tiles = c.st, a.n_rows = c.args.n_rows, a.rows_per_wg = c.args.rows_per_wg;
+  a.nq_valid = 256, a.k = c.args.k;
+  static const int burst = getenv("VS_ABL_BURST") ? atoi(getenv("VS_ABL_BURST")) : 1;
+  hipEventRecord(c.a, 0);
+  for (int i = 0; i < burst; ++i)
+    hipLaunchKernelGGL((mfma_topk_kernel<768, 3, VAR, 2>), dim3(c.nwg), dim3(512), 0, 0, a);
   hipEventRecord(c.b, 0);
   hipEventSynchronize(c.b);
   float ms = 0;
@@ -82,6 +111,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ctile, (size_t)c.nwg * 256 * cap * 4));
   CK(hipMalloc(&tmax, (size_t)c.nwg * 256 * st * 4));
   CK(hipMalloc(&cnt, (size_t)c.nwg * 256 * 4 * 4));
+  uint32_t* qmx;  // the main pass's quarter maxima (r04 select)
+  CK(hipMalloc(&qmx, (size_t)c.nwg * 256 * 4 * 4));
   CK(hipMalloc(&bnd, 256 * 4));
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -104,9 +135,12 @@ int main(int argc, char** argv) {
   MfArgs& g = c.args;
   g.X = X, g.Q = Q, g.init_score = bnd, g.lists = out;
   g.cand = cand, g.cand_tile = ctile, g.cand_cnt = cnt, g.cand_cap = cap;
+  g.cand_max = getenv("VS_ABL_NOQMAX") ? nullptr : qmx;
   g.n_rows = n, g.rows_per_wg = rpw, g.nq_valid = 256, g.k = k;
   c.a = a;
   c.b = b;
+  c.tmax = tmax;
+  c.st = st;
   // An unrolled, predicated candidate append was no faster than the ctz loop;
   // 4-16 sample tiles at 1.25M rows cut the candidates 2-8x but the main pass
   // gained what the sample pass lost (argv[3] overrides the sample tiles).
@@ -178,6 +212,17 @@ int main(int argc, char** argv) {
             {"no-epi G4 pd1", run<1, 2048 + 256, 4>, false, {}},
             {"no-epi G4 ilv", run<1, 2048 + 256 + 4194304, 4>, false, {}},
             {"no-epi G4 pd2 ilv", run<1, 2048 + 256 + 32 + 4194304, 4>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "early")) {
+    // r04: the ring's first chunks issued before the query-fragment prologue
+    // (VAR 8388608) against the product order, main pass and sample pass
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
+            {"main early", run<0, 2048 + 256 + 8388608, 2>, true, {}},
+            {"sample (product)", run_sample<2048 + 256>, false, {}},
+            {"sample early", run_sample<2048 + 256 + 8388608>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "qmax")) {
+    // r04: the main pass writing its quarter maxima (product) or not
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
+            {"main no-qmax", run_nq<0, 2048 + 256, 2>, true, {}}};
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "product")) {
     // the product main pass alone (sample-tile sweeps: argv[3])
     arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}}};
@@ -287,7 +332,8 @@ int main(int argc, char** argv) {
     std::vector<float> tsel;
     for (int r = 0; r < 3 * reps; ++r) {
       hipEventRecord(a, 0);
-      CK(launch_select_slabs((const float*)cand, ctile, cnt, c.nwg, cap, 256, k, out, 0));
+      CK(launch_select_slabs((const float*)cand, ctile, cnt, c.nwg, cap, 256, k, out, 0, 0,
+                             nullptr, c.args.cand_max));
       hipEventRecord(b, 0);
       hipEventSynchronize(b);
       float ms = 0;
@@ -297,12 +343,13 @@ int main(int argc, char** argv) {
     std::sort(tsel.begin(), tsel.end());
     printf("%-16s median %.1f us  min %.1f us\n", "slab select", 1e3 * tsel[tsel.size() / 2],
            1e3 * tsel[0]);
+    const uint32_t* cmx = nullptr;
     auto sv = [&](auto kern, const char* name) {
       std::vector<float> tv;
       for (int r = 0; r < 3 * reps; ++r) {
         hipEventRecord(a, 0);
         hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const f32x4_t*)cand,
-                           (const uint32_t*)ctile, (const uint32_t*)cnt, c.nwg, cap, k, out,
+                           (const uint32_t*)ctile, (const uint32_t*)cnt, cmx, c.nwg, cap, k, out,
                            SlabMask{nullptr, 0});
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
@@ -317,6 +364,11 @@ int main(int argc, char** argv) {
     sv(select_slab_kernel<2>, "sel: + sort");
     sv(select_slab_kernel<3>, "sel: + append");
     sv(select_slab_kernel<0>, "sel: full");
+    if (c.args.cand_max) {  // r04: the main pass's quarter maxima
+      cmx = qmx;
+      sv(select_slab_kernel<0>, "sel: qmax full");
+      cmx = nullptr;
+    }
     const uint32_t nl = 4 * c.nwg, sub = cap / 4;
     std::vector<uint32_t> hcnt((size_t)256 * nl), htile((size_t)c.nwg * 256 * cap);
     std::vector<float> hsl((size_t)c.nwg * 256 * cap * 8);
@@ -389,6 +441,10 @@ int main(int argc, char** argv) {
     for (int burst : {1, 8}) {
       if (clocks("sample", mfma_topk_kernel<768, 3, 8192, 2>, sa, burst)) return 1;
       if (clocks("main", mfma_topk_kernel<768, 0, 8192, 2>, ma, burst)) return 1;
+      if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "early")) {
+        if (clocks("sample early", mfma_topk_kernel<768, 3, 8192 + 8388608, 2>, sa, burst)) return 1;
+        if (clocks("main early", mfma_topk_kernel<768, 0, 8192 + 8388608, 2>, ma, burst)) return 1;
+      }
     }
   }
   std::vector<uint32_t> hc((size_t)c.nwg * 256 * 4);
