@@ -93,6 +93,7 @@ static int vsg_gather_merge_keys(vs_engine* h, const uint64_t* l, uint32_t nq, u
                                  uint32_t k, uint64_t* o, void* st, vsg_err* e) {
 	return vsg_fin(vs_gather_merge_keys(h, l, nq, ki, k, o, st), e);
 }
+static int vsg_runtime_check(vsg_err* e) { return vsg_fin(vs_runtime_check(), e); }
 */
 import "C"
 
@@ -422,6 +423,15 @@ func (e *Engine) Health() (string, error) {
 	var ce C.vsg_err
 	err := check(C.vsg_health(e.h, buf, 4096, &ce), &ce)
 	return C.GoString(buf), err
+}
+
+// RuntimeCheck reports whether this process maps exactly one HIP runtime
+// (vs_runtime_check). A process that also loads another libamdhip64 (e.g. a
+// framework's bundled copy) has two sets of streams with no ordering between
+// them; the device-pointer calls (GatherMergeKeys, ...) then refuse to run.
+func RuntimeCheck() error {
+	var ce C.vsg_err
+	return check(C.vsg_runtime_check(&ce), &ce)
 }
 
 // CommUniqueID makes the RCCL id of a one-process-per-GPU deployment: call it
