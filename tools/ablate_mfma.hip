@@ -219,6 +219,15 @@ int main(int argc, char** argv) {
             {"main early", run<0, 2048 + 256 + 8388608, 2>, true, {}},
             {"sample (product)", run_sample<2048 + 256>, false, {}},
             {"sample early", run_sample<2048 + 256 + 8388608>, false, {}}};
+  } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "lists")) {
+    // r04: the sorted-list pass (MODE 8: per-query top-k lists in LDS, no
+    // sample pass, no select: a merge of nwg lists instead) at large shards,
+    // unbounded and pinned, against the candidate main pass
+    arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
+            {"lists", run<8, 0, 2>, false, {}},
+            {"lists pinned", run<8, 128, 2>, false, {}},
+            {"lists 24k", run<8, 2048, 2>, false, {}},
+            {"lists bounded", run<8, 0, 2>, true, {}}};
   } else if (getenv("VS_ABL_SET") && !strcmp(getenv("VS_ABL_SET"), "qmax")) {
     // r04: the main pass writing its quarter maxima (product) or not
     arms = {{"main (product)", run<0, 2048 + 256, 2>, true, {}},
