@@ -354,7 +354,7 @@ def main():
 
     stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     # every timed step keeps its own result buffer (checked after the timer)
-    ring = max(args.steps, 20, 1)
+    ring = max(args.steps, 100)  # >= every phase's timed steps (the single-query line: 100)
     ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True, ring=ring)
     sharded = shard.ShardedSearch(ls, mg, always_gather=force_dist)
     # the data-path exchange: the engine's own RCCL communicator (all-gather +
@@ -425,8 +425,11 @@ def main():
 
     # secondary: the single-query GEMV line on the same resident corpus
     if not args.no_secondary and batch > 1:
-        steps1 = max(20, args.steps)
-        el1, tm1, outs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 3, dist_on,
+        # 100+ single-query steps after 10 of warmup: at ~2.3 ms each the line
+        # costs a quarter second, and its sampled kernel average (every 4th
+        # launch) then rests on 25+ launches instead of 13
+        steps1 = max(100, args.steps)
+        el1, tm1, outs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 10, dist_on,
                                     stream_fn, 1000)
         r1 = kernel_roofline(hi - lo, dim, elem, 1, k, tm1["scan_ms"], "hbm")
         result["secondary"] = {"workload": "same corpus, single query (GEMV path)",

@@ -18,6 +18,37 @@ G = os.path.join(ROOT, "gpurun_out")
 P = os.path.join(ROOT, "profiles")
 
 
+def pmc_mfma(tag, bid):
+    """MFMA utilisation and clock of the C3 main pass from the counter pass:
+    busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs),
+    clock = GRBM_GUI_ACTIVE / 8 / wall (MI355X_MICROARCH.md 'DVFS give-back')."""
+    f = os.path.join(G, f"{tag}_pmc_mfma_c3", "run_counter_collection.csv")
+    if not os.path.exists(f):
+        return
+    per = {}
+    for r in csv.DictReader(open(f)):
+        if "mfma_topk_kernel<768, 0" not in r["Kernel_Name"]:
+            continue
+        d = per.setdefault(r["Dispatch_Id"], {"wall_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    rows = list(per.values())[3:]  # past the clock-settling first launches
+    if not rows:
+        return
+    def avg(k):
+        return sum(x[k] for x in rows) / len(rows)
+    wall = avg("wall_ns") / 1e9
+    cyc = avg("GRBM_GUI_ACTIVE") / 8
+    busy = avg("SQ_VALU_MFMA_BUSY_CYCLES") / (cyc * 1024)
+    rec = {"kernel": "mfma_topk_kernel<768, 0, 2304, 2, false> (C3 main pass)", "build_id": bid,
+           "launches": len(rows), "wall_ms": round(wall * 1e3, 4),
+           "clock_ghz": round(cyc / wall / 1e9, 3), "mfma_busy_frac": round(busy, 4),
+           "mfma_busy_x_clock_over_peak_clock": round(busy * cyc / wall / 2.4e9, 4),
+           "sq_busy_cycles": avg("SQ_BUSY_CYCLES"), "sq_wave_cycles": avg("SQ_WAVE_CYCLES"),
+           "note": "profiled passes run below the un-profiled clock (MI355X_MICROARCH.md give-back 2)"}
+    json.dump(rec, open(os.path.join(P, f"{tag}_c3_{bid}_pmc_mfma.json"), "w"), indent=1)
+    print(json.dumps(rec))
+
+
 def main():
     tag = sys.argv[1]
     b = json.load(open(os.path.join(G, f"{tag}_bench_c3.json")))
@@ -40,6 +71,18 @@ def main():
     print(f"build {bid}: bench kernel_ms {b['roofline']['kernel_ms']} (frac {b['roofline']['frac']}); "
           f"under rocprof {pr['roofline']['kernel_ms']}; trace mean after 10 launches "
           f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10}")
+    pmc_mfma(tag, bid)
+    fetch = []
+    for cfg in ("c3", "c3b1"):
+        f = os.path.join(G, f"{tag}_pmc_fetch_{cfg}", "run_counter_collection.csv")
+        if os.path.exists(f):
+            dst = os.path.join(P, f"{tag}_{cfg}_{bid}_pmc_fetch.csv")
+            shutil.copy(f, dst)
+            fetch.append(f"{cfg}={dst}")
+    if fetch:
+        import subprocess
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
+                        f"{tag} build {bid}", *fetch], check=True)
     for src, dst in ((f"{tag}_c1_http.jsonl", f"{tag}_c1_http_both_backends.jsonl"),
                      (f"{tag}_rt_floor.json", f"{tag}_c1_rt_floor.json"),
                      (f"{tag}_concurrency_overlap.json", f"{tag}_concurrency_overlap.json")):

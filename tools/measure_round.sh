@@ -3,7 +3,8 @@
 # bench line (C3) with its CPU baseline and oracle parity, the same bench
 # under rocprofv3 (kernel trace + stats; the benched binary's build id in the
 # file names), C1 over HTTP for both backends + the dispatch floor, and the
-# concurrency-overlap trials; EXTRA="c2 c5b256 ..." adds bench configs. Raw
+# concurrency-overlap trials; EXTRA="c2 c5b256 ..." adds bench configs; C3=0,
+# PMC=0, C1=0, CONC=0 skip those parts (to split the batch over calls). Raw
 # output stays in gpurun_out/; tools/collect_round.py copies the records into
 # profiles/. Every GPU step has its own limit; the first failure stops it.
 #   bash tools/measure_round.sh TAG
@@ -13,12 +14,29 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 R="$PWD"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u bench.py > "gpurun_out/${TAG}_bench_c3.json" 2> "gpurun_out/${TAG}_bench_c3.err" || exit 1
-cat "gpurun_out/${TAG}_bench_c3.json"
-cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_c3" -o run --output-format csv \
-  -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/${TAG}_prof_c3.json" 2> "$R/gpurun_out/${TAG}_prof_c3.err" || exit 1
-cd "$R"
+if [ "${C3:-1}" = 1 ]; then
+  timeout -k 10 400 python -u bench.py > "gpurun_out/${TAG}_bench_c3.json" 2> "gpurun_out/${TAG}_bench_c3.err" || exit 1
+  cat "gpurun_out/${TAG}_bench_c3.json"
+  cd /tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_c3" -o run --output-format csv \
+    -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/${TAG}_prof_c3.json" 2> "$R/gpurun_out/${TAG}_prof_c3.err" || exit 1
+  cd "$R"
+fi
+if [ "${PMC:-1}" = 1 ]; then
+  # counters in passes of their own (no trace domains), each under a hard limit:
+  # HBM bytes of the C3 main pass and the C3 single-query scan, then the MFMA
+  # pipe's busy cycles and the clock of the C3 main pass
+  B="--steps 10 --warmup 3 --no-cpu-baseline"
+  cd /tmp
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch_c3" -o run --output-format csv \
+    -- python3 "$R/bench.py" $B --no-secondary > "$R/gpurun_out/${TAG}_pmc_fetch_c3.log" 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch_c3b1" -o run --output-format csv \
+    -- python3 "$R/bench.py" $B --config c3b1 > "$R/gpurun_out/${TAG}_pmc_fetch_c3b1.log" 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+    -d "$R/gpurun_out/${TAG}_pmc_mfma_c3" -o run --output-format csv \
+    -- python3 "$R/bench.py" $B --no-secondary > "$R/gpurun_out/${TAG}_pmc_mfma_c3.log" 2>&1 || exit 1
+  cd "$R"
+fi
 for c in ${EXTRA:-}; do
   timeout -k 10 400 python -u bench.py --config "$c" --no-cpu-baseline > "gpurun_out/${TAG}_bench_$c.json" 2> "gpurun_out/${TAG}_bench_$c.err" || exit 1
   cat "gpurun_out/${TAG}_bench_$c.json"
