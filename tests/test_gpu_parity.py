@@ -343,6 +343,12 @@ def test_bench_small_runs():
         assert line["cpu_baseline"]["cpu_model"] and line["cpu_baseline"]["isa"] in ("avx2", "avx512")
         if cfg == "c3":  # batched config: the BLAS secondary is reported too
             assert line["cpu_baseline"]["batched"]["value"] > 0
+            assert line["secondary"]["steps_verified"] >= 100
+        # r04: every timed step checked after the timer, and the timed batch
+        # checked against the oracle over the whole (300k-row) corpus
+        assert line["steps_verified"] == 3
+        assert line["parity"]["queries_checked"] >= 1 and line["parity"]["violations"] == 0, \
+            line["parity"]
 
 
 def test_large_properties(engine, orc):
@@ -722,15 +728,18 @@ def test_select_quarter_maxima_equals_full_select(pkg):
     """r04: the main pass records every candidate quarter's largest score and
     the slab select reads only the quarters that can hold a top-k key. Its
     answers must be bit-identical to the select that re-reads every slab
-    (VS_SELECT_QMAX=0): both dtypes, D 128 / 768 / 1024, k 1 .. 128, filters,
-    a row_base, and full quarters (200k identical rows)."""
+    (VS_SELECT_QMAX=0), and the one-wave-per-query select (k <= 64, the
+    default) to the block select over the same quarters (VS_SELECT_WAVE=0):
+    both dtypes, D 128 / 768 / 1024, k 1 .. 128, filters, a row_base, and
+    full quarters (200k identical rows: ties past every key buffer)."""
     import os
     base = _run_py(_QMAX)
-    os.environ["VS_SELECT_QMAX"] = "0"
-    try:
-        other = _run_py(_QMAX)
-    finally:
-        os.environ.pop("VS_SELECT_QMAX", None)
-    assert base.keys() == other.keys()
-    bad = [key for key in base if base[key] != other[key]]
-    assert not bad, bad[:5]
+    for var, val in (("VS_SELECT_WAVE", "1"), ("VS_SELECT_WAVE", "0"), ("VS_SELECT_QMAX", "0")):
+        os.environ[var] = val
+        try:
+            other = _run_py(_QMAX)
+        finally:
+            os.environ.pop(var, None)
+        assert base.keys() == other.keys()
+        bad = [key for key in base if base[key] != other[key]]
+        assert not bad, (var, bad[:5])
