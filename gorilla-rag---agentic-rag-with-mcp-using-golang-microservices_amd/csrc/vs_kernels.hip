@@ -2947,147 +2947,6 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Wave select (r04): the select of a query as ONE wave (four queries per
-// workgroup), for k <= 64 with the main pass's quarter maxima (cand_max).
-// The block select's barriers and block-wide prefix sums were most of its
-// ~11 us; here no wave waits on another. Lane l holds workgroups 4l .. 4l+3
-// (quarters 16l .. 16l+15): the bound is sel_bound_wave's (the k-th largest
-// of the lanes' maxima, each over 4 buffers), the quarters that pass it are
-// the block select's, and so are the keys and the answer (bit-identical;
-// tests/test_gpu_parity.py::test_select_quarter_maxima_equals_full_select).
-// Keys past the bound go to a per-wave LDS buffer; a full buffer is sorted
-// and cut to the running top k (adversarial ties), so any count is handled.
-constexpr int kWsWaves = 4;
-constexpr uint32_t kWsDesc = 512;  // slab descriptors per round, per wave
-constexpr uint32_t kWsKeys = 512;  // key buffer per wave
-
-// LDS accesses of one wave in program order, other lanes' stores visible
-__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-// buf[0, n) of one wave sorted descending in place (bitonic over the next
-// power of two, 0-padded; n <= kWsKeys)
-__device__ void wave_sort_lds(uint64_t* buf, uint32_t n, int lane) {
-  uint32_t p2 = 1;
-  while (p2 < n) p2 <<= 1;
-  for (uint32_t i = n + (uint32_t)lane; i < p2; i += 64) buf[i] = 0;
-  wave_fence();
-  for (uint32_t size = 2; size <= p2; size <<= 1)
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = (uint32_t)lane; i < p2 / 2; i += 64) {
-        const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-        const bool desc = (lo & size) == 0;
-        const uint64_t a = buf[lo], b = buf[hi];
-        if ((a < b) == desc) {
-          buf[lo] = b;
-          buf[hi] = a;
-        }
-      }
-      wave_fence();
-    }
-}
-
-__global__ __launch_bounds__(64 * kWsWaves) void select_wave_kernel(
-    const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
-    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ cmax, uint32_t nwg,
-    uint32_t cap, uint32_t nq, uint32_t k, uint64_t* __restrict__ out, SlabMask fm) {
-  __shared__ uint32_t desc_sh[kWsWaves][kWsDesc];
-  __shared__ uint64_t key_sh[kWsWaves][kWsKeys];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t q = blockIdx.x * kWsWaves + (uint32_t)w;
-  if (q >= nq) return;  // a whole wave; nothing below waits on another wave
-  uint32_t* desc = desc_sh[w];
-  uint64_t* keys = key_sh[w];
-  const uint32_t sub = cap >> 2;
-  // counts and maxima of this lane's 16 quarters: 8 loads of 16 B in flight
-  uint32_t c[16], x[16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t wg = 4u * (uint32_t)lane + (uint32_t)i;
-    const bool ok = wg < nwg;
-    const size_t o = ((size_t)(ok ? wg : 0u) * kMfmaQueries + q) * 4;
-    const uint4 cv = *(const uint4*)(cnt + o);
-    const uint4 xv = *(const uint4*)(cmax + o);
-    const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w}, xx[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      c[4 * i + j] = ok ? (cc[j] < sub ? cc[j] : sub) : 0u;
-      x[4 * i + j] = c[4 * i + j] ? xx[j] : 0u;
-    }
-  }
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) m = x[j] > m ? x[j] : m;
-  // the bound: the k-th largest lane maximum (sel_bound_wave's); keys > thr
-  const uint64_t b = shfl64(wave_sort_desc((uint64_t)m << 32, lane), (int)k - 1);
-  uint64_t thr = b ? b - 1 : 0;
-  const float thr_s = thr ? key_score(thr + 1) : -INFINITY;
-  // the quarters whose maximum passes it, and the wave prefix of their slabs
-  uint32_t tot = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (((uint64_t)x[j] << 32) <= thr) c[j] = 0;
-    tot += c[j];
-  }
-  uint32_t incl = tot;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  const uint32_t off = incl - tot, T = (uint32_t)__shfl((int)incl, 63, 64);
-  const uint64_t below = (1ull << lane) - 1;
-  uint32_t nk = 0;  // keys[0, nk), wave-uniform
-  for (uint32_t base = 0; base < T; base += kWsDesc) {
-    // descriptors (quarter << 8 | slot) of this round's slabs
-    uint32_t idx = off;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      for (uint32_t sl = 0; sl < c[j]; ++sl, ++idx)
-        if (idx >= base && idx < base + kWsDesc) desc[idx - base] = ((16u * (uint32_t)lane + (uint32_t)j) << 8) | sl;
-    wave_fence();
-    const uint32_t n = T - base < kWsDesc ? T - base : kWsDesc;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-      const uint32_t i = i0 + (uint32_t)lane;
-      const bool ok = i < n;
-      const uint32_t d = ok ? desc[i] : 0u;
-      const uint32_t l = d >> 8, sl = d & 255u;
-      const size_t e = ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub + sl;
-      const f32x4_t v0 = slabs[2 * e], v1 = slabs[2 * e + 1];
-      const uint32_t t = tiles[e];
-      const uint32_t bits = ok ? slab_bits(fm, t, l & 3) : 0u;
-#pragma unroll
-      for (int bb = 0; bb < 8; ++bb) {
-        if (nk + 64 > kWsKeys) {  // full: keep the running top k, raise the bound
-          wave_fence();
-          wave_sort_lds(keys, nk, lane);
-          nk = nk < k ? nk : k;
-          if (nk == k && keys[k - 1] > thr) thr = keys[k - 1];
-        }
-        const float sc = bb < 4 ? v0[bb] : v1[bb - 4];
-        uint64_t key = 0;
-        if (((bits >> bb) & 1u) && sc >= thr_s) {
-          key = make_key(sc, t + 16u * (uint32_t)(bb >> 2) + 4u * (l & 3) + (uint32_t)(bb & 3));
-          if (key <= thr) key = 0;
-        }
-        const uint64_t bal = __ballot(key != 0);
-        if (key) keys[nk + (uint32_t)__popcll(bal & below)] = key;
-        nk += (uint32_t)__popcll(bal);
-      }
-    }
-    wave_fence();  // this round's descriptors read before the next round's
-  }
-  wave_fence();
-  uint64_t* o = out + (size_t)q * k;
-  if (nk <= 64) {
-    const uint64_t v = wave_sort_desc((uint32_t)lane < nk ? keys[lane] : 0ull, lane);
-    if ((uint32_t)lane < k) o[lane] = v;
-    return;
-  }
-  wave_sort_lds(keys, nk, lane);
-  for (uint32_t j = (uint32_t)lane; j < k; j += 64) o[j] = j < nk ? keys[j] : 0ull;
-}
-
-// ---------------------------------------------------------------------------
 // sample bound: per query, a lower bound on the k-th largest of m tile maxima
 // (k maxima of k distinct tiles: k distinct rows score at least that much, so
 // it bounds the query's global k-th score from below). Radix select on the
@@ -3095,7 +2954,9 @@ __global__ __launch_bounds__(64 * kWsWaves) void select_wave_kernel(
 // + one block scan per pass; one workgroup per query. Two passes: the bound is
 // the lowest value of the 16-bit bucket holding the k-th largest (at least k
 // maxima reach it; it sits below the exact k-th by under 2^-7 relative, which
-// admits a few more rows than the exact value would, for half the passes).
+// admits a few more rows than the exact value would, for half the passes;
+// r04: four passes, the exact k-th maximum, cut the candidates by 5% at 10M
+// rows and did not make the main pass faster, so two stay the default).
 // Fewer than k maxima give -inf: every row is then admitted.
 // ---------------------------------------------------------------------------
 constexpr int kBoundThreads = 256;
@@ -3109,7 +2970,8 @@ __device__ __forceinline__ float unord_f32(uint32_t u) {
 }
 
 __global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
-    const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound) {
+    const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound,
+    int passes) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[kBoundThreads / 64];
   __shared__ uint32_t pick, above;
@@ -3121,7 +2983,7 @@ __global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
   const float* v = tmax + (size_t)q * m;
   uint32_t prefix = 0, kk = k;  // the kk-th largest of the values matching prefix
 #pragma unroll 1
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < passes; ++pass) {
     const int shift = 24 - 8 * pass;
     const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
     hist[tid] = 0;
@@ -3153,10 +3015,23 @@ __global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
   if (tid == 0) bound[q] = prefix <= ord_f32(-INFINITY) ? -INFINITY : unord_f32(prefix);
 }
 
+// Radix passes of the sample bound (VS_BOUND_PASSES, read once; 2 = the
+// 16-bit bucket floor, up to 2^-7 relative under the k-th maximum; 4 = the
+// k-th maximum exactly, a tighter bound: fewer main-pass candidates)
+static int bound_passes() {
+  static const int v = [] {
+    const char* e = getenv("VS_BOUND_PASSES");
+    const int x = e ? atoi(e) : 2;
+    return x < 2 ? 2 : (x > 4 ? 4 : x);
+  }();
+  return v;
+}
+
 hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
                                float* bound, hipStream_t st) {
   if (nq == 0 || nq > kMfmaQueries || k == 0 || k > kMfmaMaxK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sample_bound_kernel, dim3(nq), dim3(kBoundThreads), 0, st, tmax, m, k, bound);
+  hipLaunchKernelGGL(sample_bound_kernel, dim3(nq), dim3(kBoundThreads), 0, st, tmax, m, k, bound,
+                     bound_passes());
   return hipGetLastError();
 }
 
@@ -3166,27 +3041,11 @@ static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) 
 }
 
 
-// k <= 64 with quarter maxima: the wave select (r04; VS_SELECT_WAVE=1 until
-// it has run on the device; read once)
-static bool select_wave() {
-  static const bool v = [] {
-    const char* e = getenv("VS_SELECT_WAVE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
                                const uint64_t* allow, const uint32_t* cand_max) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
-  if (cand_max && k <= 64 && select_wave()) {
-    hipLaunchKernelGGL(select_wave_kernel, dim3((nq + kWsWaves - 1) / kWsWaves),
-                       dim3(64 * kWsWaves), 0, st, (const f32x4_t*)slabs, slab_tile, cand_cnt,
-                       cand_max, nwg, cap, nq, k, out, SlabMask{allow, row_base});
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
                      (const f32x4_t*)slabs, slab_tile, cand_cnt, cand_max, nwg, cap, k, out,
                      SlabMask{allow, row_base});

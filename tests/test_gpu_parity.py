@@ -728,13 +728,11 @@ def test_select_quarter_maxima_equals_full_select(pkg):
     """r04: the main pass records every candidate quarter's largest score and
     the slab select reads only the quarters that can hold a top-k key. Its
     answers must be bit-identical to the select that re-reads every slab
-    (VS_SELECT_QMAX=0), and the one-wave-per-query select (k <= 64, the
-    default) to the block select over the same quarters (VS_SELECT_WAVE=0):
-    both dtypes, D 128 / 768 / 1024, k 1 .. 128, filters, a row_base, and
-    full quarters (200k identical rows: ties past every key buffer)."""
+    (VS_SELECT_QMAX=0): both dtypes, D 128 / 768 / 1024, k 1 .. 128, filters,
+    a row_base, and full quarters (200k identical rows)."""
     import os
     base = _run_py(_QMAX)
-    for var, val in (("VS_SELECT_WAVE", "1"), ("VS_SELECT_WAVE", "0"), ("VS_SELECT_QMAX", "0")):
+    for var, val in (("VS_SELECT_QMAX", "0"),):
         os.environ[var] = val
         try:
             other = _run_py(_QMAX)
