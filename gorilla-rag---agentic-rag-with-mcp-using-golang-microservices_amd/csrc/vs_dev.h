@@ -155,6 +155,53 @@ struct HostSlot {
 };
 
 
+// Upsert staging (r04): two pinned host buffers (vectors + row numbers of one
+// chunk each) and two device buffers, so the host gathers chunk i+1 while
+// chunk i crosses PCIe and is preprocessed; done[j] marks the H2D out of
+// pin[j] complete. Guarded by the owning context's work_mu.
+struct UpsertStage {
+  void* pin[2] = {nullptr, nullptr};
+  size_t pin_bytes = 0;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  bool armed[2] = {false, false};
+  DevBuf vecs[2], rows[2];
+  UpsertStage() = default;
+  UpsertStage(const UpsertStage&) = delete;
+  UpsertStage& operator=(const UpsertStage&) = delete;
+  ~UpsertStage() {
+    for (int j = 0; j < 2; ++j) {
+      if (done[j]) (void)hipEventSynchronize(done[j]);
+      if (pin[j]) (void)hipHostFree(pin[j]);
+      if (done[j]) (void)hipEventDestroy(done[j]);
+    }
+  }
+  // pinned buffers of at least b bytes each (the stage is idle: no H2D pending)
+  hipError_t ensure(size_t b) {
+    for (int j = 0; j < 2; ++j)
+      if (!done[j]) {
+        const hipError_t e = hipEventCreateWithFlags(&done[j], hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+      }
+    if (b <= pin_bytes) return hipSuccess;
+    size_t r = 1ull << 20;  // powers of two from 1 MiB: few re-allocations
+    while (r < b) r <<= 1;
+    b = r;
+    for (int j = 0; j < 2; ++j) {
+      if (armed[j]) (void)hipEventSynchronize(done[j]);  // an earlier call that failed
+      if (pin[j]) (void)hipHostFree(pin[j]);
+      pin[j] = nullptr;
+      armed[j] = false;
+    }
+    pin_bytes = 0;
+    for (int j = 0; j < 2; ++j) {
+      const hipError_t e = hipHostMalloc(&pin[j], b, hipHostMallocDefault);
+      if (e != hipSuccess) return e;
+    }
+    pin_bytes = b;
+    return hipSuccess;
+  }
+};
+
 // A device-resident filter (vs_filter_create): bitmap, popcount and, when
 // selective, the compacted row list. Shared: a search holds its reference
 // until the device has finished with it, so a concurrent drop is safe.
@@ -192,7 +239,8 @@ struct DevEngine {
   std::shared_ptr<DevStore> store;
   std::atomic<int> inflight{0};  // host searches on this context not yet returned
   std::mutex work_mu;  // scratch buffers + stream
-  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound, upsert_vecs, upsert_rows;
+  DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound;
+  std::unique_ptr<UpsertStage> up;  // upsert staging, made at the first upsert
   DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
   DevBuf merge_tmp;                 // first stage of a two-stage GEMV merge
   DevBuf scand;                     // MFMA sample pass tile maxima

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -741,6 +742,7 @@ void close_context(DevEngine* eng) {
   }
   for (hipEvent_t ev : eng->ev_pool) (void)hipEventDestroy(ev);
   eng->host_slots.clear();
+  eng->up.reset();
   (void)hipStreamSynchronize(eng->own);
   if (eng->xev) (void)hipEventDestroy(eng->xev);
   if (eng->own) (void)hipStreamDestroy(eng->own);
@@ -879,6 +881,35 @@ int collection_drop(DevEngine* eng, const char* name) {
   return VS_OK;  // memory released with the last reference
 }
 
+// staging chunk: VS_UPSERT_CHUNK_MB (1..64, default 16; 4 / 8 / 32 measured slower) — an ablation knob
+size_t upsert_chunk_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("VS_UPSERT_CHUNK_MB");
+    const long mb = e ? std::strtol(e, nullptr, 10) : 16;
+    return (size_t)std::min(64L, std::max(1L, mb)) << 20;
+  }();
+  return v;
+}
+
+// memcpy of a large block by up to 4 threads (into pinned staging: one
+// core's copy rate, ~10 GB/s, is below what PCIe takes)
+void copy_parallel(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kSerial = 2ull << 20;
+  if (bytes <= kSerial) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t parts = std::min<size_t>(4, bytes / kSerial + 1);
+  const size_t step = (bytes / parts + 63) & ~(size_t)63;
+  std::vector<std::thread> th;
+  for (size_t p = 1; p < parts; ++p) {
+    const size_t a = p * step, b = std::min(bytes, a + step);
+    if (a < b) th.emplace_back([=] { std::memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min(bytes, step));
+  for (auto& t : th) t.join();
+}
+
 int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
               const uint64_t* rows, const float* vecs) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
@@ -891,19 +922,29 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
     return fail(VS_ERR_DIM_MISMATCH, "Vector dimension error: expected dim: " +
                                          std::to_string(c->dim) + ", got " + std::to_string(dim_in));
   std::unique_lock<std::shared_mutex> wl(c->mu);
-  // last occurrence of each row wins
-  std::vector<std::pair<uint64_t, uint64_t>> order(n);  // (row, index)
-  for (uint64_t i = 0; i < n; ++i) order[i] = {rows[i], i};
-  std::stable_sort(order.begin(), order.end(),
-                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  // Rows in strictly ascending order (an ingest appending its points, a bulk
+  // load) are taken as they are; otherwise the last occurrence of each row
+  // wins, in row order.
+  bool ascending = true;
+  for (uint64_t i = 1; i < n && ascending; ++i) ascending = rows[i - 1] < rows[i];
+  std::vector<std::pair<uint64_t, uint64_t>> order;  // (row, index), sorted
   std::vector<uint64_t> keep_idx;
-  keep_idx.reserve(n);
-  for (uint64_t i = 0; i < n; ++i)
-    if (i + 1 == n || order[i + 1].first != order[i].first) keep_idx.push_back(i);
-  // appended rows must be exactly [rows, rows + m)
+  if (!ascending) {
+    order.resize(n);
+    for (uint64_t i = 0; i < n; ++i) order[i] = {rows[i], i};
+    std::stable_sort(order.begin(), order.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+    keep_idx.reserve(n);
+    for (uint64_t i = 0; i < n; ++i)
+      if (i + 1 == n || order[i + 1].first != order[i].first) keep_idx.push_back(i);
+  }
+  const uint64_t m = ascending ? n : keep_idx.size();
+  auto row_of = [&](uint64_t t) { return ascending ? rows[t] : order[keep_idx[t]].first; };
+  auto src_of = [&](uint64_t t) { return ascending ? t : order[keep_idx[t]].second; };
+  // appended rows must be exactly [rows, rows + m')
   uint64_t expect = c->rows;
-  for (uint64_t t : keep_idx) {
-    const uint64_t r = order[t].first;
+  for (uint64_t t = 0; t < m; ++t) {
+    const uint64_t r = row_of(t);
     if (r >= c->rows) {
       if (r != expect)
         return fail(VS_ERR_INVALID_ARG, "upsert would leave a hole: appended rows must be "
@@ -917,33 +958,44 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
   VS_HIP(use_stream(eng, eng->own), "stream order");
   int rc = grow(eng, *c, expect);
   if (rc != VS_OK) return rc;
-  const uint64_t m = keep_idx.size();
   const uint32_t dim = c->dim;
-  // stream in chunks of <= 64 MiB of fp32 vectors
-  const uint64_t per = std::max<uint64_t>(1, (64ull << 20) / ((uint64_t)dim * 4));
-  std::vector<float> hv;
-  std::vector<uint64_t> hr;
-  for (uint64_t o = 0; o < m; o += per) {
+  const size_t rb = (size_t)dim * 4;
+  // chunks of <= 16 MiB of fp32 vectors + rows, double-buffered through pinned
+  // memory: the host fills chunk i+1 while chunk i crosses PCIe and the
+  // device normalises it (vsk::launch_preprocess, HBM-bound)
+  const uint64_t per =
+      std::min<uint64_t>(m, std::max<uint64_t>(1, upsert_chunk_bytes() / (rb + 8)));
+  if (!eng->up) eng->up = std::make_unique<UpsertStage>();
+  UpsertStage& stg = *eng->up;
+  VS_HIP(stg.ensure(per * rb + per * 8), "alloc pinned upsert staging");
+  for (int j = 0; j < 2; ++j) {
+    VS_HIP(stg.vecs[j].ensure(per * rb), "alloc upsert scratch");
+    VS_HIP(stg.rows[j].ensure(per * 8), "alloc upsert scratch");
+  }
+  int j = 0;
+  for (uint64_t o = 0; o < m; o += per, j ^= 1) {
     const uint64_t cnt = std::min(per, m - o);
-    hv.resize(cnt * dim);
-    hr.resize(cnt);
-    for (uint64_t t = 0; t < cnt; ++t) {
-      const auto& pr = order[keep_idx[o + t]];
-      hr[t] = pr.first;
-      std::memcpy(&hv[t * dim], vecs + pr.second * dim, (size_t)dim * 4);
+    if (stg.armed[j]) VS_HIP(hipEventSynchronize(stg.done[j]), "upsert staging");
+    float* hv = (float*)stg.pin[j];
+    uint64_t* hr = (uint64_t*)((char*)stg.pin[j] + per * rb);
+    if (ascending) {
+      copy_parallel(hv, vecs + o * dim, cnt * rb);
+      std::memcpy(hr, rows + o, cnt * 8);
+    } else {
+      for (uint64_t t = 0; t < cnt; ++t) {
+        hr[t] = row_of(o + t);
+        std::memcpy(&hv[t * dim], vecs + src_of(o + t) * dim, rb);
+      }
     }
-    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
-    VS_HIP(eng->upsert_vecs.ensure(cnt * dim * 4), "alloc upsert scratch");
-    VS_HIP(eng->upsert_rows.ensure(cnt * 8), "alloc upsert scratch");
-    VS_HIP(hipMemcpyAsync(eng->upsert_vecs.p, hv.data(), cnt * dim * 4, hipMemcpyHostToDevice,
-                          eng->stream),
+    VS_HIP(hipMemcpyAsync(stg.vecs[j].p, hv, cnt * rb, hipMemcpyHostToDevice, eng->stream),
            "upsert H2D");
-    VS_HIP(hipMemcpyAsync(eng->upsert_rows.p, hr.data(), cnt * 8, hipMemcpyHostToDevice,
-                          eng->stream),
+    VS_HIP(hipMemcpyAsync(stg.rows[j].p, hr, cnt * 8, hipMemcpyHostToDevice, eng->stream),
            "upsert H2D");
-    VS_HIP(vsk::launch_preprocess(eng->upsert_vecs.as<float>(), (uint32_t)cnt, dim,
+    VS_HIP(hipEventRecord(stg.done[j], eng->stream), "upsert staging");
+    stg.armed[j] = true;
+    VS_HIP(vsk::launch_preprocess(stg.vecs[j].as<float>(), (uint32_t)cnt, dim,
                                   c->metric == VS_METRIC_COSINE, c->dtype == VS_DTYPE_BF16,
-                                  c->data, eng->upsert_rows.as<uint64_t>(), 0, eng->stream),
+                                  c->data, stg.rows[j].as<uint64_t>(), 0, eng->stream),
            "upsert preprocess");
   }
   VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");

@@ -74,6 +74,34 @@ def test_upsert_overwrite_and_duplicates(engine, orc):
     engine.drop_collection("ow")
 
 
+def test_upsert_chunked_staging_bit_exact(engine, orc):
+    """Upserts larger than one 16 MiB staging chunk, through both pinned buffers:
+    an ascending append (the copy-through path), then a shuffled overwrite with
+    duplicates (the sorted path, last occurrence wins), then a small append after
+    the staging has grown — every stored row bit-exact with the oracle's
+    preprocess (rag/vector-service/main.go:165-182 → Qdrant upsert)."""
+    rng = np.random.default_rng(21)
+    dim, n = 256, 100_000  # 16 MiB / (1 KiB + 8 B) = 16,256 rows per chunk: 7 chunks
+    engine.create_collection("chunked", dim, 0, 1)
+    try:
+        X = (rng.standard_normal((n, dim)) * rng.uniform(0.1, 10, (n, 1))).astype(np.float32)
+        engine.upsert("chunked", np.arange(n, dtype=np.uint64), X)
+        ids = rng.integers(0, n, 70_000).astype(np.uint64)  # duplicates included
+        Y = rng.standard_normal((len(ids), dim)).astype(np.float32)
+        engine.upsert("chunked", ids, Y)
+        exp = X.copy()
+        u, first = np.unique(ids[::-1], return_index=True)
+        exp[u] = Y[len(ids) - 1 - first]  # the last occurrence of each row wins
+        Z = rng.standard_normal((5, dim)).astype(np.float32)
+        engine.upsert("chunked", np.arange(n, n + 5), Z)
+        exp = np.concatenate([exp, Z])
+        got = engine.read_rows("chunked", 0, n + 5)
+        ref = orc.preprocess(exp, True, True)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    finally:
+        engine.drop_collection("chunked")
+
+
 # ------------------------------------------------------------- search side
 @pytest.fixture(scope="module")
 def corpora(engine, orc):
