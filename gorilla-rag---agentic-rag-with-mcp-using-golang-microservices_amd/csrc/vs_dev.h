@@ -71,10 +71,25 @@ struct Collection {
   void* data = nullptr;  // cap x dim elements
   uint64_t rows = 0, cap = 0;
   std::shared_mutex mu;
+  // int8 prefilter copy (r04, vs_kernels.h "int8 prefilter"): bf16
+  // collections of q8_supported dims once they take the batched pass; kept
+  // in step with `data` by every store-side call (q8_after_write)
+  void* q8 = nullptr;         // (q8_cap + kPadRows) x dim int8
+  float* q8_meta = nullptr;   // {dt, nt} per 32-row tile
+  float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}
+  uint64_t q8_cap = 0;        // rows the int8 buffers hold
+  uint64_t q8_scaled_at = 0;  // rows when S was last chosen (rescaled at 2x)
   size_t elem() const { return dtype == VS_DTYPE_BF16 ? 2 : 4; }
   size_t row_bytes() const { return elem() * dim; }
+  void q8_free() {
+    if (q8) (void)hipFree(q8);
+    if (q8_meta) (void)hipFree(q8_meta);
+    if (q8_glob) (void)hipFree(q8_glob);
+    q8 = nullptr, q8_meta = nullptr, q8_glob = nullptr, q8_cap = 0, q8_scaled_at = 0;
+  }
   ~Collection() {
     if (data) (void)hipFree(data);
+    q8_free();
   }
 };
 
@@ -241,6 +256,8 @@ struct DevEngine {
   std::mutex work_mu;  // scratch buffers + stream
   DevBuf q_in, q_pre, q_bf16, lists, keys, sample_bound;
   std::unique_ptr<UpsertStage> up;  // upsert staging, made at the first upsert
+  DevBuf q8_q, q8_par, q8_tiles;    // int8 prefilter: int8 queries, {sqS, a, c, sigma} + gate,
+                                    // tiles an upsert touched
   DevBuf cand, cand_cnt;            // MFMA main pass candidates (vs_kernels.h)
   DevBuf merge_tmp;                 // first stage of a two-stage GEMV merge
   DevBuf scand;                     // MFMA sample pass tile maxima

@@ -174,6 +174,78 @@ int grow(DevEngine* eng, Collection& c, uint64_t need) {
   return VS_OK;
 }
 
+// ---- int8 prefilter copy (vs_kernels.h "int8 prefilter") ------
+// On by default; VS_Q8=0 (read once) makes no copy, and batched searches then
+// read the bf16 rows only.
+bool q8_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// A collection keeps an int8 copy once its batched searches take the
+// candidate pass (8 or more tiles per workgroup) -- bf16, q8_supported dims.
+bool q8_wanted(const Collection& c) {
+  return q8_enabled() && c.dtype == VS_DTYPE_BF16 && vsk::q8_supported(c.dim) &&
+         c.rows < 0xFFFFFFFFull && vsk::mfma_tiles_per_wg((uint32_t)c.rows) >= 8;
+}
+
+// Brings the int8 copy up to date after a store-side write of rows [r0, r1)
+// (or, with d_tiles, of the nt tiles listed there), on eng->stream, the
+// writer lock and work_mu held, c.rows already counting the new rows. The
+// whole copy is rebuilt -- a new scale S from max |x| -- when it is first made,
+// when the collection's buffer grew, and whenever the rows have doubled since
+// S was chosen (rows quantised with an older S stay exact: their error
+// bounds are measured, not assumed). No memory for the copy: none is kept,
+// and batched searches read the bf16 rows.
+int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
+                   const uint32_t* d_tiles = nullptr, uint32_t nt = 0) {
+  if (!q8_wanted(c)) return VS_OK;
+  const uint32_t dim = c.dim;
+  const uint32_t rows = (uint32_t)c.rows;
+  const bool full = !c.q8 || c.q8_cap < c.cap || c.rows >= 2 * c.q8_scaled_at;
+  if (full) {
+    if (c.q8_cap < c.cap) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");  // no pass reads the old copy
+      c.q8_free();
+      const uint64_t tiles = (c.cap + kPadRows) / 32 + 1;
+      hipError_t e = hipMalloc(&c.q8, (c.cap + kPadRows) * dim);
+      if (e == hipSuccess) e = hipMalloc((void**)&c.q8_meta, tiles * 8);
+      if (e == hipSuccess) e = hipMalloc((void**)&c.q8_glob, 16);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        c.q8_free();
+        return VS_OK;
+      }
+      c.q8_cap = c.cap;
+      VS_HIP(hipMemsetAsync(c.q8, 0, (c.cap + kPadRows) * dim, eng->stream), "zero int8 copy");
+    }
+    VS_HIP(hipMemsetAsync(c.q8_glob, 0, 16, eng->stream), "zero int8 bounds");
+    VS_HIP(vsk::launch_q8_absmax((const uint16_t*)c.data, (uint64_t)rows * dim, c.q8_glob,
+                                 eng->stream),
+           "int8 scale");
+    VS_HIP(vsk::launch_q8_set_scale(c.q8_glob, eng->stream), "int8 scale");
+    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, nullptr, 0,
+                                   (rows + 31) / 32, (int8_t*)c.q8, c.q8_meta, c.q8_glob,
+                                   eng->stream),
+           "int8 copy");
+    c.q8_scaled_at = c.rows;
+    return VS_OK;
+  }
+  if (d_tiles) {
+    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, d_tiles, 0, nt,
+                                   (int8_t*)c.q8, c.q8_meta, c.q8_glob, eng->stream),
+           "int8 copy");
+  } else if (r1 > r0) {
+    const uint32_t t0 = (uint32_t)(r0 / 32), t1 = (uint32_t)((r1 - 1) / 32) + 1;
+    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, nullptr, t0, t1 - t0,
+                                   (int8_t*)c.q8, c.q8_meta, c.q8_glob, eng->stream),
+           "int8 copy");
+  }
+  return VS_OK;
+}
 
 // ---- snapshot file format (include/vsearch.h vs_snapshot) -------------------
 struct SnapHeader {
@@ -464,22 +536,30 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows, dim, f32);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
+  // int8 prefilter (unfiltered batches of a collection with an int8 copy)
+  const bool q8 = fast && !allow && c.q8 && c.q8_cap >= c.rows && q8_enabled();
+  const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st, 4.0) : 0;
+  const uint32_t capx = std::max(cap, cap8);
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds
   // main pass slabs: 32 B of scores + a 4-B tile row per slot
-  const size_t slots = (size_t)maxl * PS * cap;
+  const size_t slots = (size_t)maxl * PS * capx;
   const size_t cbytes = slots * 36;
   const size_t scbytes = (size_t)maxl * st * PS * 4;  // tile maxima, [query][wg * st]
   // counts [maxl][PS][4], then (select_qmax) the quarters' maxima, same shape
   const size_t nbytes = (size_t)maxl * PS * 4 * 4 * 2;
+  const size_t q8qb = q8 ? (size_t)PS * dim : 0, q8pb = q8 ? (size_t)PS * 16 + 64 : 0;
   if (eng->lists.bytes < lbytes || eng->sample_bound.bytes < sbytes || eng->cand.bytes < cbytes ||
-      eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes) {
+      eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes || eng->q8_q.bytes < q8qb ||
+      eng->q8_par.bytes < q8pb) {
     VS_HIP(hipStreamSynchronize(eng->stream), "sync");
     VS_HIP(eng->lists.ensure(lbytes), "alloc list scratch");
     VS_HIP(eng->sample_bound.ensure(sbytes), "alloc sample bounds");
     VS_HIP(eng->cand.ensure(cbytes), "alloc candidate scratch");
     VS_HIP(eng->scand.ensure(scbytes), "alloc sample tile maxima");
     VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
+    VS_HIP(eng->q8_q.ensure(q8qb), "alloc int8 queries");
+    VS_HIP(eng->q8_par.ensure(q8pb), "alloc int8 query bounds");
   }
   const void* X = c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
@@ -509,13 +589,44 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // 1. sample pass -> tile maxima -> per-query bound (k-th largest maximum)
     float* bound = eng->sample_bound.as<float>();
     float* tmax = eng->scand.as<float>();
+    int8_t* q8q = q8 ? eng->q8_q.as<int8_t>() : nullptr;
+    float* q8par = q8 ? eng->q8_par.as<float>() : nullptr;
+    uint32_t* gate = q8 ? (uint32_t*)(q8par + 4 * PS) : nullptr;
+    if (q8)
+      VS_HIP(vsk::launch_q8_query((const uint16_t*)qb, nv, dim, c.q8_glob, q8q, q8par, gate,
+                                  eng->stream),
+             "int8 queries");
     VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qb, nv, k, st, tmax, maxl, &L,
                                    eng->stream, allow),
            "mfma sample scan");
     VS_HIP(vsk::launch_sample_bound(tmax, L * st, nv, k, bound, eng->stream), "sample bound");
+    uint32_t* qmax = select_qmax() ? eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4 : nullptr;
+    if (q8) {
+      // 2'. int8 pass -> bounded candidates -> rescored top k; the bf16 pass and
+      // select behind it run only if the int8 pass overflowed (*gate)
+      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
+                                      c.q8_glob, slabs, slab_tile, cap8,
+                                      eng->cand_cnt.as<uint32_t>(), maxl, &L, gate, eng->stream),
+             "int8 scan");
+      VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      VS_HIP(vsk::launch_select_q8(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap8, nv, k,
+                                   out, row_base, (const uint16_t*)X, (const uint16_t*)qb, dim,
+                                   q8par, c.q8_glob, c.q8_meta, bound, gate, eng->stream),
+             "int8 select");
+      VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
+                                   slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl, &L,
+                                   eng->stream, nullptr, qmax, gate),
+             "mfma scan (int8 fallback)");
+      VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
+                                      k, out, eng->stream, row_base, nullptr, qmax, gate),
+             "select (int8 fallback)");
+      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+      continue;
+    }
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-    uint32_t* qmax = select_qmax() ? eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4 : nullptr;
     VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
                                  slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl,
                                  &L, eng->stream, allow, qmax),
@@ -998,8 +1109,30 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
                                   c->data, stg.rows[j].as<uint64_t>(), 0, eng->stream),
            "upsert preprocess");
   }
-  VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");
+  const uint64_t old_rows = c->rows;
   c->rows = expect;
+  if (q8_wanted(*c)) {
+    // the tiles this call wrote: one range for rows in ascending order, else
+    // the distinct tiles of the (row-sorted) kept rows
+    if (ascending) {
+      rc = q8_after_write(eng, *c, rows[0], rows[n - 1] + 1);
+    } else {
+      std::vector<uint32_t> tl;
+      for (uint64_t t = 0; t < m; ++t) {
+        const uint32_t ti = (uint32_t)(row_of(t) / 32);
+        if (tl.empty() || tl.back() != ti) tl.push_back(ti);
+      }
+      VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");  // q8_tiles is free
+      VS_HIP(eng->q8_tiles.ensure(tl.size() * 4), "alloc tile list");
+      VS_HIP(hipMemcpyAsync(eng->q8_tiles.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice,
+                            eng->stream),
+             "tile list H2D");
+      rc = q8_after_write(eng, *c, 0, 0, eng->q8_tiles.as<uint32_t>(), (uint32_t)tl.size());
+    }
+    (void)old_rows;
+    if (rc != VS_OK) return rc;
+  }
+  VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");
   return VS_OK;
 }
 
@@ -1022,8 +1155,10 @@ int generate(DevEngine* eng, const char* coll, uint64_t n, uint64_t seed, uint64
   VS_HIP(vsk::launch_generate(seed, g0, n, c->dim, c->dtype == VS_DTYPE_BF16, c->data, c->rows,
                               eng->stream, stride),
          "generate");
-  VS_HIP(hipStreamSynchronize(eng->stream), "generate sync");
   c->rows += n;
+  rc = q8_after_write(eng, *c, c->rows - n, c->rows);
+  if (rc != VS_OK) return rc;
+  VS_HIP(hipStreamSynchronize(eng->stream), "generate sync");
   return VS_OK;
 }
 
@@ -1103,8 +1238,10 @@ int append_raw(DevEngine* eng, const char* coll, uint64_t n, const void* rows) {
   VS_HIP(hipMemcpyAsync((char*)c->data + c->rows * c->row_bytes(), rows, n * c->row_bytes(),
                         hipMemcpyHostToDevice, eng->stream),
          "restore H2D");
-  VS_HIP(hipStreamSynchronize(eng->stream), "restore sync");
   c->rows += n;
+  rc = q8_after_write(eng, *c, c->rows - n, c->rows);
+  if (rc != VS_OK) return rc;
+  VS_HIP(hipStreamSynchronize(eng->stream), "restore sync");
   return VS_OK;
 }
 
@@ -1690,7 +1827,8 @@ int restore(DevEngine* eng, const char* coll, const char* path) {
     }
     if (err == VS_OK) {
       c->rows = h.rows;
-      err = device_checksum(eng, *c, &sum);
+      err = q8_after_write(eng, *c, 0, c->rows);
+      if (err == VS_OK) err = device_checksum(eng, *c, &sum);
       if (err != VS_OK) msg = last_error();
       else if (sum != h.data_checksum) {
         err = VS_ERR_IO;

@@ -196,7 +196,7 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
                             uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
                             hipStream_t st, const uint64_t* allow = nullptr,
-                            uint32_t* cand_max = nullptr);
+                            uint32_t* cand_max = nullptr, const uint32_t* run_if = nullptr);
 hipError_t launch_mfma_lists(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                              uint32_t row_base, const void* Q, uint32_t nq_valid,
                              uint32_t k, const float* init_score, uint64_t* lists,
@@ -210,11 +210,55 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base = 0,
                                const uint64_t* allow = nullptr,
-                               const uint32_t* cand_max = nullptr);
+                               const uint32_t* cand_max = nullptr,
+                               const uint32_t* run_if = nullptr);
+// run_if (nullable, both launches above): the launch does nothing unless
+// *run_if != 0 -- the bf16 pass standing behind the int8 prefilter.
+
+// int8 prefilter (r04, DESIGN.md §5 "int8 prefilter"): bf16 collections
+// keep an int8 copy X8 (x ~ S * x8, one scale S per collection) and per
+// 32-row tile {dt, nt} = the largest |x - S x8| and |x| of its rows, rounded
+// up; glob = {absmax, dmax, nmax, S}. The main pass runs on
+// v_mfma_i32_16x16x64_i8 (twice the bf16 rate, half the bytes) against int8
+// queries Q8 with per-query {sqS, a, c, sigma} (q8par) and admits every row
+// whose upper bound on its fp32 score reaches the sample bound;
+// launch_select_q8 bounds, rescores the survivors from the bf16 rows and
+// writes the top k. Any overflow (a full quarter, too many survivors) sets
+// *gate, and the bf16 pass + select enqueued behind with run_if = gate
+// answer the batch instead. Exact: the answer is the bf16 pass's.
+bool q8_supported(uint32_t dim);
+hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                               const void* Q8, uint32_t nq_valid, uint32_t k,
+                               const float* init_score, const float* q8par, const float* q8glob,
+                               float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
+                               uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
+                               uint32_t* gate, hipStream_t st);
+hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
+                            uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out,
+                            uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
+                            const float* q8par, const float* q8glob, const float* meta,
+                            const float* bound, uint32_t* gate, hipStream_t st);
+// Store side (vs_q8.hip): glob[0] = max |x| over n bf16 values (atomic max;
+// zero it first); glob[3] = S = glob[0] / 127 (1 when 0).
+hipError_t launch_q8_absmax(const uint16_t* X, uint64_t n, float* glob, hipStream_t st);
+hipError_t launch_q8_set_scale(float* glob, hipStream_t st);
+// Requantise whole 32-row tiles (tiles[i] if non-null, else t0 + i; rows past
+// n_rows are written as zeros) with the scale glob[3]: X8, meta[tile] = {dt,
+// nt}, and glob[1], glob[2] raised to the tiles' maxima.
+hipError_t launch_q8_quantize(const uint16_t* X, uint32_t n_rows, uint32_t dim,
+                              const uint32_t* tiles, uint32_t t0, uint32_t ntiles, int8_t* X8,
+                              float* meta, float* glob, hipStream_t st);
+// Queries (bf16, nq x dim) -> int8 rows Q8 and q8par[q] = {sq * S, |sq q8|,
+// |q - sq q8|, sigma}, norms rounded up.
+// Also zeroes *gate (the batch's overflow word) ahead of the int8 pass.
+hipError_t launch_q8_query(const uint16_t* qb, uint32_t nq, uint32_t dim, const float* glob,
+                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows, uint32_t dim = 768, bool f32 = false);
-uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles);
+// (scale: expected survivors relative to the bf16 pass's; the int8 pass
+// admits ~4x as many rows, its upper bounds being looser than exact scores)
+uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles, double scale = 1.0);
 uint32_t mfma_max_lists(uint32_t n_rows);
 uint32_t mfma_tiles_per_wg(uint32_t n_rows);
 void mfma_grid(uint32_t n_rows, uint32_t* nwg, uint32_t* rows_per_wg);

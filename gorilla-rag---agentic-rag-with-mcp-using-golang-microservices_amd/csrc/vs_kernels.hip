@@ -16,6 +16,7 @@
 //   * merge_keys_kernel — global top-k over per-workgroup / per-shard lists.
 // Store side (upsert, Qdrant cosine preprocess) and the synthetic generator
 // are here too. Numerics contract: include/vsearch.h and DESIGN.md.
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <hip/hip_runtime.h>
@@ -1632,6 +1633,7 @@ constexpr int kMfRingBytes = 112 * 1024;
 static_assert(kMfmaListMaxK == 16, "list insert assumes 4 lanes x 4 entries per query");
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
 // Kernel arguments (one struct, passed by value in the kernarg segment).
 struct MfArgs {
@@ -1649,6 +1651,16 @@ struct MfArgs {
   const uint64_t* allow;    // nullable: filter pre-mask, bit r admits local row r
   uint32_t n_rows, row_base, rows_per_wg, max_tiles, nq_valid, k, cand_cap;
   const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
+  // int8 prefilter pass (I8, r04; DESIGN.md §5 "int8 prefilter"): per query
+  // {sqS, a, c, sigma} (q8par, float4) and the collection's {-, dmax, nmax, S}
+  // (q8glob) turn the sample bound into an integer dot threshold; a full
+  // quarter raises *gate (the batch is then answered by the bf16 pass).
+  const float* q8par;
+  const float* q8glob;
+  uint32_t* gate;
+  // nullable: the launch does nothing unless *run_if != 0 (the bf16 pass and
+  // select that stand behind the int8 pass, enqueued every batch)
+  const uint32_t* run_if;
 };
 
 // XOR swizzle of the 16-B chunk inside a 128-B row piece: spreads the
@@ -1764,6 +1776,29 @@ __device__ __forceinline__ void mf_insert(uint32_t m, KeyOf key_of, lds_vu64_t* 
       }
     }
   }
+}
+
+__device__ __forceinline__ int imax3(int a, int b, int c) {
+  return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
+}
+
+// I8 main pass: the integer dot threshold of query q. Rows whose upper bound
+// U = sqS * dot + a * dmax + (c + sigma) * nmax is below b - sigma * nmax
+// (b: the sample bound, a lower bound on the k-th score as computed by an
+// fp32 pass) cannot be in the top k ("int8 prefilter"), so
+// dot >= (b - a dmax - (c + 2 sigma) nmax) / sqS admits every row that can;
+// one unit lower absorbs the float rounding of this expression.
+template <typename Args>
+__device__ __forceinline__ int q8_dot_threshold(const Args& a, uint32_t q, bool valid, float b) {
+  if (!valid) return INT_MAX;
+  if (b == -INFINITY) return INT_MIN + 2;  // no bound: every row
+  const f32x4_t p = ((const f32x4_t*)a.q8par)[q];  // sqS, a, c, sigma
+  const float dmax = a.q8glob[1], nmax = a.q8glob[2];
+  if (!(p[0] > 0.f)) return INT_MIN + 2;  // a zero query: every dot is 0
+  const float t = (b - p[1] * dmax - (p[2] + 2.f * p[3]) * nmax) / p[0] - 1.f;
+  if (t <= -1073741824.f) return INT_MIN + 2;
+  if (t >= 1073741824.f) return 1073741824;
+  return (int)floorf(t);
 }
 
 // Raises this lane's running quarter maximum (LDS word `base` + tid of the
@@ -1889,11 +1924,13 @@ struct MfShape {
 // fp32 accumulation; 1/16 of the bf16 rate, so the pass is MFMA-bound): same
 // stream, layout and epilogue, a step's 16-B fragment holding 4 k of each
 // lane's k-quarter, consumed by four MFMAs.
-template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D), bool F32 = false>
+template <int D, int MODE = 0, int VAR = 0, int G = mf_groups(D), bool F32 = false, bool I8 = false>
 __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_waves(G)) void mfma_topk_kernel(
     const MfArgs a) {
   constexpr int WAVES = mf_waves(G), THREADS = 64 * WAVES, QPW = 16 * G;
-  constexpr int EB = F32 ? 4 : 2;
+  constexpr int EB = F32 ? 4 : (I8 ? 1 : 2);
+  static_assert(!I8 || (!F32 && (MODE == 0 || MODE == 1 || MODE == 6)), "int8: the main pass only");
+  if (a.run_if && *a.run_if == 0u) return;  // uniform: the whole launch stands down
   constexpr int RBY = D * EB;
   static_assert(WAVES * QPW <= (int)kMfmaQueries, "one launch covers <= kMfmaQueries");
   static_assert(G * (RBY / 64) * 4 <= (mf_waves(G) == 4 ? 400 : 192),
@@ -2036,6 +2073,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   uint32_t ql[G];
   bool qvalid[G];
   float th_s[G];     // admit rows whose score reaches th_s
+  int th_i[G];       // I8: admit rows whose int8 dot reaches th_i
   // cntl[g * THREADS + tid]: keys this lane appended to its quarter of the
   // query's buffer (candidate passes). The main pass keeps the counts and
   // each lane's first slot in registers instead (no LDS round trip and no
@@ -2061,6 +2099,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
     for (int t = 0; t < S::T; ++t) qf[g][t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
     th_s[g] = (a.init_score && qvalid[g]) ? a.init_score[ql[g]] : -INFINITY;
+    if constexpr (I8) th_i[g] = q8_dot_threshold(a, ql[g], qvalid[g], th_s[g]);
   }
 
   // VAR 8192: the prologue's loads drained and timed (ablation only)
@@ -2225,8 +2264,15 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
                 // row half 1 reuses half 0's fragment against the next step's
                 // query fragment (a distinct chain, so nothing merges)
                 const int qs = MODE == 13 && hr == 1 ? (sig + 1) % S::T : sig;
-                acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][qs], acc[hr][g], 0,
-                                                                     0, 0);
+                if constexpr (I8)  // 64 int8 k per step; exact int32 sums (bits kept in acc)
+                  acc[hr][g] = __builtin_bit_cast(
+                      f32x4_t, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                   __builtin_bit_cast(i32x4_t, av),
+                                   __builtin_bit_cast(i32x4_t, qf[g][qs]),
+                                   __builtin_bit_cast(i32x4_t, acc[hr][g]), 0, 0, 0));
+                else
+                  acc[hr][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, qf[g][qs], acc[hr][g], 0,
+                                                                       0, 0);
               }
             }
           }
@@ -2281,6 +2327,48 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             for (int g = 0; g < G; ++g)
               acc[hr][g][i] = ((am >> (hr * 4 + i)) & 1u) ? acc[hr][g][i] : -INFINITY;
       }
+    }
+    if constexpr (I8 && MODE == 0) {
+      // int8 prefilter: a lane whose largest dot of the tile reaches the
+      // query's integer threshold appends its 8 dots (int32 bits) -- the
+      // select bounds and rescores them. No filter on this pass.
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
+        // one ext_vector element (it reads element 0; tools/q8_check.hip found it)
+        const i32x4_t a0 = __builtin_bit_cast(i32x4_t, acc[0][g]);
+        const i32x4_t a1 = __builtin_bit_cast(i32x4_t, acc[1][g]);
+        int v[8];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
+        if (!full) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1) v[b] = INT_MIN;
+          acc[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
+          acc[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
+        }
+        const int mx = imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
+        if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
+          const uint32_t sub = a.cand_cap >> 2;
+          const uint32_t cg = cnt_r[g];
+          if (cg >= sub) {
+            if (a.gate) a.gate[0] = 1u;  // a full quarter: the bf16 pass answers
+          } else {
+            const size_t slot = (size_t)slot0[g] + cg;
+            f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
+            sp[0] = acc[0][g];
+            sp[1] = acc[1][g];
+            a.cand_tile[slot] = a.row_base + trow0;
+            cnt_r[g] = cg + 1;
+          }
+        }
+      }
+      return;
+    } else if constexpr (I8) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) asm volatile("" ::"v"(acc[0][g][0]), "v"(acc[1][g][3]));
+      return;
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -2577,7 +2665,8 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
                             const float* init_score, float* slabs,
                             uint32_t* slab_tile, uint32_t cand_cap,
                             uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
-                            hipStream_t st, const uint64_t* allow, uint32_t* cand_max) {
+                            hipStream_t st, const uint64_t* allow, uint32_t* cand_max,
+                            const uint32_t* run_if) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || cand_cap < 4 * k || cand_cap % 4 ||
       cand_cap > kMfmaMaxCandCap)
     return hipErrorInvalidValue;
@@ -2588,16 +2677,55 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
   a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.cand_max = cand_max;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap, a.allow = allow;
+  a.run_if = run_if;
   return mfma_launch_mode<0>(dim, f32, *nlists, a, st);
 }
 
-uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles) {
+// int8 prefilter pass (r04): D = 768 rows of int8 (768 B, whole-row 24 KiB
+// K-chunks through the 144 KiB ring), 256 queries, no filter.
+bool q8_supported(uint32_t dim) { return dim == 768; }
+
+template <int VAR>
+static hipError_t launch_q8_var(uint32_t nwg, const MfArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((mfma_topk_kernel<768, 0, VAR, 2, false, true>), dim3(nwg), dim3(512), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                               const void* Q8, uint32_t nq_valid, uint32_t k,
+                               const float* init_score, const float* q8par, const float* q8glob,
+                               float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
+                               uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
+                               uint32_t* gate, hipStream_t st) {
+  if (!q8_supported(dim) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
+      cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate)
+    return hipErrorInvalidValue;
+  MfArgs a{};
+  mfma_grid(n_rows, nlists, &a.rows_per_wg);
+  if (*nlists > max_lists) return hipErrorInvalidValue;
+  a.X = X8, a.Q = Q8, a.init_score = init_score, a.cand = (uint64_t*)slabs;
+  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt;
+  a.n_rows = n_rows, a.row_base = row_base;
+  a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
+  a.q8par = q8par, a.q8glob = q8glob, a.gate = gate;
+  static const int var = [] {
+    const char* e = getenv("VS_Q8_VAR");
+    return e ? atoi(e) : 2048 + 256;
+  }();
+  switch (var) {
+    case 0: return launch_q8_var<0>(*nlists, a, st);
+    case 256: return launch_q8_var<256>(*nlists, a, st);
+    default: return launch_q8_var<2048 + 256>(*nlists, a, st);
+  }
+}
+
+uint32_t mfma_cand_cap(uint32_t n_rows, uint32_t k, uint32_t sample_tiles, double scale) {
   uint32_t nwg, rpw;
   mfma_grid(n_rows, &nwg, &rpw);
   const double tpw = (rpw + 31) / 32;
   // expected survivors of the sample bound per (workgroup, query): the bound
   // is the k-th of ~k / f rows (f = sampled fraction), spread over nwg
-  const double e = (double)k * tpw / (double)(sample_tiles ? sample_tiles : 1) / nwg;
+  const double e = scale * (double)k * tpw / (double)(sample_tiles ? sample_tiles : 1) / nwg;
   const double want = 3.0 * e + 32.0;
   uint32_t cap = 64;
   while (cap < want && cap < kMfmaMaxCandCap) cap <<= 1;
@@ -2733,7 +2861,9 @@ template <int SV = 0>
 __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ cmax, uint32_t nwg,
-    uint32_t cap, uint32_t k, uint64_t* __restrict__ out, SlabMask fm) {
+    uint32_t cap, uint32_t k, uint64_t* __restrict__ out, SlabMask fm,
+    const uint32_t* __restrict__ run_if) {
+  if (run_if && *run_if == 0u) return;  // the int8 pass answered this batch
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -3044,11 +3174,228 @@ static bool select_args_ok(uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k) 
 hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
                                const uint32_t* cand_cnt, uint32_t nwg, uint32_t cap, uint32_t nq,
                                uint32_t k, uint64_t* out, hipStream_t st, uint32_t row_base,
-                               const uint64_t* allow, const uint32_t* cand_max) {
+                               const uint64_t* allow, const uint32_t* cand_max,
+                               const uint32_t* run_if) {
   if (!select_args_ok(nwg, cap, nq, k)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_slab_kernel<0>, dim3(nq), dim3(kSelThreads), 0, st,
                      (const f32x4_t*)slabs, slab_tile, cand_cnt, cand_max, nwg, cap, k, out,
-                     SlabMask{allow, row_base});
+                     SlabMask{allow, row_base}, run_if);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// select of the int8 prefilter pass (r04): bound, rescore, top k
+// ---------------------------------------------------------------------------
+// One workgroup per query over the I8 main pass's slabs (8 int32 dots of one
+// lane's rows of a tile). With the query's {sqS, a, c, sigma} and the tile's
+// {dt, nt} (largest quantisation-error norm and row norm of its 32 rows),
+// every slab row has L = sqS dot - m - sigma nt <= its fp32 score <= U =
+// sqS dot + m + sigma nt, m = a dt + c nt. Pass 1: per
+// workgroup the largest L; the k-th largest of those is a lower bound on
+// the k-th score (k distinct rows reach it), and so is b - sigma nmax (the
+// sample bound). Pass 2: rows whose U reaches the larger of the two are the
+// only ones that can be in the top k; they are rescored exactly from the
+// bf16 rows (fp32 sums of exact bf16 products, as the bf16 pass) and the top
+// k of those keys is the answer. More survivors than the LDS buffer holds
+// raise *gate: the bf16 pass and select then answer the batch.
+constexpr int kQ8SelMaxDim = 768;
+
+__global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
+    const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
+    const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
+    uint64_t* __restrict__ out, uint32_t row_base, const uint16_t* __restrict__ X,
+    const uint16_t* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
+    const float* __restrict__ q8glob, const float* __restrict__ meta,
+    const float* __restrict__ bound, uint32_t* __restrict__ gate) {
+  __shared__ uint64_t buf[kMfmaSelBuf];
+  __shared__ uint64_t lmax[kMfmaMaxLists];
+  __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
+  __shared__ uint16_t owner[kSelChunk];
+  __shared__ uint32_t wtot[kSelThreads / 64];
+  __shared__ float qs[kQ8SelMaxDim];
+  __shared__ uint32_t fill, spill;
+  __shared__ uint64_t thr_sh;
+  const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (*gate) return;  // already handed to the bf16 pass (which rewrites every answer)
+  const uint32_t sub = cap >> 2, nl = 4 * nwg;
+  const f32x4_t par = q8par[q];  // sqS, a, c, sigma
+  const float sqS = par[0], pa = par[1], pc = par[2], sig = par[3];
+  const float nmax = q8glob[2];
+  const float b = bound[q];
+  for (uint32_t d = tid; d < dim; d += kSelThreads) qs[d] = vs::bf16_to_f32(qb[(size_t)q * dim + d]);
+  const uint32_t l0 = 2 * tid;
+  uint32_t c0 = 0, c1 = 0;
+  {
+    const uint32_t a0 = l0 < nl ? l0 : 0u, a1 = l0 + 1 < nl ? l0 + 1 : 0u;
+    const uint32_t r0 = cnt[((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3)];
+    const uint32_t r1 = cnt[((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3)];
+    c0 = l0 < nl ? (r0 < sub ? r0 : sub) : 0u;
+    c1 = l0 + 1 < nl ? (r1 < sub ? r1 : sub) : 0u;
+  }
+  if (tid < kMfmaMaxLists) lmax[tid] = 0;
+  if (tid == 0) fill = 0, spill = 0;
+  uint32_t incl = c0 + c1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if ((int)lane >= d) incl += y;
+  }
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  uint32_t woff = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kSelThreads / 64; ++i) {
+    const uint32_t x = wtot[i];
+    woff += (uint32_t)i < w ? x : 0u;
+    total += x;
+  }
+  const uint32_t ex = woff + incl - (c0 + c1);
+  pre[l0] = ex;
+  pre[l0 + 1] = ex + c0;
+  if (tid == 0) pre[2 * kSelThreads] = total;
+  for (uint32_t j = 0; j < c0; ++j)
+    if (ex + j < kSelChunk) owner[ex + j] = (uint16_t)l0;
+  for (uint32_t j = 0; j < c1; ++j)
+    if (ex + c0 + j < kSelChunk) owner[ex + c0 + j] = (uint16_t)(l0 + 1);
+  __syncthreads();
+  const uint32_t T = total;
+  auto slab_at = [&](uint32_t l, uint32_t j) -> size_t {
+    return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub + j;
+  };
+  auto list_of = [&](uint32_t i) -> uint32_t {
+    if (i < kSelChunk) return owner[i];
+    uint32_t lo = 0, hi = 2 * kSelThreads;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  i32x4_t v[kSelHeld][2];
+  uint32_t tl[kSelHeld], ls[kSelHeld];
+  float mt[kSelHeld];  // m + sigma nt of the slab's tile; -1: no slab
+  auto load_chunk = [&](uint32_t base) {
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      const uint32_t i = base + tid + (uint32_t)u * kSelThreads;
+      const bool ok = i < T;
+      const uint32_t l = ok ? list_of(i) : 0u;
+      const size_t e = slab_at(l, ok ? i - pre[l] : 0u);
+      ls[u] = l;
+      v[u][0] = __builtin_bit_cast(i32x4_t, slabs[2 * e]);
+      v[u][1] = __builtin_bit_cast(i32x4_t, slabs[2 * e + 1]);
+      tl[u] = ok ? tiles[e] : row_base;
+      mt[u] = ok ? 0.f : -1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      const uint32_t lt = (tl[u] - row_base) >> 5;
+      const float dt = meta[2 * (size_t)lt], nt = meta[2 * (size_t)lt + 1];
+      mt[u] = mt[u] < 0.f ? -1.f : pa * dt + (pc + sig) * nt;
+    }
+  };
+  // pass 1: per workgroup the largest lower bound L
+  for (uint32_t base = 0; base < T; base += kSelChunk) {
+    load_chunk(base);
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      if (mt[u] < 0.f) continue;
+      const int dm = imax3(imax3(v[u][0][0], v[u][0][1], v[u][0][2]),
+                           imax3(v[u][0][3], v[u][1][0], v[u][1][1]),
+                           imax3(v[u][1][2], v[u][1][3], INT_MIN));
+      if (dm == INT_MIN) continue;
+      const float L = (float)dm * sqS - mt[u];
+      atomicMax((unsigned long long*)&lmax[ls[u] >> 2], (unsigned long long)make_key(L, 0xFFFFFFFFu));
+    }
+  }
+  __syncthreads();
+  uint64_t thr = 0;
+  if (k <= 64) {
+    if (w == 0) {
+      const uint64_t bb = sel_bound_wave(lmax, k, (int)lane);
+      if (lane == 0) thr_sh = bb;
+    }
+    __syncthreads();
+    thr = thr_sh;
+  } else {
+    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+    thr = k <= kMfmaMaxLists ? lmax[k - 1] : 0;
+  }
+  const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
+  const float tl_l = thr ? key_score(thr) : -INFINITY;
+  const float Tcut = tl_b > tl_l ? tl_b : tl_l;
+  // pass 2: rows whose upper bound reaches Tcut -> buf (local rows)
+  for (uint32_t base = 0; base < T; base += kSelChunk) {
+    if (T > kSelChunk) load_chunk(base);
+#pragma unroll
+    for (int u = 0; u < kSelHeld; ++u) {
+      if (mt[u] < 0.f) continue;
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb) {
+        const int dt = v[u][bb >> 2][bb & 3];
+        if (dt == INT_MIN) continue;
+        if ((float)dt * sqS + mt[u] >= Tcut) {
+          const uint32_t row = tl[u] - row_base + 16u * (uint32_t)(bb >> 2) + 4u * (ls[u] & 3) +
+                               (uint32_t)(bb & 3);
+          const uint32_t pos = atomicAdd(&fill, 1u);
+          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = row; else spill = 1u;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (spill) {  // uniform
+    if (tid == 0) *gate = 1u;
+    return;
+  }
+  const uint32_t ns = fill;
+  // rescore: wave w takes survivors w, w + 8, ... four at a time; lane l
+  // sums elements 2l, 2l+1 (+128 j) in order, then the xor butterfly
+  for (uint32_t i0 = w * 4; i0 < ns; i0 += 4 * (kSelThreads / 64)) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = i0 + j < ns ? (uint32_t)buf[i0 + j] : (uint32_t)buf[i0];
+    for (uint32_t d = 2 * lane; d < dim; d += 128) {
+      uint32_t x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = *(const uint32_t*)(X + (size_t)r[j] * dim + d);
+      const float q0 = qs[d], q1 = qs[d + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = fmaf(__uint_as_float(x[j] << 16), q0, acc[j]);
+        acc[j] = fmaf(__uint_as_float(x[j] & 0xFFFF0000u), q1, acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float sc = wave_sum(acc[j]);
+      if (lane == 0 && i0 + j < ns) buf[i0 + j] = make_key(sc, row_base + r[j]);
+    }
+  }
+  __syncthreads();
+  if (ns <= 64) {
+    if (w == 0) sel_finish_wave(buf, ns, k, (int)lane, out + (size_t)q * k);
+    return;
+  }
+  int p2 = 1;
+  while ((uint32_t)p2 < ns) p2 <<= 1;
+  for (uint32_t i = ns + tid; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+  __syncthreads();
+  bitonic_sort_desc_n(buf, p2, kSelThreads);
+  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < ns ? buf[j] : 0;
+}
+
+hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
+                            uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out,
+                            uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
+                            const float* q8par, const float* q8glob, const float* meta,
+                            const float* bound, uint32_t* gate, hipStream_t st) {
+  if (!select_args_ok(nwg, cap, nq, k) || dim > (uint32_t)kQ8SelMaxDim || dim % 128)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_q8_kernel, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
+                     slab_tile, cand_cnt, nwg, cap, k, out, row_base, X, qb, dim,
+                     (const f32x4_t*)q8par, q8glob, meta, bound, gate);
   return hipGetLastError();
 }
 

@@ -1,0 +1,201 @@
+// vs_q8.hip — store and query side of the int8 prefilter (r04; DESIGN.md §5
+// "int8 prefilter", launchers declared in vs_kernels.h).
+//
+// A bf16 collection keeps an int8 copy x8 = clamp(rint(x / S), -127, 127)
+// with one scale S per collection, and per 32-row tile two bounds rounded
+// up: dt = max_r |x_r - S x8_r| and nt = max_r |x_r|. A query q (bf16) gets
+// its own scale sq and the same pair |sq q8|, |q - sq q8|. Then, exactly,
+//   q . x = sq S (q8 . x8) + sq q8 . (x - S x8) + (q - sq q8) . x,
+// and Cauchy-Schwarz bounds the two error terms by |sq q8| dt + |q - sq q8| nt,
+// so an exact int32 dot on v_mfma_i32_16x16x64_i8 brackets the fp32 score.
+// Every norm is summed in fp64 and rounded up, so the brackets hold for the
+// values the device stores, not just in exact arithmetic.
+#include <climits>
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "vs_common.h"
+#include "vs_kernels.h"
+
+namespace vsk {
+namespace {
+
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
+  return v;
+}
+// sqrt of a non-negative fp64 sum, rounded up to float with a relative margin
+// for the sum's own fp64 rounding (dim <= 2^11 terms: far below 2^-30)
+__device__ __forceinline__ float norm_up(double s) {
+  return __double2float_ru(sqrt(s) * (1.0 + 0x1p-30));
+}
+__device__ __forceinline__ void atomic_max_pos(float* p, float v) {
+  // non-negative floats order as their bit patterns
+  atomicMax((unsigned int*)p, __float_as_uint(v));
+}
+
+// max |x| over n bf16 values, 16 B per lane per step
+__global__ __launch_bounds__(256) void q8_absmax_kernel(const uint4* __restrict__ X, uint64_t n16,
+                                                        float* __restrict__ glob) {
+  uint32_t m = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const uint4 v = X[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = w[j] & 0x7FFFu, hi = (w[j] >> 16) & 0x7FFFu;
+      m = lo > m ? lo : m;
+      m = hi > m ? hi : m;
+    }
+  }
+  // bf16 magnitude bits order as the values (NaN never stored: preprocess
+  // output of finite input)
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint32_t o = __shfl_xor(m, s, 64);
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomic_max_pos(glob, vs::bf16_to_f32((uint16_t)m));
+}
+
+__global__ void q8_set_scale_kernel(float* glob) {
+  const float a = glob[0];
+  glob[3] = a > 0.f ? a / 127.f : 1.f;
+}
+
+// One wave per 32-row tile; lane l holds elements 2l, 2l + 1 (+128 j) of a row.
+__global__ __launch_bounds__(256) void q8_quantize_kernel(
+    const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t dim,
+    const uint32_t* __restrict__ tiles, uint32_t t0, uint32_t ntiles, int8_t* __restrict__ X8,
+    float* __restrict__ meta, float* __restrict__ glob) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= ntiles) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t tile = tiles ? tiles[i] : t0 + i;
+  const float S = glob[3];
+  float dt = 0.f, nt = 0.f;
+  for (uint32_t rr = 0; rr < 32; ++rr) {
+    const uint64_t r = (uint64_t)tile * 32 + rr;
+    const bool live = r < n_rows;
+    double dd = 0.0, xx = 0.0;
+    for (uint32_t d = 2 * lane; d < dim; d += 128) {
+      const uint32_t xv = live ? *(const uint32_t*)(X + r * dim + d) : 0u;
+      const float x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xFFFF0000u);
+      const float y0 = fminf(fmaxf(rintf(x0 / S), -127.f), 127.f);
+      const float y1 = fminf(fmaxf(rintf(x1 / S), -127.f), 127.f);
+      // S * y is exact in fp64 (24 x 7 bits), and so is x - S y
+      const double e0 = (double)x0 - (double)S * (double)y0;
+      const double e1 = (double)x1 - (double)S * (double)y1;
+      dd = dd + e0 * e0 + e1 * e1;
+      xx = xx + (double)x0 * (double)x0 + (double)x1 * (double)x1;
+      const uint16_t pk = (uint16_t)(uint8_t)(int8_t)(int)y0 | ((uint16_t)(uint8_t)(int8_t)(int)y1 << 8);
+      *(uint16_t*)(X8 + r * dim + d) = pk;
+    }
+    if (!live) continue;
+    dd = wave_sum_d(dd);
+    xx = wave_sum_d(xx);
+    dt = fmaxf(dt, norm_up(dd));
+    nt = fmaxf(nt, norm_up(xx));
+  }
+  if (lane == 0) {
+    meta[2 * (size_t)tile] = dt;
+    meta[2 * (size_t)tile + 1] = nt;
+    atomic_max_pos(glob + 1, dt);
+    atomic_max_pos(glob + 2, nt);
+  }
+}
+
+// One wave per query.
+__global__ __launch_bounds__(256) void q8_query_kernel(const uint16_t* __restrict__ qb, uint32_t nq,
+                                                       uint32_t dim, const float* __restrict__ glob,
+                                                       int8_t* __restrict__ q8,
+                                                       float* __restrict__ q8par,
+                                                       uint32_t* __restrict__ gate) {
+  if (gate && blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nq) return;
+  const int lane = threadIdx.x & 63;
+  const uint16_t* x = qb + (size_t)i * dim;
+  float amax = 0.f;
+  for (uint32_t d = 2 * lane; d < dim; d += 128) {
+    const uint32_t xv = *(const uint32_t*)(x + d);
+    amax = fmaxf(amax, fmaxf(fabsf(__uint_as_float(xv << 16)), fabsf(__uint_as_float(xv & 0xFFFF0000u))));
+  }
+  amax = wave_max_f(amax);
+  const float sq = amax > 0.f ? amax / 127.f : 0.f;
+  double aa = 0.0, cc = 0.0, nn = 0.0;
+  for (uint32_t d = 2 * lane; d < dim; d += 128) {
+    const uint32_t xv = *(const uint32_t*)(x + d);
+    const float x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xFFFF0000u);
+    const float y0 = sq > 0.f ? fminf(fmaxf(rintf(x0 / sq), -127.f), 127.f) : 0.f;
+    const float y1 = sq > 0.f ? fminf(fmaxf(rintf(x1 / sq), -127.f), 127.f) : 0.f;
+    const double s0 = (double)sq * (double)y0, s1 = (double)sq * (double)y1;
+    const double e0 = (double)x0 - s0, e1 = (double)x1 - s1;
+    aa = aa + s0 * s0 + s1 * s1;
+    cc = cc + e0 * e0 + e1 * e1;
+    nn = nn + (double)x0 * (double)x0 + (double)x1 * (double)x1;
+    const uint16_t pk = (uint16_t)(uint8_t)(int8_t)(int)y0 | ((uint16_t)(uint8_t)(int8_t)(int)y1 << 8);
+    *(uint16_t*)(q8 + (size_t)i * dim + d) = pk;
+  }
+  aa = wave_sum_d(aa);
+  cc = wave_sum_d(cc);
+  nn = wave_sum_d(nn);
+  if (lane == 0) {
+    // sigma covers, per unit of |x|: the fp32 evaluation error of an MFMA or
+    // rescore score (<= 2 dim u |q| |x| each, u = 2^-24) on both sides of a
+    // bound, and the float rounding of sqS * dot, m and the comparisons
+    const float nq_up = norm_up(nn);
+    const float sigma = (float)((4.0 * dim + 64.0) * 0x1p-24 * (double)nq_up * (1.0 + 0x1p-20));
+    float* p = q8par + 4 * (size_t)i;
+    p[0] = sq * glob[3];
+    p[1] = norm_up(aa);
+    p[2] = norm_up(cc);
+    p[3] = sigma;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_q8_absmax(const uint16_t* X, uint64_t n, float* glob, hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;  // whole rows of dim % 128 == 0
+  const uint64_t n16 = n / 8;
+  uint64_t blocks = (n16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(q8_absmax_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, (const uint4*)X,
+                     n16, glob);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_set_scale(float* glob, hipStream_t st) {
+  hipLaunchKernelGGL(q8_set_scale_kernel, dim3(1), dim3(1), 0, st, glob);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_quantize(const uint16_t* X, uint32_t n_rows, uint32_t dim,
+                              const uint32_t* tiles, uint32_t t0, uint32_t ntiles, int8_t* X8,
+                              float* meta, float* glob, hipStream_t st) {
+  if (dim % 128 || dim == 0) return hipErrorInvalidValue;
+  if (ntiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(q8_quantize_kernel, dim3((ntiles + 3) / 4), dim3(256), 0, st, X, n_rows, dim,
+                     tiles, t0, ntiles, X8, meta, glob);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_query(const uint16_t* qb, uint32_t nq, uint32_t dim, const float* glob,
+                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st) {
+  if (dim % 128 || dim == 0) return hipErrorInvalidValue;
+  if (nq == 0) return hipSuccess;
+  hipLaunchKernelGGL(q8_query_kernel, dim3((nq + 3) / 4), dim3(256), 0, st, qb, nq, dim, glob, q8,
+                     q8par, gate);
+  return hipGetLastError();
+}
+
+}  // namespace vsk
