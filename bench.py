@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_DENSE_TFLOPS = 2516.6       # 256 CU x 4096 flop/clk x 2.4 GHz (dense, no sparsity)
 F32_MFMA_TFLOPS = 157.3          # v_mfma_f32_16x16x4_f32: 1/16 of bf16 (MI355X_MICROARCH.md)
+I8_DENSE_TOPS = 2 * BF16_DENSE_TFLOPS  # v_mfma_i32_16x16x64_i8: 2x the bf16 rate per clock
 
 CONFIGS = {
     # name: (rows, dim, dtype, metric, batch, k, description; {rows} = the corpus size)
@@ -125,6 +126,28 @@ def kernel_roofline(cfg_rows_local, dim, elem, batch, k, t_ms, bound, queries_pe
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(t_ms, 4),
             "bytes_per_launch": int(bytes_)}
+
+
+def int8_roofline(rows_local, dim, batch, k, t_ms, queries_per_pass=256):
+    """The int8 prefilter pass (DESIGN.md §5 "int8 prefilter"): it streams the
+    int8 copy (D bytes per row) and does 2 B D int8 MACs per row; at B = 256
+    its intensity (512 op/B) is under the i8 ridge (5033 TOP/s / 8 TB/s = 629),
+    so HBM is the roof it is priced against, with the MFMA figures beside it.
+    `exact_tflops_vs_bf16_peak` is the exact search's delivered work (the
+    bf16 pass's 2 B N D flops) per second over the bf16 dense peak: the
+    north_star's batched target, met through the prefilter."""
+    per_launch = min(batch, queries_per_pass)
+    bytes_ = rows_local * dim + per_launch * dim + per_launch * k * 12
+    ops = 2.0 * per_launch * rows_local * dim
+    t = t_ms / 1e3
+    gbs, tops = bytes_ / t / 1e9, ops / t / 1e12
+    return {"bound": "hbm", "kernel": "int8 prefilter pass (v_mfma_i32_16x16x64_i8)",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "mfma_achieved_tops": round(tops, 1),
+            "mfma_peak_tops": I8_DENSE_TOPS, "mfma_frac": round(tops / I8_DENSE_TOPS, 4),
+            "exact_tflops_vs_bf16_peak": round(tops / BF16_DENSE_TFLOPS, 4),
+            "launches_per_step": -(-batch // per_launch), "kernel_ms": round(t_ms, 4),
+            "bytes_per_launch": int(bytes_), "ops_per_launch": int(ops)}
 
 
 def pmc_traffic(workload):
@@ -397,9 +420,15 @@ def main():
     elem = 2 if dtype == "bf16" else 4
     bound = "mfma" if batch > 1 else "hbm"
     qpp = 256 if (dtype == "bf16" and dim <= 768) or (dtype == "f32" and dim <= 384) else 128
-    roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound, qpp)
+    # batched bf16 searches of a collection with an int8 copy run the int8
+    # prefilter pass (the engine's default; VS_FLAG_NO_PREFILTER turns it off)
+    int8 = batch > 1 and dtype == "bf16" and eng.prefilter_bytes(coll) > 0
+    if int8:
+        roof = int8_roofline(hi - lo, dim, batch, k, tm["scan_ms"], qpp)
+    else:
+        roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound, qpp)
     # PMC traffic is recorded per default-size workload only
-    roof["traffic"] = None if args.rows else pmc_traffic(args.config)
+    roof["traffic"] = None if args.rows else pmc_traffic(args.config + ("_i8" if int8 else ""))
     roof["kernel_launches_timed"] = tm["scan_n"]
 
     result = {
@@ -413,12 +442,13 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": dtype,
+        # int8 pass + exact bf16 rescoring of its survivors (same keys as bf16)
+        "dtype": "i8+bf16" if int8 else dtype,
         "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
                    "rows_per_gpu": hi - lo, "collective": collective,
-                   "build_id": pkg.build_id()},
+                   "int8_prefilter": int8, "build_id": pkg.build_id()},
         "roofline": roof,
         "steps_verified": steps_verified,
     }
@@ -436,6 +466,34 @@ def main():
                                "value": round(steps1 / el1, 2), "unit": "queries/s",
                                "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1,
                                "steps_verified": verify_steps(pkg, outs1, k, n_full)}
+
+    # secondary (one GPU): the same batch on the bf16 pass alone -- a second
+    # engine without the int8 copy over the same generated rows
+    if int8 and world == 1 and not dist_on and not args.no_secondary:
+        eng.drop_collection(coll)  # room for the second corpus
+        e2 = pkg.VectorEngine(device=local, timing=True, timing_sample=True, prefilter=False)
+        try:
+            e2.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else
+                                 pkg.METRIC_COSINE, pkg.DTYPE_BF16, hi - lo, lo)
+            e2.generate(coll, hi - lo, 0x5EED)
+            ls2, mg2 = shard.engine_callables(e2, coll, dim, stream_fn, reuse=True, ring=ring)
+            sh2 = shard.ShardedSearch(ls2, mg2)
+            el2, tm2, outs2 = run_phase(e2, sh2, coll, dim, batch, k, args.steps, args.warmup,
+                                        False, stream_fn, 0)
+            # the two paths sum the same products in different orders: rows
+            # agree except where exact scores tie within an ulp or two
+            m32 = np.uint64(0xFFFFFFFF)
+            same = float(((outs2[-1].cpu().numpy().view(np.uint64) & m32) ==
+                          (out.cpu().numpy().view(np.uint64) & m32)).mean())
+            result["bf16_pass"] = {
+                "workload": "the same batch on the bf16 MFMA pass (VS_FLAG_NO_PREFILTER)",
+                "value": round(batch * args.steps / el2, 2), "unit": "queries/s",
+                "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                "roofline": kernel_roofline(hi - lo, dim, 2, batch, k, tm2["scan_ms"], "mfma", qpp),
+                "steps_verified": verify_steps(pkg, outs2, k, n_full),
+                "rows_equal_to_int8_path": round(same, 6)}
+        finally:
+            e2.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

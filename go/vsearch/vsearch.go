@@ -36,6 +36,9 @@ static int vsg_engine_layout(vs_engine* h, uint32_t* s, uint32_t* d, vsg_err* e)
 static int vsg_collection_placement(vs_engine* h, const char* n, int32_t* d, vsg_err* e) {
 	return vsg_fin(vs_collection_placement(h, n, d), e);
 }
+static int vsg_collection_prefilter_bytes(vs_engine* h, const char* n, uint64_t* b, vsg_err* e) {
+	return vsg_fin(vs_collection_prefilter_bytes(h, n, b), e);
+}
 static int vsg_collection_info(vs_engine* h, const char* n, uint32_t* d, uint64_t* r, vsg_err* e) {
 	return vsg_fin(vs_collection_info(h, n, d, r, NULL, NULL), e);
 }
@@ -195,6 +198,17 @@ func (e *Engine) Placement(name string) (int, error) {
 	var ce C.vsg_err
 	err := check(C.vsg_collection_placement(e.h, cs, &d, &ce), &ce)
 	return int(d), err
+}
+
+// PrefilterBytes is the HBM held by the collection's int8 prefilter copy
+// (0: none). See VS_FLAG_NO_PREFILTER.
+func (e *Engine) PrefilterBytes(name string) (uint64, error) {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var b C.uint64_t
+	var ce C.vsg_err
+	err := check(C.vsg_collection_prefilter_bytes(e.h, cs, &b, &ce), &ce)
+	return uint64(b), err
 }
 
 // OpenShards opens one engine over row shards: shard s on HIP device

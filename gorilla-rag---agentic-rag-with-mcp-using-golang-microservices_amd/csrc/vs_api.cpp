@@ -1140,6 +1140,23 @@ int vs_collection_drop(vs_engine* eng, const char* name) {
   return sharded_drop(eng, name);
 }
 
+int vs_collection_prefilter_bytes(vs_engine* eng, const char* name, uint64_t* bytes) {
+  if (!eng || !bytes) return fail(VS_ERR_INVALID_ARG, "engine and bytes are required");
+  if (!eng->sharded) return vsd::prefilter_bytes(eng->dev[0], name, bytes);
+  auto sc = find_scoll(eng, name);
+  if (!sc) return not_found(name);
+  if (sc->home >= 0) return vsd::prefilter_bytes(home_eng(eng, *sc), sc->iname[0].c_str(), bytes);
+  uint64_t sum = 0;
+  for (uint32_t s = 0; s < eng->shards(); ++s) {
+    uint64_t part = 0;
+    const int rc = vsd::prefilter_bytes(shard_eng(eng, s), sc->iname[s].c_str(), &part);
+    if (rc != VS_OK) return rc;
+    sum += part;
+  }
+  *bytes = sum;
+  return VS_OK;
+}
+
 int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim, const uint64_t* rows,
               const float* vecs) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");

@@ -304,6 +304,7 @@ int collection_create(DevEngine* eng, const char* name, uint32_t dim, int metric
 int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* rows, int* metric,
                     int* dtype);
 int collection_drop(DevEngine* eng, const char* name);
+int prefilter_bytes(DevEngine* eng, const char* name, uint64_t* bytes);
 int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim, const uint64_t* rows,
            const float* vecs);
 // appends n generator rows whose global numbers are g0, g0 + stride, ...

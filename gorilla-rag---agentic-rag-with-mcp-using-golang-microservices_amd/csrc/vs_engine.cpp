@@ -187,8 +187,8 @@ bool q8_enabled() {
 
 // A collection keeps an int8 copy once its batched searches take the
 // candidate pass (8 or more tiles per workgroup) -- bf16, q8_supported dims.
-bool q8_wanted(const Collection& c) {
-  return q8_enabled() && c.dtype == VS_DTYPE_BF16 && vsk::q8_supported(c.dim) &&
+bool q8_wanted(const DevEngine* eng, const Collection& c) {
+  return q8_enabled() && !(eng->flags & VS_FLAG_NO_PREFILTER) && c.dtype == VS_DTYPE_BF16 && vsk::q8_supported(c.dim) &&
          c.rows < 0xFFFFFFFFull && vsk::mfma_tiles_per_wg((uint32_t)c.rows) >= 8;
 }
 
@@ -202,7 +202,7 @@ bool q8_wanted(const Collection& c) {
 // and batched searches read the bf16 rows.
 int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
                    const uint32_t* d_tiles = nullptr, uint32_t nt = 0) {
-  if (!q8_wanted(c)) return VS_OK;
+  if (!q8_wanted(eng, c)) return VS_OK;
   const uint32_t dim = c.dim;
   const uint32_t rows = (uint32_t)c.rows;
   const bool full = !c.q8 || c.q8_cap < c.cap || c.rows >= 2 * c.q8_scaled_at;
@@ -605,13 +605,17 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       // 2'. int8 pass -> bounded candidates -> rescored top k; the bf16 pass and
       // select behind it run only if the int8 pass overflowed (*gate)
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      // the quarters' largest dots go where the bf16 pass keeps its maxima
+      uint32_t* q8max = eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4;
       VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                       c.q8_glob, slabs, slab_tile, cap8,
-                                      eng->cand_cnt.as<uint32_t>(), maxl, &L, gate, eng->stream),
+                                      eng->cand_cnt.as<uint32_t>(), q8max, maxl, &L, gate,
+                                      eng->stream),
              "int8 scan");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-      VS_HIP(vsk::launch_select_q8(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap8, nv, k,
+      VS_HIP(vsk::launch_select_q8(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), q8max, L, cap8,
+                                   nv, k,
                                    out, row_base, (const uint16_t*)X, (const uint16_t*)qb, dim,
                                    q8par, c.q8_glob, c.q8_meta, bound, gate, eng->stream),
              "int8 select");
@@ -966,6 +970,16 @@ int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* r
   return VS_OK;
 }
 
+int prefilter_bytes(DevEngine* eng, const char* name, uint64_t* bytes) {
+  if (!eng || !bytes) return fail(VS_ERR_INVALID_ARG, "engine and bytes are required");
+  auto c = find_coll(eng, name);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (name ? name : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  *bytes = c->q8 ? (c->q8_cap + kPadRows) * c->dim : 0;
+  return VS_OK;
+}
+
 int collection_drop(DevEngine* eng, const char* name) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");
   std::shared_ptr<Collection> c;
@@ -1111,7 +1125,7 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
   }
   const uint64_t old_rows = c->rows;
   c->rows = expect;
-  if (q8_wanted(*c)) {
+  if (q8_wanted(eng, *c)) {
     // the tiles this call wrote: one range for rows in ascending order, else
     // the distinct tiles of the (row-sorted) kept rows
     if (ascending) {

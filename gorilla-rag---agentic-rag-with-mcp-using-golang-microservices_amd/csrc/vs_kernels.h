@@ -231,10 +231,14 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                const void* Q8, uint32_t nq_valid, uint32_t k,
                                const float* init_score, const float* q8par, const float* q8glob,
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
-                               uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
-                               uint32_t* gate, hipStream_t st);
+                               uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
+                               uint32_t* nlists, uint32_t* gate, hipStream_t st);
+// cand_max (same shape as cand_cnt): each quarter's largest appended dot
+// (int32; INT_MIN when empty), so the select reads only the quarters that
+// can hold a top-k row.
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
-                            uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out,
+                            const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
+                            uint32_t k, uint64_t* out,
                             uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, uint32_t* gate, hipStream_t st);

@@ -2082,8 +2082,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // against LDS counters and default-policy DMA (r01, 2 x 40 / 16 reps).
   constexpr bool kRegCnt = MODE == 0 && (VAR & 131072) == 0;
   uint32_t cnt_r[G], slot0[G];
+  int qmx_r[G];  // I8: the largest dot this lane appended (INT_MIN: none)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
+    qmx_r[g] = INT_MIN;
     // (the register-count main pass keeps each lane's running quarter maximum
     // here instead: score_ord of the largest admitted score, 0 = none)
     if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
@@ -2361,6 +2363,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
             cnt_r[g] = cg + 1;
+            qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
           }
         }
       }
@@ -2521,7 +2524,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       if constexpr (kRegCnt)
         if (a.cand_max)
           a.cand_max[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
-              cntl[g * THREADS + threadIdx.x];
+              I8 ? (uint32_t)qmx_r[g] : cntl[g * THREADS + threadIdx.x];
     } else if constexpr (MODE == 3) {
       // a workgroup with fewer tiles than max_tiles: the rest are empty
       for (uint32_t t = ntiles + kq; t < a.max_tiles; t += 4)
@@ -2695,16 +2698,16 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                const void* Q8, uint32_t nq_valid, uint32_t k,
                                const float* init_score, const float* q8par, const float* q8glob,
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
-                               uint32_t* cand_cnt, uint32_t max_lists, uint32_t* nlists,
-                               uint32_t* gate, hipStream_t st) {
+                               uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
+                               uint32_t* nlists, uint32_t* gate, hipStream_t st) {
   if (!q8_supported(dim) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
-      cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate)
+      cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate || !cand_max)
     return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X8, a.Q = Q8, a.init_score = init_score, a.cand = (uint64_t*)slabs;
-  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt;
+  a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.cand_max = cand_max;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
   a.q8par = q8par, a.q8glob = q8glob, a.gate = gate;
@@ -3202,13 +3205,14 @@ constexpr int kQ8SelMaxDim = 768;
 
 __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
-    const uint32_t* __restrict__ cnt, uint32_t nwg, uint32_t cap, uint32_t k,
-    uint64_t* __restrict__ out, uint32_t row_base, const uint16_t* __restrict__ X,
+    const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
+    uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const uint16_t* __restrict__ X,
     const uint16_t* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, uint32_t* __restrict__ gate) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
+  __shared__ int lmaxd[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint16_t owner[kSelChunk];
   __shared__ uint32_t wtot[kSelThreads / 64];
@@ -3220,20 +3224,54 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
   const f32x4_t par = q8par[q];  // sqS, a, c, sigma
   const float sqS = par[0], pa = par[1], pc = par[2], sig = par[3];
-  const float nmax = q8glob[2];
+  const float dmax = q8glob[1], nmax = q8glob[2];
+  const float mg = pa * dmax + (pc + sig) * nmax;  // m + sigma n of any row
   const float b = bound[q];
   for (uint32_t d = tid; d < dim; d += kSelThreads) qs[d] = vs::bf16_to_f32(qb[(size_t)q * dim + d]);
+  // lists 2 tid, 2 tid + 1: counts and largest appended dots
   const uint32_t l0 = 2 * tid;
   uint32_t c0 = 0, c1 = 0;
+  int x0 = INT_MIN, x1 = INT_MIN;
   {
     const uint32_t a0 = l0 < nl ? l0 : 0u, a1 = l0 + 1 < nl ? l0 + 1 : 0u;
-    const uint32_t r0 = cnt[((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3)];
-    const uint32_t r1 = cnt[((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3)];
+    const size_t i0 = ((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3);
+    const size_t i1 = ((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3);
+    const uint32_t r0 = cnt[i0], r1 = cnt[i1];
+    const int m0 = cmax[i0], m1 = cmax[i1];
     c0 = l0 < nl ? (r0 < sub ? r0 : sub) : 0u;
     c1 = l0 + 1 < nl ? (r1 < sub ? r1 : sub) : 0u;
+    x0 = c0 ? m0 : INT_MIN;
+    x1 = c1 ? m1 : INT_MIN;
   }
-  if (tid < kMfmaMaxLists) lmax[tid] = 0;
+  if (tid < kMfmaMaxLists) lmaxd[tid] = INT_MIN, lmax[tid] = 0;
   if (tid == 0) fill = 0, spill = 0;
+  __syncthreads();
+  // per workgroup the largest dot -> its lower bound sqS dot - mg (k distinct
+  // rows reach the k-th largest of those, so it bounds the k-th score)
+  if (x0 != INT_MIN) atomicMax(&lmaxd[l0 >> 2], x0);
+  if (x1 != INT_MIN) atomicMax(&lmaxd[(l0 + 1) >> 2], x1);
+  __syncthreads();
+  if (tid < kMfmaMaxLists && lmaxd[tid] != INT_MIN)
+    lmax[tid] = make_key((float)lmaxd[tid] * sqS - mg, 0xFFFFFFFFu);
+  __syncthreads();
+  uint64_t thr = 0;
+  if (k <= 64) {
+    if (w == 0) {
+      const uint64_t bb = sel_bound_wave(lmax, k, (int)lane);
+      if (lane == 0) thr_sh = bb;
+    }
+    __syncthreads();
+    thr = thr_sh;
+  } else {
+    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
+    thr = k <= kMfmaMaxLists ? lmax[k - 1] : 0;
+  }
+  const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
+  const float tl_l = thr ? key_score(thr) : -INFINITY;
+  const float Tcut = tl_b > tl_l ? tl_b : tl_l;
+  // only quarters whose largest dot can reach Tcut hold survivors
+  if (c0 && (float)x0 * sqS + mg < Tcut) c0 = 0;
+  if (c1 && (float)x1 * sqS + mg < Tcut) c1 = 0;
   uint32_t incl = c0 + c1;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3271,70 +3309,33 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     }
     return lo;
   };
-  i32x4_t v[kSelHeld][2];
-  uint32_t tl[kSelHeld], ls[kSelHeld];
-  float mt[kSelHeld];  // m + sigma nt of the slab's tile; -1: no slab
-  auto load_chunk = [&](uint32_t base) {
+  // the passing quarters' slabs: rows whose upper bound (the tile's m) reaches Tcut
+  for (uint32_t base = 0; base < T; base += kSelChunk) {
+    i32x4_t v[kSelHeld][2];
+    uint32_t tl[kSelHeld], ls[kSelHeld];
+    bool ok[kSelHeld];
 #pragma unroll
     for (int u = 0; u < kSelHeld; ++u) {
       const uint32_t i = base + tid + (uint32_t)u * kSelThreads;
-      const bool ok = i < T;
-      const uint32_t l = ok ? list_of(i) : 0u;
-      const size_t e = slab_at(l, ok ? i - pre[l] : 0u);
+      ok[u] = i < T;
+      const uint32_t l = ok[u] ? list_of(i) : 0u;
+      const size_t e = slab_at(l, ok[u] ? i - pre[l] : 0u);
       ls[u] = l;
       v[u][0] = __builtin_bit_cast(i32x4_t, slabs[2 * e]);
       v[u][1] = __builtin_bit_cast(i32x4_t, slabs[2 * e + 1]);
-      tl[u] = ok ? tiles[e] : row_base;
-      mt[u] = ok ? 0.f : -1.f;
+      tl[u] = ok[u] ? tiles[e] : row_base;
     }
 #pragma unroll
     for (int u = 0; u < kSelHeld; ++u) {
       const uint32_t lt = (tl[u] - row_base) >> 5;
       const float dt = meta[2 * (size_t)lt], nt = meta[2 * (size_t)lt + 1];
-      mt[u] = mt[u] < 0.f ? -1.f : pa * dt + (pc + sig) * nt;
-    }
-  };
-  // pass 1: per workgroup the largest lower bound L
-  for (uint32_t base = 0; base < T; base += kSelChunk) {
-    load_chunk(base);
-#pragma unroll
-    for (int u = 0; u < kSelHeld; ++u) {
-      if (mt[u] < 0.f) continue;
-      const int dm = imax3(imax3(v[u][0][0], v[u][0][1], v[u][0][2]),
-                           imax3(v[u][0][3], v[u][1][0], v[u][1][1]),
-                           imax3(v[u][1][2], v[u][1][3], INT_MIN));
-      if (dm == INT_MIN) continue;
-      const float L = (float)dm * sqS - mt[u];
-      atomicMax((unsigned long long*)&lmax[ls[u] >> 2], (unsigned long long)make_key(L, 0xFFFFFFFFu));
-    }
-  }
-  __syncthreads();
-  uint64_t thr = 0;
-  if (k <= 64) {
-    if (w == 0) {
-      const uint64_t bb = sel_bound_wave(lmax, k, (int)lane);
-      if (lane == 0) thr_sh = bb;
-    }
-    __syncthreads();
-    thr = thr_sh;
-  } else {
-    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
-    thr = k <= kMfmaMaxLists ? lmax[k - 1] : 0;
-  }
-  const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
-  const float tl_l = thr ? key_score(thr) : -INFINITY;
-  const float Tcut = tl_b > tl_l ? tl_b : tl_l;
-  // pass 2: rows whose upper bound reaches Tcut -> buf (local rows)
-  for (uint32_t base = 0; base < T; base += kSelChunk) {
-    if (T > kSelChunk) load_chunk(base);
-#pragma unroll
-    for (int u = 0; u < kSelHeld; ++u) {
-      if (mt[u] < 0.f) continue;
+      const float mt = pa * dt + (pc + sig) * nt;
+      if (!ok[u]) continue;
 #pragma unroll
       for (int bb = 0; bb < 8; ++bb) {
-        const int dt = v[u][bb >> 2][bb & 3];
-        if (dt == INT_MIN) continue;
-        if ((float)dt * sqS + mt[u] >= Tcut) {
+        const int dv = v[u][bb >> 2][bb & 3];
+        if (dv == INT_MIN) continue;
+        if ((float)dv * sqS + mt >= Tcut) {
           const uint32_t row = tl[u] - row_base + 16u * (uint32_t)(bb >> 2) + 4u * (ls[u] & 3) +
                                (uint32_t)(bb & 3);
           const uint32_t pos = atomicAdd(&fill, 1u);
@@ -3349,26 +3350,33 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     return;
   }
   const uint32_t ns = fill;
-  // rescore: wave w takes survivors w, w + 8, ... four at a time; lane l
-  // sums elements 2l, 2l+1 (+128 j) in order, then the xor butterfly
-  for (uint32_t i0 = w * 4; i0 < ns; i0 += 4 * (kSelThreads / 64)) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    uint32_t r[4];
+  // rescore: wave w takes survivors 8 at a time (w * 8 + 64 j ...); lane l
+  // sums elements 4l .. 4l+3 (+256 j) in order, then the xor butterfly:
+  // fp32 sums of exact bf16 products, as the bf16 pass scores
+  constexpr int RB = 8;
+  for (uint32_t i0 = w * RB; i0 < ns; i0 += RB * (kSelThreads / 64)) {
+    float acc[RB];
+    uint32_t r[RB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = i0 + j < ns ? (uint32_t)buf[i0 + j] : (uint32_t)buf[i0];
-    for (uint32_t d = 2 * lane; d < dim; d += 128) {
-      uint32_t x[4];
+    for (int j = 0; j < RB; ++j) {
+      acc[j] = 0.f;
+      r[j] = i0 + j < ns ? (uint32_t)buf[i0 + j] : (uint32_t)buf[i0];
+    }
+    for (uint32_t d = 4 * lane; d < dim; d += 256) {
+      uint2 x[RB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = *(const uint32_t*)(X + (size_t)r[j] * dim + d);
-      const float q0 = qs[d], q1 = qs[d + 1];
+      for (int j = 0; j < RB; ++j) x[j] = *(const uint2*)(X + (size_t)r[j] * dim + d);
+      const float q0 = qs[d], q1 = qs[d + 1], q2 = qs[d + 2], q3 = qs[d + 3];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] = fmaf(__uint_as_float(x[j] << 16), q0, acc[j]);
-        acc[j] = fmaf(__uint_as_float(x[j] & 0xFFFF0000u), q1, acc[j]);
+      for (int j = 0; j < RB; ++j) {
+        acc[j] = fmaf(__uint_as_float(x[j].x << 16), q0, acc[j]);
+        acc[j] = fmaf(__uint_as_float(x[j].x & 0xFFFF0000u), q1, acc[j]);
+        acc[j] = fmaf(__uint_as_float(x[j].y << 16), q2, acc[j]);
+        acc[j] = fmaf(__uint_as_float(x[j].y & 0xFFFF0000u), q3, acc[j]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < RB; ++j) {
       const float sc = wave_sum(acc[j]);
       if (lane == 0 && i0 + j < ns) buf[i0 + j] = make_key(sc, row_base + r[j]);
     }
@@ -3387,14 +3395,16 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
 }
 
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
-                            uint32_t nwg, uint32_t cap, uint32_t nq, uint32_t k, uint64_t* out,
+                            const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
+                            uint32_t k, uint64_t* out,
                             uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, uint32_t* gate, hipStream_t st) {
-  if (!select_args_ok(nwg, cap, nq, k) || dim > (uint32_t)kQ8SelMaxDim || dim % 128)
+  if (!select_args_ok(nwg, cap, nq, k) || dim > (uint32_t)kQ8SelMaxDim || dim % 256 || !cand_max)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(select_q8_kernel, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
-                     slab_tile, cand_cnt, nwg, cap, k, out, row_base, X, qb, dim,
+                     slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb,
+                     dim,
                      (const f32x4_t*)q8par, q8glob, meta, bound, gate);
   return hipGetLastError();
 }

@@ -106,6 +106,13 @@ typedef struct vs_config {
  * it is otherwise only reachable with two GPUs. Ignored without placement:
  * RCCL holds one rank per device. */
 #define VS_FLAG_ENGINE_PER_SHARD 16u
+/* No int8 prefilter copies (r04) for this engine's collections: batched
+ * searches of bf16 collections then always run the bf16 MFMA pass. By
+ * default a bf16 collection (dim 768) that takes the batched candidate pass
+ * keeps an int8 copy of its rows (+50% of its HBM) and answers batches from
+ * an int8 MFMA pass whose candidates are rescored exactly from the bf16 rows:
+ * the same keys as the bf16 pass ("int8 prefilter"). */
+#define VS_FLAG_NO_PREFILTER 32u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 
@@ -165,6 +172,10 @@ int vs_collection_info(vs_engine* eng, const char* name, uint32_t* dim,
 
 /* Frees the collection's device memory. */
 int vs_collection_drop(vs_engine* eng, const char* name);
+
+/* HBM bytes of the collection's int8 prefilter copy (summed over shards; 0 =
+ * none: its batched searches run the bf16 pass). See VS_FLAG_NO_PREFILTER. */
+int vs_collection_prefilter_bytes(vs_engine* eng, const char* name, uint64_t* bytes);
 
 /* ---- store side ----------------------------------------------------------- */
 

@@ -1,0 +1,152 @@
+"""Int8 prefilter (r04; DESIGN.md §5 "int8 prefilter", vs_q8.hip): batched
+searches of bf16 collections run an int8 MFMA pass that admits every row
+whose proven upper bound reaches the sample bound, and the survivors are
+rescored exactly from the bf16 rows. The answer must be the bf16 pass's:
+checked here against the oracle after every kind of store-side write that
+must keep the int8 copy in step (appends, shuffled overwrites with
+duplicates, rows past the collection's int8 scale, the rescale at doubled
+rows, snapshot / restore), and on the paths that hand a batch back to the
+bf16 pass on the device (a zero query, quarters overflowing on equal rows).
+
+Bar (BASELINE.json north_star, oracle.check_topk): rows equal the oracle's
+except exact-score near-ties < 1e-5 relative; scores within 1e-5 relative.
+Anchor: Points.Search, rag/vector-service/main.go:249-254.
+"""
+import numpy as np
+import pytest
+
+DIM = 768
+SCORE_RTOL = 1e-5
+
+
+def _parity(orc, X, Qp, s, r, c, k):
+    _, s64, rows, cnt = orc.search(X, Qp, k)
+    resc = orc.rescore(X, Qp, r, c)
+    bad = orc.check_topk(s, r, c, s64, rows, cnt, resc, SCORE_RTOL)
+    assert not bad, bad[:8]
+
+
+@pytest.fixture(scope="module")
+def pair(pkg):
+    """Two engines over the same 300k x 768 bf16 rows (inner product):
+    prefilter on (default) and off (VS_FLAG_NO_PREFILTER)."""
+    a = pkg.VectorEngine(device=0)
+    b = pkg.VectorEngine(device=0, prefilter=False)
+    for e in (a, b):
+        e.create_collection("p", DIM, pkg.METRIC_DOT, pkg.DTYPE_BF16, 300_000)
+        e.generate("p", 300_000, 77)
+    yield a, b
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_prefilter_copy_is_kept(pair):
+    a, b = pair
+    assert a.prefilter_bytes("p") >= 300_000 * DIM
+    assert b.prefilter_bytes("p") == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq,k", [(256, 10), (256, 100), (17, 1), (300, 128), (2, 50)])
+def test_prefilter_equals_oracle_and_bf16_pass(pair, orc, nq, k):
+    a, b = pair
+    X = orc.generate(77, 0, 300_000, DIM, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 500, nq, DIM)
+    Qp = orc.preprocess(Q, False, True)
+    s1, r1, c1 = a.search("p", Q, k)
+    _parity(orc, X, Qp, s1, r1, c1, k)
+    s2, r2, c2 = b.search("p", Q, k)
+    assert np.array_equal(c1, c2)
+    # the two passes sum the same exact products in different orders
+    np.testing.assert_allclose(s1, s2, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_prefilter_follows_every_write(pkg, orc, tmp_path):
+    rng = np.random.default_rng(5)
+    e = pkg.VectorEngine(device=0)
+    try:
+        n0 = 200_000
+        e.create_collection("w", DIM, pkg.METRIC_DOT, pkg.DTYPE_BF16)
+        e.generate("w", n0, 91)
+        assert e.prefilter_bytes("w") > 0
+        X = orc.generate(91, 0, n0, DIM, bf16=True)
+        Q = (rng.standard_normal((8, DIM)) / np.sqrt(DIM)).astype(np.float32)
+        Qp = orc.preprocess(Q, False, True)
+
+        def check(k=10):
+            s, r, c = e.search("w", Q, k)
+            _parity(orc, X, Qp, s, r, c, k)
+            return r
+
+        check()
+        # 1. shuffled overwrites with duplicates (the tile-list refresh): rows
+        # made to match the queries must come out on top
+        ids = rng.choice(n0, 3000, replace=True).astype(np.uint64)
+        V = (0.2 * rng.standard_normal((len(ids), DIM)) / np.sqrt(DIM)).astype(np.float32)
+        V[:8] += 3.0 * Q  # the first 8 overwritten rows align with the queries
+        e.upsert("w", ids, V)
+        u, first = np.unique(ids[::-1], return_index=True)
+        X[u] = orc.preprocess(V[len(ids) - 1 - first], False, True)
+        r = check()
+        for i in range(8):
+            if ids[i] not in ids[8:]:  # not overwritten again later in the call
+                assert int(ids[i]) in set(r[i].tolist())
+        # 2. an ascending append past the collection's int8 scale (clipped
+        # values: measured error bounds) that holds the best rows
+        big = (4.0 * rng.standard_normal((20_000, DIM)) / np.sqrt(DIM)).astype(np.float32)
+        big[100:108] = 5.0 * Q
+        e.upsert("w", np.arange(n0, n0 + len(big)), big)
+        X = np.concatenate([X, orc.preprocess(big, False, True)])
+        r = check(16)
+        for i in range(8):
+            assert n0 + 100 + i in set(r[i].tolist())
+        # 3. rows doubled: the copy is rebuilt with a new scale
+        e.generate("w", 250_000, 92)
+        n1 = X.shape[0]
+        X = np.concatenate([X, orc.generate(92, n1, 250_000, DIM, bf16=True)])
+        check(50)
+        # 4. snapshot / restore: the restored collection gets its own copy
+        path = str(tmp_path / "w.snap")
+        e.snapshot("w", path)
+        e.restore("w2", path)
+        assert e.prefilter_bytes("w2") > 0
+        s, r, c = e.search("w2", Q, 10)
+        _parity(orc, X, Qp, s, r, c, 10)
+        e.drop_collection("w2")
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_prefilter_hands_batches_to_bf16_pass(pkg, orc):
+    """A zero query (every dot 0: every row admitted) and 100k equal rows
+    (quarters overflow) set the batch's gate; the bf16 pass behind it answers."""
+    e = pkg.VectorEngine(device=0)
+    try:
+        n = 150_000
+        e.create_collection("g", DIM, pkg.METRIC_DOT, pkg.DTYPE_BF16)
+        X = orc.generate(31, 0, n, DIM, bf16=True)
+        X[20_000:120_000] = X[5]
+        e.upsert("g", np.arange(n), X)
+        assert e.prefilter_bytes("g") > 0
+        Q = orc.generate(orc.SEED_QUERY, 900, 6, DIM)
+        Q[0] = 0.0
+        Q[1] = X[5] * 2.0  # the equal rows lead
+        Qp = orc.preprocess(Q, False, True)
+        for k in (10, 64):
+            s, r, c = e.search("g", Q, k)
+            _parity(orc, X, Qp, s, r, c, k)
+    finally:
+        e.close()
+
+
+def test_prefilter_flag_and_symbol(pkg):
+    """(CPU) The flag and the accessor are part of the boundary."""
+    assert pkg.FLAG_NO_PREFILTER == 32
+    import re
+    import os
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "vsearch.h")).read()
+    assert re.search(r"#define VS_FLAG_NO_PREFILTER 32u", hdr)
+    assert "vs_collection_prefilter_bytes" in hdr
