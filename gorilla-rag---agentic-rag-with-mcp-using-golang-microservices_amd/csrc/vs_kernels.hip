@@ -3193,16 +3193,17 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // lane's rows of a tile). With the query's {sqS, a, c, sigma} and the tile's
 // {dt, nt} (largest quantisation-error norm and row norm of its 32 rows),
 // every slab row has L = sqS dot - m - sigma nt <= its fp32 score <= U =
-// sqS dot + m + sigma nt, m = a dt + c nt. Pass 1: per
-// workgroup the largest L; the k-th largest of those is a lower bound on
-// the k-th score (k distinct rows reach it), and so is b - sigma nmax (the
-// sample bound). Pass 2: rows whose U reaches the larger of the two are the
-// only ones that can be in the top k; they are rescored exactly from the
-// bf16 rows (fp32 sums of exact bf16 products, as the bf16 pass) and the top
-// k of those keys is the answer. More survivors than the LDS buffer holds
-// raise *gate: the bf16 pass and select then answer the batch.
-constexpr int kQ8SelMaxDim = 768;
+// sqS dot + m + sigma nt, m = a dt + c nt. From the quarters'
+// largest dots: per workgroup the largest L; the k-th largest of those is a
+// lower bound on the k-th score (k distinct rows reach it), and so is
+// b - sigma nmax (the sample bound). Rows whose U reaches the larger of the
+// two (read from the quarters whose largest U does) are the only ones that
+// can be in the top k; they are rescored from the bf16 rows on the bf16
+// pass's own MFMA chain -- the same score bits -- and the top k of those keys
+// is the bf16 pass's answer. More survivors than the LDS buffer holds raise
+// *gate: the bf16 pass and select then answer the batch.
 
+template <int D>
 __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
@@ -3216,7 +3217,6 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint16_t owner[kSelChunk];
   __shared__ uint32_t wtot[kSelThreads / 64];
-  __shared__ float qs[kQ8SelMaxDim];
   __shared__ uint32_t fill, spill;
   __shared__ uint64_t thr_sh;
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -3227,7 +3227,6 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   const float dmax = q8glob[1], nmax = q8glob[2];
   const float mg = pa * dmax + (pc + sig) * nmax;  // m + sigma n of any row
   const float b = bound[q];
-  for (uint32_t d = tid; d < dim; d += kSelThreads) qs[d] = vs::bf16_to_f32(qb[(size_t)q * dim + d]);
   // lists 2 tid, 2 tid + 1: counts and largest appended dots
   const uint32_t l0 = 2 * tid;
   uint32_t c0 = 0, c1 = 0;
@@ -3350,35 +3349,38 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     return;
   }
   const uint32_t ns = fill;
-  // rescore: wave w takes survivors 8 at a time (w * 8 + 64 j ...); lane l
-  // sums elements 4l .. 4l+3 (+256 j) in order, then the xor butterfly:
-  // fp32 sums of exact bf16 products, as the bf16 pass scores
-  constexpr int RB = 8;
-  for (uint32_t i0 = w * RB; i0 < ns; i0 += RB * (kSelThreads / 64)) {
-    float acc[RB];
-    uint32_t r[RB];
+  // rescore on the bf16 pass's own arithmetic: 16 survivors per group as the
+  // A rows of v_mfma_f32_16x16x32_bf16, the query as every B column, the
+  // row's 64-B steps in the pass's order from a zero accumulator -- each
+  // score is the bf16 pass's, bit for bit (an MFMA output element depends
+  // on its own row, column and accumulator only). Lane (col, kq) loads bytes
+  // 64 s + 16 kq of row col of the group and of the query, as the pass does.
+  constexpr int TS = D / 32;  // 64-B steps per row
+  const int col = (int)(lane & 15), kq = (int)(lane >> 4);
+  bf16x8_t qf[TS];
+  {
+    const uint4* qrow = (const uint4*)(qb + (size_t)q * D);
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      acc[j] = 0.f;
-      r[j] = i0 + j < ns ? (uint32_t)buf[i0 + j] : (uint32_t)buf[i0];
-    }
-    for (uint32_t d = 4 * lane; d < dim; d += 256) {
-      uint2 x[RB];
+    for (int t = 0; t < TS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
+  }
+  const uint32_t ngroups = (ns + 15) / 16;
+  for (uint32_t gi = w; gi < ngroups; gi += kSelThreads / 64) {
+    const uint32_t e = gi * 16 + (uint32_t)col;
+    const uint32_t r = (uint32_t)buf[e < ns ? e : gi * 16];
+    const uint4* xrow = (const uint4*)(X + (size_t)r * D);
+    bf16x8_t af[TS];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) x[j] = *(const uint2*)(X + (size_t)r[j] * dim + d);
-      const float q0 = qs[d], q1 = qs[d + 1], q2 = qs[d + 2], q3 = qs[d + 3];
+    for (int t = 0; t < TS; ++t) af[t] = __builtin_bit_cast(bf16x8_t, xrow[4 * t + kq]);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        acc[j] = fmaf(__uint_as_float(x[j].x << 16), q0, acc[j]);
-        acc[j] = fmaf(__uint_as_float(x[j].x & 0xFFFF0000u), q1, acc[j]);
-        acc[j] = fmaf(__uint_as_float(x[j].y << 16), q2, acc[j]);
-        acc[j] = fmaf(__uint_as_float(x[j].y & 0xFFFF0000u), q3, acc[j]);
-      }
-    }
+    for (int t = 0; t < TS; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], qf[t], acc, 0, 0, 0);
+    // C[4 kq + i][col] = score of group row 4 kq + i (every column alike)
+    uint32_t rr[4];
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const float sc = wave_sum(acc[j]);
-      if (lane == 0 && i0 + j < ns) buf[i0 + j] = make_key(sc, row_base + r[j]);
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t ei = gi * 16 + 4 * (uint32_t)kq + (uint32_t)i;
+      rr[i] = (uint32_t)__shfl((int)r, 4 * kq + i, 64);  // lane 4kq+i (col = 4kq+i, kq = 0) holds that row
+      if (col == 0 && ei < ns) buf[ei] = make_key(acc[i], row_base + rr[i]);
     }
   }
   __syncthreads();
@@ -3400,9 +3402,10 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, uint32_t* gate, hipStream_t st) {
-  if (!select_args_ok(nwg, cap, nq, k) || dim > (uint32_t)kQ8SelMaxDim || dim % 256 || !cand_max)
+  if (!select_args_ok(nwg, cap, nq, k) || !cand_max)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_q8_kernel, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
+  if (dim != 768) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(select_q8_kernel<768>, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
                      slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb,
                      dim,
                      (const f32x4_t*)q8par, q8glob, meta, bound, gate);
