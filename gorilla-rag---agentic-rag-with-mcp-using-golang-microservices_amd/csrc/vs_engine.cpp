@@ -538,7 +538,10 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   // int8 prefilter (unfiltered batches of a collection with an int8 copy)
   const bool q8 = fast && !allow && c.q8 && c.q8_cap >= c.rows && q8_enabled();
-  const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st, 4.0) : 0;
+  // the int8 pass admits ~5x the bf16 pass's rows (7.6k slabs per query at
+  // 10M rows, k = 10; fullest quarter 29 -- tools/q8_check.hip stats mode):
+  // sized at 8x so a full quarter (and the bf16 hand-back) stays rare
+  const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st, 8.0) : 0;
   const uint32_t capx = std::max(cap, cap8);
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds

@@ -241,7 +241,8 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             uint32_t k, uint64_t* out,
                             uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
-                            const float* bound, uint32_t* gate, hipStream_t st);
+                            const float* bound, uint32_t* gate, hipStream_t st,
+                            uint32_t* stats = nullptr);  // (tools) += slabs read, survivors
 // Store side (vs_q8.hip): glob[0] = max |x| over n bf16 values (atomic max;
 // zero it first); glob[3] = S = glob[0] / 127 (1 when 0).
 hipError_t launch_q8_absmax(const uint16_t* X, uint64_t n, float* glob, hipStream_t st);

@@ -2351,6 +2351,11 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           acc[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
         }
         const int mx = imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
+        // VAR 16777216 (timing ablation only, wrong answers): never append
+        if ((VAR & 16777216) != 0) {
+          asm volatile("" ::"v"(mx >= th_i[g]));
+          continue;
+        }
         if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
           const uint32_t sub = a.cand_cap >> 2;
           const uint32_t cg = cnt_r[g];
@@ -2685,8 +2690,10 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
 }
 
 // int8 prefilter pass (r04): D = 768 rows of int8 (768 B, whole-row 24 KiB
-// K-chunks through the 144 KiB ring), 256 queries, no filter.
-bool q8_supported(uint32_t dim) { return dim == 768; }
+// K-chunks through the 144 KiB ring), 256 queries; D = 1024 (C5's rows):
+// 16 KiB chunks (32 rows x 512 B) through the 144 KiB ring, 128 queries per
+// launch as the bf16 pass and sample pass there. No filter.
+bool q8_supported(uint32_t dim) { return dim == 768 || dim == 1024; }
 
 template <int VAR>
 static hipError_t launch_q8_var(uint32_t nwg, const MfArgs& a, hipStream_t st) {
@@ -2711,13 +2718,19 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
   a.q8par = q8par, a.q8glob = q8glob, a.gate = gate;
+  if (dim == 1024) {
+    hipLaunchKernelGGL((mfma_topk_kernel<1024, 0, 256, 1, false, true>), dim3(*nlists), dim3(512), 0,
+                       st, a);
+    return hipGetLastError();
+  }
   static const int var = [] {
     const char* e = getenv("VS_Q8_VAR");
     return e ? atoi(e) : 2048 + 256;
   }();
-  switch (var) {
+  switch (var) {  // VS_Q8_VAR: ablation arms (read once)
     case 0: return launch_q8_var<0>(*nlists, a, st);
     case 256: return launch_q8_var<256>(*nlists, a, st);
+    case 2048 + 256 + 16777216: return launch_q8_var<2048 + 256 + 16777216>(*nlists, a, st);
     default: return launch_q8_var<2048 + 256>(*nlists, a, st);
   }
 }
@@ -2826,6 +2839,22 @@ __device__ __forceinline__ void sel_finish_wave(const uint64_t* buf, uint32_t c,
   for (uint32_t j = (uint32_t)lane; j < k; j += 64) out[j] = j < 64 ? x : 0ull;
 }
 
+
+// Top 64 of two descending wave lists (one key per lane): the element-wise
+// maximum of one list and the other reversed is a bitonic sequence holding
+// the 64 largest keys; a half-cleaner cascade sorts it descending.
+__device__ __forceinline__ uint64_t wave_merge_top(uint64_t a, uint64_t b_desc, int lane) {
+  const uint64_t br = shfl64(b_desc, 63 - lane);
+  uint64_t y = a > br ? a : br;
+#pragma unroll
+  for (int stride = 32; stride > 0; stride >>= 1) {
+    const uint32_t lo = __shfl_xor((unsigned)(uint32_t)y, stride, 64);
+    const uint32_t hi = __shfl_xor((unsigned)(uint32_t)(y >> 32), stride, 64);
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    y = (lane & stride) == 0 ? (y > o ? y : o) : (y < o ? y : o);
+  }
+  return y;
+}
 
 // Main-pass slabs: slab j of quarter list l holds the scores of rows
 // tile + 16 (b / 4) + 4 kq + b % 4, b = 0..7 (the MFMA accumulator layout; kq
@@ -3203,14 +3232,14 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // is the bf16 pass's answer. More survivors than the LDS buffer holds raise
 // *gate: the bf16 pass and select then answer the batch.
 
-template <int D>
+template <int D, int SV = 0>  // SV (timing ablation, VS_Q8_SEL_SV): return after stage SV
 __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
     uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const uint16_t* __restrict__ X,
     const uint16_t* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
-    const float* __restrict__ bound, uint32_t* __restrict__ gate) {
+    const float* __restrict__ bound, uint32_t* __restrict__ gate, uint32_t* __restrict__ stats) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t lmax[kMfmaMaxLists];
   __shared__ int lmaxd[kMfmaMaxLists];
@@ -3255,8 +3284,20 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __syncthreads();
   uint64_t thr = 0;
   if (k <= 64) {
+    // the k-th largest lower bound over all 4 nwg quarters (disjoint rows):
+    // each wave keeps the top 64 of its 128 quarters in registers, wave 0
+    // merges the 8 lists (as many quarters as workgroups passed at k = 50,
+    // whose 50th-largest workgroup maximum sits far under the 50th score)
+    const uint64_t y0 = x0 != INT_MIN ? make_key((float)x0 * sqS - mg, 0xFFFFFFFFu) : 0ull;
+    const uint64_t y1 = x1 != INT_MIN ? make_key((float)x1 * sqS - mg, 0xFFFFFFFFu) : 0ull;
+    buf[w * 64 + lane] = wave_merge_top(wave_sort_desc(y0, (int)lane),
+                                        wave_sort_desc(y1, (int)lane), (int)lane);
+    __syncthreads();
     if (w == 0) {
-      const uint64_t bb = sel_bound_wave(lmax, k, (int)lane);
+      uint64_t R0 = buf[lane];
+#pragma unroll 1
+      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, buf[v * 64 + lane], (int)lane);
+      const uint64_t bb = readlane64(R0, (int)k - 1);
       if (lane == 0) thr_sh = bb;
     }
     __syncthreads();
@@ -3268,6 +3309,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
   const float tl_l = thr ? key_score(thr) : -INFINITY;
   const float Tcut = tl_b > tl_l ? tl_b : tl_l;
+  if constexpr (SV == 1) return;
   // only quarters whose largest dot can reach Tcut hold survivors
   if (c0 && (float)x0 * sqS + mg < Tcut) c0 = 0;
   if (c1 && (float)x1 * sqS + mg < Tcut) c1 = 0;
@@ -3344,11 +3386,16 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     }
   }
   __syncthreads();
+  if constexpr (SV == 2) return;
   if (spill) {  // uniform
     if (tid == 0) *gate = 1u;
     return;
   }
   const uint32_t ns = fill;
+  if (stats && tid == 0) {  // (tools/q8_check.hip) slabs read, survivors
+    atomicAdd(stats, T);
+    atomicAdd(stats + 1, ns);
+  }
   // rescore on the bf16 pass's own arithmetic: 16 survivors per group as the
   // A rows of v_mfma_f32_16x16x32_bf16, the query as every B column, the
   // row's 64-B steps in the pass's order from a zero accumulator -- each
@@ -3356,12 +3403,20 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   // on its own row, column and accumulator only). Lane (col, kq) loads bytes
   // 64 s + 16 kq of row col of the group and of the query, as the pass does.
   constexpr int TS = D / 32;  // 64-B steps per row
+  // D > 768: the query's fragments come from LDS (registers hold the row's)
+  constexpr bool kQL = TS > 24;
+  __shared__ uint4 qsh[kQL ? D / 8 : 1];
   const int col = (int)(lane & 15), kq = (int)(lane >> 4);
-  bf16x8_t qf[TS];
+  bf16x8_t qf[kQL ? 1 : TS];
   {
     const uint4* qrow = (const uint4*)(qb + (size_t)q * D);
+    if constexpr (kQL) {
+      for (uint32_t i = tid; i < (uint32_t)D / 8; i += kSelThreads) qsh[i] = qrow[i];
+      __syncthreads();
+    } else {
 #pragma unroll
-    for (int t = 0; t < TS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
+      for (int t = 0; t < TS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
+    }
   }
   const uint32_t ngroups = (ns + 15) / 16;
   for (uint32_t gi = w; gi < ngroups; gi += kSelThreads / 64) {
@@ -3373,7 +3428,14 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     for (int t = 0; t < TS; ++t) af[t] = __builtin_bit_cast(bf16x8_t, xrow[4 * t + kq]);
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < TS; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], qf[t], acc, 0, 0, 0);
+    for (int t = 0; t < TS; ++t) {
+      bf16x8_t bq;
+      if constexpr (kQL)
+        bq = __builtin_bit_cast(bf16x8_t, qsh[4 * t + kq]);
+      else
+        bq = qf[t];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bq, acc, 0, 0, 0);
+    }
     // C[4 kq + i][col] = score of group row 4 kq + i (every column alike)
     uint32_t rr[4];
 #pragma unroll
@@ -3383,9 +3445,29 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       if (col == 0 && ei < ns) buf[ei] = make_key(acc[i], row_base + rr[i]);
     }
   }
+  if constexpr (SV == 3) return;
   __syncthreads();
   if (ns <= 64) {
     if (w == 0) sel_finish_wave(buf, ns, k, (int)lane, out + (size_t)q * k);
+    return;
+  }
+  if (k <= 64) {
+    // each wave keeps the top 64 of its share in registers (64 keys sorted
+    // and merged at a time, no barrier), then wave 0 merges the 8 lists
+    uint64_t R = 0;
+    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
+      const uint64_t x = base + lane < ns ? buf[base + lane] : 0ull;
+      R = wave_merge_top(R, wave_sort_desc(x, (int)lane), (int)lane);
+    }
+    __syncthreads();  // every read of buf done
+    buf[w * 64 + lane] = R;
+    __syncthreads();
+    if (w == 0) {
+      uint64_t R0 = buf[lane];
+#pragma unroll 1
+      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, buf[v * 64 + lane], (int)lane);
+      if (lane < k) out[(size_t)q * k + lane] = R0;
+    }
     return;
   }
   int p2 = 1;
@@ -3401,14 +3483,28 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             uint32_t k, uint64_t* out,
                             uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
-                            const float* bound, uint32_t* gate, hipStream_t st) {
+                            const float* bound, uint32_t* gate, hipStream_t st, uint32_t* stats) {
   if (!select_args_ok(nwg, cap, nq, k) || !cand_max)
     return hipErrorInvalidValue;
+  if (dim == 1024) {
+    hipLaunchKernelGGL(select_q8_kernel<1024>, dim3(nq), dim3(kSelThreads), 0, st,
+                       (const f32x4_t*)slabs, slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k,
+                       out, row_base, X, qb, dim, (const f32x4_t*)q8par, q8glob, meta, bound, gate,
+                       stats);
+    return hipGetLastError();
+  }
   if (dim != 768) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(select_q8_kernel<768>, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
+  static const int sv = [] {
+    const char* e = getenv("VS_Q8_SEL_SV");
+    return e ? atoi(e) : 0;
+  }();
+  auto kern = sv == 1 ? select_q8_kernel<768, 1>
+            : sv == 2 ? select_q8_kernel<768, 2>
+            : sv == 3 ? select_q8_kernel<768, 3> : select_q8_kernel<768, 0>;
+  hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
                      slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb,
                      dim,
-                     (const f32x4_t*)q8par, q8glob, meta, bound, gate);
+                     (const f32x4_t*)q8par, q8glob, meta, bound, gate, stats);
   return hipGetLastError();
 }
 

@@ -64,6 +64,29 @@ def test_prefilter_equals_oracle_and_bf16_pass(pair, orc, nq, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nq,k", [(256, 50), (100, 10), (3, 128)])
+def test_prefilter_1024_cosine(pkg, orc, nq, k):
+    """C5's row shape: 1024-d cosine rows, 128 queries per int8 launch."""
+    a = pkg.VectorEngine(device=0)
+    b = pkg.VectorEngine(device=0, prefilter=False)
+    try:
+        n = 160_000
+        for e in (a, b):
+            e.create_collection("c", 1024, pkg.METRIC_COSINE, pkg.DTYPE_BF16, n)
+            e.generate("c", n, 55)
+        assert a.prefilter_bytes("c") > 0 and b.prefilter_bytes("c") == 0
+        X = orc.generate(55, 0, n, 1024, bf16=True)
+        Q = orc.generate(orc.SEED_QUERY, 7000, nq, 1024)
+        s1, r1, c1 = a.search("c", Q, k)
+        _parity(orc, X, orc.preprocess(Q, True, True), s1, r1, c1, k)
+        s2, r2, c2 = b.search("c", Q, k)
+        assert np.array_equal(r1, r2) and np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
 def test_prefilter_follows_every_write(pkg, orc, tmp_path):
     rng = np.random.default_rng(5)
     e = pkg.VectorEngine(device=0)

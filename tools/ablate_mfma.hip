@@ -359,7 +359,7 @@ int main(int argc, char** argv) {
         hipEventRecord(a, 0);
         hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const f32x4_t*)cand,
                            (const uint32_t*)ctile, (const uint32_t*)cnt, cmx, c.nwg, cap, k, out,
-                           SlabMask{nullptr, 0});
+                           SlabMask{nullptr, 0}, (const uint32_t*)nullptr);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms = 0;

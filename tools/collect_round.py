@@ -18,7 +18,14 @@ G = os.path.join(ROOT, "gpurun_out")
 P = os.path.join(ROOT, "profiles")
 
 
-def pmc_mfma(tag, bid):
+def main_pass(bench):
+    """The kernel name of the bench's dominant pass: the int8 prefilter pass
+    when the line says so (r04), else the bf16 pass."""
+    i8 = "i8" in str(bench.get("dtype", ""))
+    return f"mfma_topk_kernel<768, 0, 2304, 2, false, {'true' if i8 else 'false'}>"
+
+
+def pmc_mfma(tag, bid, kname):
     """MFMA utilisation and clock of the C3 main pass from the counter pass:
     busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs),
     clock = GRBM_GUI_ACTIVE / 8 / wall (MI355X_MICROARCH.md 'DVFS give-back')."""
@@ -27,7 +34,7 @@ def pmc_mfma(tag, bid):
         return
     per = {}
     for r in csv.DictReader(open(f)):
-        if "mfma_topk_kernel<768, 0" not in r["Kernel_Name"]:
+        if kname not in r["Kernel_Name"]:
             continue
         d = per.setdefault(r["Dispatch_Id"], {"wall_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -39,7 +46,8 @@ def pmc_mfma(tag, bid):
     wall = avg("wall_ns") / 1e9
     cyc = avg("GRBM_GUI_ACTIVE") / 8
     busy = avg("SQ_VALU_MFMA_BUSY_CYCLES") / (cyc * 1024)
-    rec = {"kernel": "mfma_topk_kernel<768, 0, 2304, 2, false> (C3 main pass)", "build_id": bid,
+    # the busy counter counts an i8 16x16x64 like a bf16 16x16x32 (same cycles)
+    rec = {"kernel": kname + " (C3 main pass)", "build_id": bid,
            "launches": len(rows), "wall_ms": round(wall * 1e3, 4),
            "clock_ghz": round(cyc / wall / 1e9, 3), "mfma_busy_frac": round(busy, 4),
            "mfma_busy_x_clock_over_peak_clock": round(busy * cyc / wall / 2.4e9, 4),
@@ -58,8 +66,9 @@ def main():
                 os.path.join(P, f"{tag}_c3_{bid}_bench_under_rocprof.json"))
     d = os.path.join(G, f"{tag}_prof_c3")
     shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(P, f"{tag}_c3_{bid}_kernel_stats.csv"))
+    kname = main_pass(b)
     rows = [r for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv")))
-            if "mfma_topk_kernel<768, 0" in r["Kernel_Name"]]
+            if kname in r["Kernel_Name"]]
     with open(os.path.join(P, f"{tag}_c3_{bid}_main_pass_trace.csv"), "w") as f:
         w = csv.writer(f)
         w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Duration_ns"])
@@ -71,14 +80,15 @@ def main():
     print(f"build {bid}: bench kernel_ms {b['roofline']['kernel_ms']} (frac {b['roofline']['frac']}); "
           f"under rocprof {pr['roofline']['kernel_ms']}; trace mean after 10 launches "
           f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10}")
-    pmc_mfma(tag, bid)
+    pmc_mfma(tag, bid, kname)
     fetch = []
     for cfg in ("c3", "c3b1"):
         f = os.path.join(G, f"{tag}_pmc_fetch_{cfg}", "run_counter_collection.csv")
         if os.path.exists(f):
             dst = os.path.join(P, f"{tag}_{cfg}_{bid}_pmc_fetch.csv")
             shutil.copy(f, dst)
-            fetch.append(f"{cfg}={dst}")
+            key = cfg + ("_i8" if cfg == "c3" and "true" in kname else "")
+            fetch.append(f"{key}={dst}")
     if fetch:
         import subprocess
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),

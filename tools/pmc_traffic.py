@@ -13,7 +13,13 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SCAN = {"c3": "mfma_topk_kernel<768, 0,", "c3b1": "gemv_topk_kernel<768, true, 1",
+# (r04) batched bf16 configs run the int8 prefilter pass by default: "_i8"
+# entries are that pass (the bf16 pass's launch behind it stands down at once
+# and must not enter the average), the plain ones the bf16 pass
+SCAN = {"c3": "mfma_topk_kernel<768, 0, 2304, 2, false, false>",
+        "c3_i8": "mfma_topk_kernel<768, 0, 2304, 2, false, true>",
+        "c5b256_i8": "mfma_topk_kernel<1024, 0, 256, 1, false, true>",
+        "c3b1": "gemv_topk_kernel<768, true, 1",
         "c2": "gemv_topk_kernel<768, false, 1", "c4": "mfma_topk_kernel<768, 0,",
         "c4b1": "gemv_topk_kernel<768, true, 2", "c5b256": "mfma_topk_kernel<1024, 0,"}
 

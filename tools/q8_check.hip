@@ -27,7 +27,77 @@
     }                                                                         \
   } while (0)
 
-int main() {
+// Stats mode: q8_check N [NQ [DIM [K]]] (N > 65536): device-generated rows and
+// queries, the pipeline once, slabs / survivors per query; no host check.
+int stats_mode(uint32_t n, uint32_t nq, uint32_t dim, uint32_t k) {
+  uint16_t *dX, *dQ;
+  int8_t *dX8, *dQ8;
+  float *meta, *glob, *par, *tmax, *bound;
+  CK(hipMalloc(&dX, (size_t)(n + 32) * dim * 2));
+  CK(hipMalloc(&dQ, (size_t)256 * dim * 2));
+  CK(hipMalloc(&dX8, (size_t)(n + 32) * dim));
+  CK(hipMalloc(&dQ8, (size_t)256 * dim));
+  CK(hipMalloc(&meta, (size_t)(n / 32 + 2) * 8));
+  CK(hipMalloc(&glob, 16));
+  CK(hipMalloc(&par, 256 * 16 + 64));
+  CK(hipMemset(dX, 0, (size_t)(n + 32) * dim * 2));
+  CK(vsk::launch_generate(0x5EED, 0, n, dim, true, dX, 0, 0));
+  CK(vsk::launch_generate(0xC0FFEE, 0, nq, dim, true, dQ, 0, 0));
+  CK(hipMemset(glob, 0, 16));
+  CK(vsk::launch_q8_absmax(dX, (uint64_t)n * dim, glob, 0));
+  CK(vsk::launch_q8_set_scale(glob, 0));
+  CK(vsk::launch_q8_quantize(dX, n, dim, nullptr, 0, (n + 31) / 32, dX8, meta, glob, 0));
+  uint32_t* gate = (uint32_t*)(par + 4 * 256);
+  CK(vsk::launch_q8_query(dQ, nq, dim, glob, dQ8, par, gate, 0));
+  const uint32_t nwg = vsk::mfma_max_lists(n), st = vsk::mfma_sample_tiles(n, dim, false);
+  const uint32_t cap = vsk::mfma_cand_cap(n, k, st, 8.0);  // as search_mfma
+  float* slabs;
+  uint32_t *tiles, *cnt, *cmx, *stats;
+  const size_t slots = (size_t)nwg * 256 * cap;
+  CK(hipMalloc(&slabs, slots * 32));
+  CK(hipMalloc(&tiles, slots * 4));
+  CK(hipMalloc(&cnt, (size_t)nwg * 256 * 16));
+  CK(hipMalloc(&cmx, (size_t)nwg * 256 * 16));
+  CK(hipMalloc(&stats, 8));
+  CK(hipMemset(stats, 0, 8));
+  CK(hipMalloc(&tmax, (size_t)256 * nwg * st * 4));
+  CK(hipMalloc(&bound, 256 * 4));
+  uint64_t* out;
+  CK(hipMalloc(&out, 256 * k * 8));
+  uint32_t L = 0;
+  CK(vsk::launch_mfma_sample(dX, false, dim, n, 0, dQ, nq, k, st, tmax, nwg, &L, 0));
+  CK(vsk::launch_sample_bound(tmax, L * st, nq, k, bound, 0));
+  CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, bound, par, glob, slabs, tiles, cap, cnt,
+                              cmx, nwg, &L, gate, 0));
+  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, dim, par, glob,
+                           meta, bound, gate, 0, stats));
+  CK(hipDeviceSynchronize());
+  std::vector<uint32_t> hc((size_t)nwg * 256 * 4);
+  CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
+  uint32_t hs[2], hgate;
+  CK(hipMemcpy(hs, stats, 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&hgate, gate, 4, hipMemcpyDeviceToHost));
+  uint64_t tot = 0, qmax = 0;
+  for (uint32_t w = 0; w < nwg; ++w)
+    for (uint32_t q = 0; q < nq; ++q)
+      for (uint32_t kq = 0; kq < 4; ++kq) {
+        const uint32_t c = hc[((size_t)w * 256 + q) * 4 + kq];
+        tot += c;
+        qmax = std::max<uint64_t>(qmax, c);
+      }
+  std::printf("{\"rows\": %u, \"dim\": %u, \"k\": %u, \"queries\": %u, \"cap\": %u, \"gate\": %u, "
+              "\"slabs_per_query\": %.1f, \"fullest_quarter\": %llu, "
+              "\"slabs_read_per_query\": %.1f, \"survivors_per_query\": %.1f}\n",
+              n, dim, k, nq, cap, hgate, (double)tot / nq, (unsigned long long)qmax, (double)hs[0] / nq,
+              (double)hs[1] / nq);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::atoi(argv[1]) > 65536)
+    return stats_mode((uint32_t)std::atoi(argv[1]), argc > 2 ? (uint32_t)std::atoi(argv[2]) : 256,
+                      argc > 3 ? (uint32_t)std::atoi(argv[3]) : 768,
+                      argc > 4 ? (uint32_t)std::atoi(argv[4]) : 10);
   const uint32_t dim = 768, n = 65536, nq = 4, k = 10;
   std::mt19937 rng(7);
   std::normal_distribution<float> nd;
@@ -72,9 +142,11 @@ int main() {
   CK(hipMalloc(&slabs, slots * 32));
   CK(hipMalloc(&tiles, slots * 4));
   CK(hipMalloc(&cnt, (size_t)nwg * 256 * 4 * 4));
+  uint32_t* cmx;
+  CK(hipMalloc(&cmx, (size_t)nwg * 256 * 4 * 4));
   uint32_t L = 0;
   CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, nullptr, par, glob, slabs, tiles, cap,
-                              cnt, nwg, &L, gate, 0));
+                              cnt, cmx, nwg, &L, gate, 0));
   CK(hipDeviceSynchronize());
   std::vector<int8_t> X8((size_t)n * dim), Q8((size_t)nq * dim);
   std::vector<float> hm((size_t)(n / 32) * 2), hg(4), hp(4 * nq);
@@ -149,7 +221,7 @@ int main() {
   CK(vsk::launch_sample_bound(tmax, L * st, nq, k, bound, 0));
   CK(vsk::launch_q8_query(dQ, nq, dim, glob, dQ8, par, gate, 0));
   CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, bound, par, glob, slabs, tiles, cap,
-                              cnt, nwg, &L, gate, 0));
+                              cnt, cmx, nwg, &L, gate, 0));
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
   CK(hipMemcpy(&hgate, gate, 4, hipMemcpyDeviceToHost));
@@ -188,7 +260,7 @@ int main() {
     std::printf("q %u host threshold %.1f; admitted slab maxima in [%d, %d]; best dot %d\n", q, th,
                 mn, mxall, best);
   }
-  CK(vsk::launch_select_q8(slabs, tiles, cnt, nwg, cap, nq, k, out, 0, dX, dQ, dim, par, glob, meta,
+  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, dim, par, glob, meta,
                            bound, gate, 0));
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(&hgate, gate, 4, hipMemcpyDeviceToHost));
