@@ -422,9 +422,9 @@ def main():
     qpp = 256 if (dtype == "bf16" and dim <= 768) or (dtype == "f32" and dim <= 384) else 128
     # batched bf16 searches of a collection with an int8 copy run the int8
     # prefilter pass (the engine's default; VS_FLAG_NO_PREFILTER turns it off)
-    int8 = batch > 1 and dtype == "bf16" and eng.prefilter_bytes(coll) > 0
-    if int8:
-        roof = int8_roofline(hi - lo, dim, batch, k, tm["scan_ms"], qpp)
+    int8 = batch > 1 and eng.prefilter_bytes(coll) > 0
+    if int8:  # the int8 pass takes 256 queries a launch up to 768-d, 128 above
+        roof = int8_roofline(hi - lo, dim, batch, k, tm["scan_ms"], 256 if dim <= 768 else 128)
     else:
         roof = kernel_roofline(hi - lo, dim, elem, batch, k, tm["scan_ms"], bound, qpp)
     # PMC traffic is recorded per default-size workload only
@@ -442,8 +442,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        # int8 pass + exact bf16 rescoring of its survivors (same keys as bf16)
-        "dtype": "i8+bf16" if int8 else dtype,
+        # int8 pass + rescoring of its survivors on the bf16 / f32 pass's chain
+        "dtype": f"i8+{dtype}" if int8 else dtype,
         "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
@@ -467,14 +467,15 @@ def main():
                                "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1,
                                "steps_verified": verify_steps(pkg, outs1, k, n_full)}
 
-    # secondary (one GPU): the same batch on the bf16 pass alone -- a second
-    # engine without the int8 copy over the same generated rows
+    # secondary (one GPU): the same batch on the bf16 / f32 pass alone -- a
+    # second engine without the int8 copy over the same generated rows
     if int8 and world == 1 and not dist_on and not args.no_secondary:
         eng.drop_collection(coll)  # room for the second corpus
         e2 = pkg.VectorEngine(device=local, timing=True, timing_sample=True, prefilter=False)
         try:
             e2.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else
-                                 pkg.METRIC_COSINE, pkg.DTYPE_BF16, hi - lo, lo)
+                                 pkg.METRIC_COSINE,
+                                 pkg.DTYPE_BF16 if dtype == "bf16" else pkg.DTYPE_F32, hi - lo, lo)
             e2.generate(coll, hi - lo, 0x5EED)
             ls2, mg2 = shard.engine_callables(e2, coll, dim, stream_fn, reuse=True, ring=ring)
             sh2 = shard.ShardedSearch(ls2, mg2)
@@ -483,11 +484,11 @@ def main():
             # the int8 path rescores on the bf16 pass's MFMA chain: same keys
             same = float((outs2[-1].cpu().numpy().view(np.uint64) ==
                           out.cpu().numpy().view(np.uint64)).mean())
-            result["bf16_pass"] = {
-                "workload": "the same batch on the bf16 MFMA pass (VS_FLAG_NO_PREFILTER)",
+            result[f"{dtype}_pass"] = {
+                "workload": f"the same batch on the {dtype} MFMA pass (VS_FLAG_NO_PREFILTER)",
                 "value": round(batch * args.steps / el2, 2), "unit": "queries/s",
                 "ms_per_step": round(el2 / args.steps * 1e3, 4),
-                "roofline": kernel_roofline(hi - lo, dim, 2, batch, k, tm2["scan_ms"], "mfma", qpp),
+                "roofline": kernel_roofline(hi - lo, dim, elem, batch, k, tm2["scan_ms"], "mfma", qpp),
                 "steps_verified": verify_steps(pkg, outs2, k, n_full),
                 "keys_equal_to_int8_path": round(same, 6)}
         finally:

@@ -186,9 +186,11 @@ bool q8_enabled() {
 }
 
 // A collection keeps an int8 copy once its batched searches take the
-// candidate pass (8 or more tiles per workgroup) -- bf16, q8_supported dims.
+// candidate pass (8 or more tiles per workgroup) -- q8_supported dims (bf16
+// 768 / 1024, fp32 768).
 bool q8_wanted(const DevEngine* eng, const Collection& c) {
-  return q8_enabled() && !(eng->flags & VS_FLAG_NO_PREFILTER) && c.dtype == VS_DTYPE_BF16 && vsk::q8_supported(c.dim) &&
+  return q8_enabled() && !(eng->flags & VS_FLAG_NO_PREFILTER) &&
+         vsk::q8_supported(c.dim, c.dtype == VS_DTYPE_F32) &&
          c.rows < 0xFFFFFFFFull && vsk::mfma_tiles_per_wg((uint32_t)c.rows) >= 8;
 }
 
@@ -223,11 +225,11 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
       VS_HIP(hipMemsetAsync(c.q8, 0, (c.cap + kPadRows) * dim, eng->stream), "zero int8 copy");
     }
     VS_HIP(hipMemsetAsync(c.q8_glob, 0, 16, eng->stream), "zero int8 bounds");
-    VS_HIP(vsk::launch_q8_absmax((const uint16_t*)c.data, (uint64_t)rows * dim, c.q8_glob,
+    VS_HIP(vsk::launch_q8_absmax(c.data, c.dtype == VS_DTYPE_F32, (uint64_t)rows * dim, c.q8_glob,
                                  eng->stream),
            "int8 scale");
     VS_HIP(vsk::launch_q8_set_scale(c.q8_glob, eng->stream), "int8 scale");
-    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, nullptr, 0,
+    VS_HIP(vsk::launch_q8_quantize(c.data, c.dtype == VS_DTYPE_F32, rows, dim, nullptr, 0,
                                    (rows + 31) / 32, (int8_t*)c.q8, c.q8_meta, c.q8_glob,
                                    eng->stream),
            "int8 copy");
@@ -235,12 +237,12 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
     return VS_OK;
   }
   if (d_tiles) {
-    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, d_tiles, 0, nt,
+    VS_HIP(vsk::launch_q8_quantize(c.data, c.dtype == VS_DTYPE_F32, rows, dim, d_tiles, 0, nt,
                                    (int8_t*)c.q8, c.q8_meta, c.q8_glob, eng->stream),
            "int8 copy");
   } else if (r1 > r0) {
     const uint32_t t0 = (uint32_t)(r0 / 32), t1 = (uint32_t)((r1 - 1) / 32) + 1;
-    VS_HIP(vsk::launch_q8_quantize((const uint16_t*)c.data, rows, dim, nullptr, t0, t1 - t0,
+    VS_HIP(vsk::launch_q8_quantize(c.data, c.dtype == VS_DTYPE_F32, rows, dim, nullptr, t0, t1 - t0,
                                    (int8_t*)c.q8, c.q8_meta, c.q8_glob, eng->stream),
            "int8 copy");
   }
@@ -568,14 +570,73 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   uint64_t* lists = eng->lists.as<uint64_t>();
   float* slabs = eng->cand.as<float>();
   uint32_t* slab_tile = (uint32_t*)((char*)eng->cand.p + slots * 32);
+  float* bound = eng->sample_bound.as<float>();
+  float* tmax = eng->scand.as<float>();
+  uint32_t* cnt = eng->cand_cnt.as<uint32_t>();
+  // the quarters' maxima (bf16 / f32 pass: largest admitted score, int8 pass:
+  // largest appended dot) beside the counts
+  uint32_t* qmax = cnt + (size_t)maxl * PS * 4;
+  uint32_t* qmax_sel = select_qmax() ? qmax : nullptr;
+  // queries q .. in the collection's dtype: the bf16 copy, or the preprocessed
+  // fp32 queries themselves (zero-padded past nq)
+  auto qptr = [&](uint32_t q) -> const void* {
+    return f32 ? (const void*)(qp + (size_t)q * dim)
+               : (const void*)(eng->q_bf16.as<uint16_t>() + (size_t)q * dim);
+  };
+  if (q8) {
+    // int8 pass: up to 256 queries per launch (128 at 1024-d); the sample and
+    // bf16 / f32 passes run P queries a launch (fp32 768-d: 128, so two each)
+    const uint32_t P8 = vsk::mfma_queries(dim, false);
+    int8_t* q8q = eng->q8_q.as<int8_t>();
+    float* q8par = eng->q8_par.as<float>();
+    uint32_t* gate = (uint32_t*)(q8par + 4 * PS);
+    for (uint32_t q0 = 0; q0 < nq; q0 += P8) {
+      const uint32_t nv = std::min(P8, nq - q0);
+      uint64_t* out = d_keys + (size_t)q0 * k;
+      uint32_t L = 0;
+      VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream),
+             "int8 queries");
+      // 1. sample pass(es) -> per-query lower bounds on the k-th score
+      for (uint32_t s0 = 0; s0 < nv; s0 += P) {
+        const uint32_t ns = std::min(P, nv - s0);
+        VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k, st,
+                                       tmax, maxl, &L, eng->stream, nullptr),
+               "mfma sample scan");
+        VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream),
+               "sample bound");
+      }
+      // 2. int8 pass -> bounded candidates -> rescored top k; the bf16 / f32
+      // pass and select behind it run only if the int8 pass overflowed (*gate)
+      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
+                                      c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
+                                      eng->stream),
+             "int8 scan");
+      VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
+                                   qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, gate,
+                                   eng->stream),
+             "int8 select");
+      for (uint32_t s0 = 0; s0 < nv; s0 += P) {
+        const uint32_t ns = std::min(P, nv - s0);
+        VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k,
+                                     bound + s0, slabs, slab_tile, cap, cnt, maxl, &L, eng->stream,
+                                     nullptr, qmax_sel, gate),
+               "mfma scan (int8 fallback)");
+        VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, cnt, L, cap, ns, k, out + (size_t)s0 * k,
+                                        eng->stream, row_base, nullptr, qmax_sel, gate),
+               "select (int8 fallback)");
+      }
+      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+    }
+    return VS_OK;
+  }
   for (uint32_t p = 0; p < npass; ++p) {
     const uint32_t q0 = p * P;
     const uint32_t nv = std::min(P, nq - q0);
     uint64_t* out = d_keys + (size_t)q0 * k;
-    // the pass's queries in the collection's dtype: the bf16 copy, or the
-    // preprocessed fp32 queries themselves (zero-padded past nq)
-    const void* qb = f32 ? (const void*)(qp + (size_t)q0 * dim)
-                         : (const void*)(eng->q_bf16.as<uint16_t>() + (size_t)q0 * dim);
+    const void* qb = qptr(q0);
     uint32_t L = 0;
     if (!fast) {
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
@@ -590,58 +651,19 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       continue;
     }
     // 1. sample pass -> tile maxima -> per-query bound (k-th largest maximum)
-    float* bound = eng->sample_bound.as<float>();
-    float* tmax = eng->scand.as<float>();
-    int8_t* q8q = q8 ? eng->q8_q.as<int8_t>() : nullptr;
-    float* q8par = q8 ? eng->q8_par.as<float>() : nullptr;
-    uint32_t* gate = q8 ? (uint32_t*)(q8par + 4 * PS) : nullptr;
-    if (q8)
-      VS_HIP(vsk::launch_q8_query((const uint16_t*)qb, nv, dim, c.q8_glob, q8q, q8par, gate,
-                                  eng->stream),
-             "int8 queries");
     VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qb, nv, k, st, tmax, maxl, &L,
                                    eng->stream, allow),
            "mfma sample scan");
     VS_HIP(vsk::launch_sample_bound(tmax, L * st, nv, k, bound, eng->stream), "sample bound");
-    uint32_t* qmax = select_qmax() ? eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4 : nullptr;
-    if (q8) {
-      // 2'. int8 pass -> bounded candidates -> rescored top k; the bf16 pass and
-      // select behind it run only if the int8 pass overflowed (*gate)
-      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
-      // the quarters' largest dots go where the bf16 pass keeps its maxima
-      uint32_t* q8max = eng->cand_cnt.as<uint32_t>() + (size_t)maxl * PS * 4;
-      VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
-                                      c.q8_glob, slabs, slab_tile, cap8,
-                                      eng->cand_cnt.as<uint32_t>(), q8max, maxl, &L, gate,
-                                      eng->stream),
-             "int8 scan");
-      VS_HIP(ev_end(eng, eng->scan_ev), "event");
-      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-      VS_HIP(vsk::launch_select_q8(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), q8max, L, cap8,
-                                   nv, k,
-                                   out, row_base, (const uint16_t*)X, (const uint16_t*)qb, dim,
-                                   q8par, c.q8_glob, c.q8_meta, bound, gate, eng->stream),
-             "int8 select");
-      VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
-                                   slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl, &L,
-                                   eng->stream, nullptr, qmax, gate),
-             "mfma scan (int8 fallback)");
-      VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                                      k, out, eng->stream, row_base, nullptr, qmax, gate),
-             "select (int8 fallback)");
-      VS_HIP(ev_end(eng, eng->merge_ev), "event");
-      continue;
-    }
     // 2. main pass -> candidates -> select
     VS_HIP(ev_begin(eng, eng->scan_ev), "event");
     VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qb, nv, k, bound, slabs,
-                                 slab_tile, cap, eng->cand_cnt.as<uint32_t>(), maxl,
-                                 &L, eng->stream, allow, qmax),
+                                 slab_tile, cap, cnt, maxl, &L, eng->stream, allow, qmax_sel),
            "mfma scan");
     VS_HIP(ev_end(eng, eng->scan_ev), "event");
     VS_HIP(ev_begin(eng, eng->merge_ev), "event");
-    VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, eng->cand_cnt.as<uint32_t>(), L, cap, nv,
-                                    k, out, eng->stream, row_base, allow, qmax),
+    VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, cnt, L, cap, nv, k, out, eng->stream,
+                                    row_base, allow, qmax_sel),
            "select");
     VS_HIP(ev_end(eng, eng->merge_ev), "event");
   }

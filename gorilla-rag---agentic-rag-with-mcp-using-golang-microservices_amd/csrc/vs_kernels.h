@@ -226,7 +226,8 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // writes the top k. Any overflow (a full quarter, too many survivors) sets
 // *gate, and the bf16 pass + select enqueued behind with run_if = gate
 // answer the batch instead. Exact: the answer is the bf16 pass's.
-bool q8_supported(uint32_t dim);
+// dims with an int8 pass: bf16 rows 768 / 1024, fp32 rows 768 (r04)
+bool q8_supported(uint32_t dim, bool f32);
 hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                                const void* Q8, uint32_t nq_valid, uint32_t k,
                                const float* init_score, const float* q8par, const float* q8glob,
@@ -236,27 +237,30 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
 // cand_max (same shape as cand_cnt): each quarter's largest appended dot
 // (int32; INT_MIN when empty), so the select reads only the quarters that
 // can hold a top-k row.
+// X / Q: the collection's rows and the pass's queries in its dtype (bf16, or
+// fp32 when f32: survivors rescored on the f32 pass's 16x16x4 chain).
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
                             const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
                             uint32_t k, uint64_t* out,
-                            uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
+                            uint32_t row_base, const void* X, const void* qb, bool f32, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, uint32_t* gate, hipStream_t st,
                             uint32_t* stats = nullptr);  // (tools) += slabs read, survivors
-// Store side (vs_q8.hip): glob[0] = max |x| over n bf16 values (atomic max;
-// zero it first); glob[3] = S = glob[0] / 127 (1 when 0).
-hipError_t launch_q8_absmax(const uint16_t* X, uint64_t n, float* glob, hipStream_t st);
+// Store side (vs_q8.hip; X: bf16 rows, or fp32 rows when f32): glob[0] = max
+// |x| over n values (atomic max; zero it first); glob[3] = S = glob[0] / 127
+// (1 when 0).
+hipError_t launch_q8_absmax(const void* X, bool f32, uint64_t n, float* glob, hipStream_t st);
 hipError_t launch_q8_set_scale(float* glob, hipStream_t st);
 // Requantise whole 32-row tiles (tiles[i] if non-null, else t0 + i; rows past
 // n_rows are written as zeros) with the scale glob[3]: X8, meta[tile] = {dt,
 // nt}, and glob[1], glob[2] raised to the tiles' maxima.
-hipError_t launch_q8_quantize(const uint16_t* X, uint32_t n_rows, uint32_t dim,
+hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t dim,
                               const uint32_t* tiles, uint32_t t0, uint32_t ntiles, int8_t* X8,
                               float* meta, float* glob, hipStream_t st);
-// Queries (bf16, nq x dim) -> int8 rows Q8 and q8par[q] = {sq * S, |sq q8|,
-// |q - sq q8|, sigma}, norms rounded up.
+// Queries (bf16, or fp32 when f32; nq x dim) -> int8 rows Q8 and q8par[q] =
+// {sq * S, |sq q8|, |q - sq q8|, sigma}, norms rounded up.
 // Also zeroes *gate (the batch's overflow word) ahead of the int8 pass.
-hipError_t launch_q8_query(const uint16_t* qb, uint32_t nq, uint32_t dim, const float* glob,
+hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st);
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.

@@ -2693,7 +2693,9 @@ hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_ro
 // K-chunks through the 144 KiB ring), 256 queries; D = 1024 (C5's rows):
 // 16 KiB chunks (32 rows x 512 B) through the 144 KiB ring, 128 queries per
 // launch as the bf16 pass and sample pass there. No filter.
-bool q8_supported(uint32_t dim) { return dim == 768 || dim == 1024; }
+bool q8_supported(uint32_t dim, bool f32) {
+  return f32 ? dim == 768 : (dim == 768 || dim == 1024);
+}
 
 template <int VAR>
 static hipError_t launch_q8_var(uint32_t nwg, const MfArgs& a, hipStream_t st) {
@@ -2707,7 +2709,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
                                uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
                                uint32_t* nlists, uint32_t* gate, hipStream_t st) {
-  if (!q8_supported(dim) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
+  if (!q8_supported(dim, false) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
       cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate || !cand_max)
     return hipErrorInvalidValue;
   MfArgs a{};
@@ -3232,12 +3234,15 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // is the bf16 pass's answer. More survivors than the LDS buffer holds raise
 // *gate: the bf16 pass and select then answer the batch.
 
-template <int D, int SV = 0>  // SV (timing ablation, VS_Q8_SEL_SV): return after stage SV
+// SV (timing ablation, VS_Q8_SEL_SV): return after stage SV. F32: fp32 rows
+// and queries, survivors rescored on the f32 pass's v_mfma_f32_16x16x4_f32
+// chain (four MFMAs per 16-B fragment, as that pass), so again its bits.
+template <int D, int SV = 0, bool F32 = false>
 __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
-    uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const uint16_t* __restrict__ X,
-    const uint16_t* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
+    uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
+    const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, uint32_t* __restrict__ gate, uint32_t* __restrict__ stats) {
   __shared__ uint64_t buf[kMfmaSelBuf];
@@ -3402,39 +3407,50 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   // score is the bf16 pass's, bit for bit (an MFMA output element depends
   // on its own row, column and accumulator only). Lane (col, kq) loads bytes
   // 64 s + 16 kq of row col of the group and of the query, as the pass does.
-  constexpr int TS = D / 32;  // 64-B steps per row
-  // D > 768: the query's fragments come from LDS (registers hold the row's)
+  constexpr int RBY = D * (F32 ? 4 : 2);  // row bytes
+  constexpr int TS = RBY / 64;            // 64-B steps per row
+  // rows past 24 steps (bf16 D = 1024, fp32): the query's fragments come from
+  // LDS, and fp32 rows are read in halves of 24 steps (96 VGPRs each)
   constexpr bool kQL = TS > 24;
-  __shared__ uint4 qsh[kQL ? D / 8 : 1];
+  constexpr int HS = TS % 24 == 0 ? 24 : (TS % 16 == 0 ? 16 : TS);  // steps held per round
+  static_assert(TS % HS == 0, "whole rounds of steps");
+  __shared__ uint4 qsh[kQL ? RBY / 16 : 1];
   const int col = (int)(lane & 15), kq = (int)(lane >> 4);
-  bf16x8_t qf[kQL ? 1 : TS];
+  uint4 qf[kQL ? 1 : TS];
   {
-    const uint4* qrow = (const uint4*)(qb + (size_t)q * D);
+    const uint4* qrow = (const uint4*)((const unsigned char*)qb + (size_t)q * RBY);
     if constexpr (kQL) {
-      for (uint32_t i = tid; i < (uint32_t)D / 8; i += kSelThreads) qsh[i] = qrow[i];
+      for (uint32_t i = tid; i < (uint32_t)RBY / 16; i += kSelThreads) qsh[i] = qrow[i];
       __syncthreads();
     } else {
 #pragma unroll
-      for (int t = 0; t < TS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, qrow[4 * t + kq]);
+      for (int t = 0; t < TS; ++t) qf[t] = qrow[4 * t + kq];
     }
   }
   const uint32_t ngroups = (ns + 15) / 16;
   for (uint32_t gi = w; gi < ngroups; gi += kSelThreads / 64) {
     const uint32_t e = gi * 16 + (uint32_t)col;
     const uint32_t r = (uint32_t)buf[e < ns ? e : gi * 16];
-    const uint4* xrow = (const uint4*)(X + (size_t)r * D);
-    bf16x8_t af[TS];
-#pragma unroll
-    for (int t = 0; t < TS; ++t) af[t] = __builtin_bit_cast(bf16x8_t, xrow[4 * t + kq]);
+    const uint4* xrow = (const uint4*)((const unsigned char*)X + (size_t)r * RBY);
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < TS; ++t) {
-      bf16x8_t bq;
-      if constexpr (kQL)
-        bq = __builtin_bit_cast(bf16x8_t, qsh[4 * t + kq]);
-      else
-        bq = qf[t];
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bq, acc, 0, 0, 0);
+    for (int h = 0; h < TS / HS; ++h) {
+      uint4 af[HS];
+#pragma unroll
+      for (int t = 0; t < HS; ++t) af[t] = xrow[4 * (h * HS + t) + kq];
+#pragma unroll
+      for (int t = 0; t < HS; ++t) {
+        const int ts = h * HS + t;
+        const uint4 bq = kQL ? qsh[4 * ts + kq] : qf[kQL ? 0 : ts];
+        if constexpr (F32) {
+          const f32x4_t av = __builtin_bit_cast(f32x4_t, af[t]), bv = __builtin_bit_cast(f32x4_t, bq);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[t]),
+                                                        __builtin_bit_cast(bf16x8_t, bq), acc, 0, 0, 0);
+        }
+      }
     }
     // C[4 kq + i][col] = score of group row 4 kq + i (every column alike)
     uint32_t rr[4];
@@ -3481,29 +3497,26 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
                             const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
                             uint32_t k, uint64_t* out,
-                            uint32_t row_base, const uint16_t* X, const uint16_t* qb, uint32_t dim,
+                            uint32_t row_base, const void* X, const void* qb, bool f32, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, uint32_t* gate, hipStream_t st, uint32_t* stats) {
-  if (!select_args_ok(nwg, cap, nq, k) || !cand_max)
-    return hipErrorInvalidValue;
-  if (dim == 1024) {
-    hipLaunchKernelGGL(select_q8_kernel<1024>, dim3(nq), dim3(kSelThreads), 0, st,
-                       (const f32x4_t*)slabs, slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k,
-                       out, row_base, X, qb, dim, (const f32x4_t*)q8par, q8glob, meta, bound, gate,
-                       stats);
-    return hipGetLastError();
-  }
-  if (dim != 768) return hipErrorInvalidValue;
+  if (!select_args_ok(nwg, cap, nq, k) || !cand_max) return hipErrorInvalidValue;
   static const int sv = [] {
     const char* e = getenv("VS_Q8_SEL_SV");
     return e ? atoi(e) : 0;
   }();
-  auto kern = sv == 1 ? select_q8_kernel<768, 1>
-            : sv == 2 ? select_q8_kernel<768, 2>
-            : sv == 3 ? select_q8_kernel<768, 3> : select_q8_kernel<768, 0>;
-  hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs,
-                     slab_tile, cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb,
-                     dim,
+  decltype(&select_q8_kernel<768, 0, false>) kern;
+  if (f32 && dim == 768)
+    kern = select_q8_kernel<768, 0, true>;
+  else if (!f32 && dim == 1024)
+    kern = select_q8_kernel<1024, 0, false>;
+  else if (!f32 && dim == 768)
+    kern = sv == 1 ? select_q8_kernel<768, 1> : sv == 2 ? select_q8_kernel<768, 2>
+         : sv == 3 ? select_q8_kernel<768, 3> : select_q8_kernel<768, 0>;
+  else
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
+                     cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
                      (const f32x4_t*)q8par, q8glob, meta, bound, gate, stats);
   return hipGetLastError();
 }

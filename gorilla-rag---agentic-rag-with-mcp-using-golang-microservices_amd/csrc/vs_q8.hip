@@ -65,14 +65,46 @@ __global__ __launch_bounds__(256) void q8_absmax_kernel(const uint4* __restrict_
   if ((threadIdx.x & 63) == 0 && m) atomic_max_pos(glob, vs::bf16_to_f32((uint16_t)m));
 }
 
+// max |x| over n fp32 values (fp32 collections, r04)
+__global__ __launch_bounds__(256) void q8_absmax_f32_kernel(const uint4* __restrict__ X, uint64_t n4,
+                                                            float* __restrict__ glob) {
+  uint32_t m = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const uint4 v = X[i];
+    const uint32_t w[4] = {v.x & 0x7FFFFFFFu, v.y & 0x7FFFFFFFu, v.z & 0x7FFFFFFFu, v.w & 0x7FFFFFFFu};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m = w[j] > m ? w[j] : m;
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint32_t o = __shfl_xor(m, s, 64);
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomic_max_pos(glob, __uint_as_float(m));
+}
+
+// two consecutive elements of a bf16 (32-bit word) or fp32 (64-bit) row
+template <bool F32>
+__device__ __forceinline__ void load2(const void* X, uint64_t e, bool live, float& x0, float& x1) {
+  if constexpr (F32) {
+    const float2 v = live ? *(const float2*)((const float*)X + e) : float2{0.f, 0.f};
+    x0 = v.x, x1 = v.y;
+  } else {
+    const uint32_t xv = live ? *(const uint32_t*)((const uint16_t*)X + e) : 0u;
+    x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xFFFF0000u);
+  }
+}
+
 __global__ void q8_set_scale_kernel(float* glob) {
   const float a = glob[0];
   glob[3] = a > 0.f ? a / 127.f : 1.f;
 }
 
 // One wave per 32-row tile; lane l holds elements 2l, 2l + 1 (+128 j) of a row.
+template <bool F32>
 __global__ __launch_bounds__(256) void q8_quantize_kernel(
-    const uint16_t* __restrict__ X, uint32_t n_rows, uint32_t dim,
+    const void* __restrict__ X, uint32_t n_rows, uint32_t dim,
     const uint32_t* __restrict__ tiles, uint32_t t0, uint32_t ntiles, int8_t* __restrict__ X8,
     float* __restrict__ meta, float* __restrict__ glob) {
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -86,11 +118,11 @@ __global__ __launch_bounds__(256) void q8_quantize_kernel(
     const bool live = r < n_rows;
     double dd = 0.0, xx = 0.0;
     for (uint32_t d = 2 * lane; d < dim; d += 128) {
-      const uint32_t xv = live ? *(const uint32_t*)(X + r * dim + d) : 0u;
-      const float x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xFFFF0000u);
+      float x0, x1;
+      load2<F32>(X, r * dim + d, live, x0, x1);
       const float y0 = fminf(fmaxf(rintf(x0 / S), -127.f), 127.f);
       const float y1 = fminf(fmaxf(rintf(x1 / S), -127.f), 127.f);
-      // S * y is exact in fp64 (24 x 7 bits), and so is x - S y
+      // S * y is exact in fp64 (24 x 7 bits), and so is x - S y (x: 24 bits)
       const double e0 = (double)x0 - (double)S * (double)y0;
       const double e1 = (double)x1 - (double)S * (double)y1;
       dd = dd + e0 * e0 + e1 * e1;
@@ -112,8 +144,10 @@ __global__ __launch_bounds__(256) void q8_quantize_kernel(
   }
 }
 
-// One wave per query.
-__global__ __launch_bounds__(256) void q8_query_kernel(const uint16_t* __restrict__ qb, uint32_t nq,
+// One wave per query (bf16 queries of a bf16 collection, or the fp32
+// preprocessed queries of an fp32 one).
+template <bool F32>
+__global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ qb, uint32_t nq,
                                                        uint32_t dim, const float* __restrict__ glob,
                                                        int8_t* __restrict__ q8,
                                                        float* __restrict__ q8par,
@@ -122,18 +156,19 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const uint16_t* __restric
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nq) return;
   const int lane = threadIdx.x & 63;
-  const uint16_t* x = qb + (size_t)i * dim;
+  const uint64_t x = (uint64_t)i * dim;
   float amax = 0.f;
   for (uint32_t d = 2 * lane; d < dim; d += 128) {
-    const uint32_t xv = *(const uint32_t*)(x + d);
-    amax = fmaxf(amax, fmaxf(fabsf(__uint_as_float(xv << 16)), fabsf(__uint_as_float(xv & 0xFFFF0000u))));
+    float x0, x1;
+    load2<F32>(qb, x + d, true, x0, x1);
+    amax = fmaxf(amax, fmaxf(fabsf(x0), fabsf(x1)));
   }
   amax = wave_max_f(amax);
   const float sq = amax > 0.f ? amax / 127.f : 0.f;
   double aa = 0.0, cc = 0.0, nn = 0.0;
   for (uint32_t d = 2 * lane; d < dim; d += 128) {
-    const uint32_t xv = *(const uint32_t*)(x + d);
-    const float x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xFFFF0000u);
+    float x0, x1;
+    load2<F32>(qb, x + d, true, x0, x1);
     const float y0 = sq > 0.f ? fminf(fmaxf(rintf(x0 / sq), -127.f), 127.f) : 0.f;
     const float y1 = sq > 0.f ? fminf(fmaxf(rintf(x1 / sq), -127.f), 127.f) : 0.f;
     const double s0 = (double)sq * (double)y0, s1 = (double)sq * (double)y1;
@@ -163,14 +198,18 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const uint16_t* __restric
 
 }  // namespace
 
-hipError_t launch_q8_absmax(const uint16_t* X, uint64_t n, float* glob, hipStream_t st) {
+hipError_t launch_q8_absmax(const void* X, bool f32, uint64_t n, float* glob, hipStream_t st) {
   if (n % 8) return hipErrorInvalidValue;  // whole rows of dim % 128 == 0
-  const uint64_t n16 = n / 8;
+  const uint64_t n16 = f32 ? n / 4 : n / 8;  // 16-B loads
   uint64_t blocks = (n16 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(q8_absmax_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, (const uint4*)X,
-                     n16, glob);
+  if (f32)
+    hipLaunchKernelGGL(q8_absmax_f32_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       (const uint4*)X, n16, glob);
+  else
+    hipLaunchKernelGGL(q8_absmax_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, (const uint4*)X,
+                       n16, glob);
   return hipGetLastError();
 }
 
@@ -179,22 +218,30 @@ hipError_t launch_q8_set_scale(float* glob, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_q8_quantize(const uint16_t* X, uint32_t n_rows, uint32_t dim,
+hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t dim,
                               const uint32_t* tiles, uint32_t t0, uint32_t ntiles, int8_t* X8,
                               float* meta, float* glob, hipStream_t st) {
   if (dim % 128 || dim == 0) return hipErrorInvalidValue;
   if (ntiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(q8_quantize_kernel, dim3((ntiles + 3) / 4), dim3(256), 0, st, X, n_rows, dim,
-                     tiles, t0, ntiles, X8, meta, glob);
+  if (f32)
+    hipLaunchKernelGGL(q8_quantize_kernel<true>, dim3((ntiles + 3) / 4), dim3(256), 0, st, X,
+                       n_rows, dim, tiles, t0, ntiles, X8, meta, glob);
+  else
+    hipLaunchKernelGGL(q8_quantize_kernel<false>, dim3((ntiles + 3) / 4), dim3(256), 0, st, X,
+                       n_rows, dim, tiles, t0, ntiles, X8, meta, glob);
   return hipGetLastError();
 }
 
-hipError_t launch_q8_query(const uint16_t* qb, uint32_t nq, uint32_t dim, const float* glob,
+hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st) {
   if (dim % 128 || dim == 0) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
-  hipLaunchKernelGGL(q8_query_kernel, dim3((nq + 3) / 4), dim3(256), 0, st, qb, nq, dim, glob, q8,
-                     q8par, gate);
+  if (f32)
+    hipLaunchKernelGGL(q8_query_kernel<true>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
+                       glob, q8, q8par, gate);
+  else
+    hipLaunchKernelGGL(q8_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
+                       glob, q8, q8par, gate);
   return hipGetLastError();
 }
 

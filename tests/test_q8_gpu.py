@@ -87,6 +87,31 @@ def test_prefilter_1024_cosine(pkg, orc, nq, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nq,k", [(256, 10), (300, 64), (129, 128), (5, 1)])
+def test_prefilter_fp32_rows(pkg, orc, nq, k):
+    """fp32 collections (the reference's own dtype): one int8 launch of up to
+    256 queries over two 128-query f32 sample passes, survivors rescored on
+    the f32 pass's 16x16x4 chain -- its keys, bit for bit."""
+    a = pkg.VectorEngine(device=0)
+    b = pkg.VectorEngine(device=0, prefilter=False)
+    try:
+        n = 150_000
+        for e in (a, b):
+            e.create_collection("f", DIM, pkg.METRIC_COSINE, pkg.DTYPE_F32, n)
+            e.generate("f", n, 66)
+        assert a.prefilter_bytes("f") > 0 and b.prefilter_bytes("f") == 0
+        X = orc.generate(66, 0, n, DIM)
+        Q = orc.generate(orc.SEED_QUERY, 8000, nq, DIM)
+        s1, r1, c1 = a.search("f", Q, k)
+        _parity(orc, X, orc.preprocess(Q, True, False), s1, r1, c1, k)
+        s2, r2, c2 = b.search("f", Q, k)
+        assert np.array_equal(r1, r2) and np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
 def test_prefilter_follows_every_write(pkg, orc, tmp_path):
     rng = np.random.default_rng(5)
     e = pkg.VectorEngine(device=0)

@@ -44,11 +44,11 @@ int stats_mode(uint32_t n, uint32_t nq, uint32_t dim, uint32_t k) {
   CK(vsk::launch_generate(0x5EED, 0, n, dim, true, dX, 0, 0));
   CK(vsk::launch_generate(0xC0FFEE, 0, nq, dim, true, dQ, 0, 0));
   CK(hipMemset(glob, 0, 16));
-  CK(vsk::launch_q8_absmax(dX, (uint64_t)n * dim, glob, 0));
+  CK(vsk::launch_q8_absmax(dX, false, (uint64_t)n * dim, glob, 0));
   CK(vsk::launch_q8_set_scale(glob, 0));
-  CK(vsk::launch_q8_quantize(dX, n, dim, nullptr, 0, (n + 31) / 32, dX8, meta, glob, 0));
+  CK(vsk::launch_q8_quantize(dX, false, n, dim, nullptr, 0, (n + 31) / 32, dX8, meta, glob, 0));
   uint32_t* gate = (uint32_t*)(par + 4 * 256);
-  CK(vsk::launch_q8_query(dQ, nq, dim, glob, dQ8, par, gate, 0));
+  CK(vsk::launch_q8_query(dQ, false, nq, dim, glob, dQ8, par, gate, 0));
   const uint32_t nwg = vsk::mfma_max_lists(n), st = vsk::mfma_sample_tiles(n, dim, false);
   const uint32_t cap = vsk::mfma_cand_cap(n, k, st, 8.0);  // as search_mfma
   float* slabs;
@@ -69,7 +69,7 @@ int stats_mode(uint32_t n, uint32_t nq, uint32_t dim, uint32_t k) {
   CK(vsk::launch_sample_bound(tmax, L * st, nq, k, bound, 0));
   CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, bound, par, glob, slabs, tiles, cap, cnt,
                               cmx, nwg, &L, gate, 0));
-  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, dim, par, glob,
+  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, false, dim, par, glob,
                            meta, bound, gate, 0, stats));
   CK(hipDeviceSynchronize());
   std::vector<uint32_t> hc((size_t)nwg * 256 * 4);
@@ -128,11 +128,11 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dQ, Q.data(), Q.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemset(dX8, 0, (size_t)(n + 32) * dim));
   CK(hipMemset(glob, 0, 16));
-  CK(vsk::launch_q8_absmax(dX, (uint64_t)n * dim, glob, 0));
+  CK(vsk::launch_q8_absmax(dX, false, (uint64_t)n * dim, glob, 0));
   CK(vsk::launch_q8_set_scale(glob, 0));
-  CK(vsk::launch_q8_quantize(dX, n, dim, nullptr, 0, n / 32, dX8, meta, glob, 0));
+  CK(vsk::launch_q8_quantize(dX, false, n, dim, nullptr, 0, n / 32, dX8, meta, glob, 0));
   uint32_t* gate = (uint32_t*)(par + 4 * 256);
-  CK(vsk::launch_q8_query(dQ, nq, dim, glob, dQ8, par, gate, 0));
+  CK(vsk::launch_q8_query(dQ, false, nq, dim, glob, dQ8, par, gate, 0));
   uint32_t nwg = vsk::mfma_max_lists(n), tpw = vsk::mfma_tiles_per_wg(n);
   const uint32_t cap = 4 * tpw < 64 ? 64 : 4 * tpw;
   std::printf("nwg %u tiles/wg %u cap %u\n", nwg, tpw, cap);
@@ -219,7 +219,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(out, 0, 256 * k * 8));
   CK(vsk::launch_mfma_sample(dX, false, dim, n, 0, dQ, nq, k, st, tmax, nwg, &L, 0));
   CK(vsk::launch_sample_bound(tmax, L * st, nq, k, bound, 0));
-  CK(vsk::launch_q8_query(dQ, nq, dim, glob, dQ8, par, gate, 0));
+  CK(vsk::launch_q8_query(dQ, false, nq, dim, glob, dQ8, par, gate, 0));
   CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, bound, par, glob, slabs, tiles, cap,
                               cnt, cmx, nwg, &L, gate, 0));
   CK(hipDeviceSynchronize());
@@ -260,7 +260,7 @@ int main(int argc, char** argv) {
     std::printf("q %u host threshold %.1f; admitted slab maxima in [%d, %d]; best dot %d\n", q, th,
                 mn, mxall, best);
   }
-  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, dim, par, glob, meta,
+  CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, false, dim, par, glob, meta,
                            bound, gate, 0));
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(&hgate, gate, 4, hipMemcpyDeviceToHost));
