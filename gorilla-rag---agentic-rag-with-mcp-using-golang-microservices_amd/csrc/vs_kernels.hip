@@ -3225,9 +3225,9 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // {dt, nt} (largest quantisation-error norm and row norm of its 32 rows),
 // every slab row has L = sqS dot - m - sigma nt <= its fp32 score <= U =
 // sqS dot + m + sigma nt, m = a dt + c nt. From the quarters'
-// largest dots: per workgroup the largest L; the k-th largest of those is a
-// lower bound on the k-th score (k distinct rows reach it), and so is
-// b - sigma nmax (the sample bound). Rows whose U reaches the larger of the
+// largest dots: each quarter's largest L (global m); the k-th largest of
+// those is a lower bound on the k-th score (the quarters hold disjoint rows),
+// and so is b - sigma nmax (the sample bound). Rows whose U reaches the larger of the
 // two (read from the quarters whose largest U does) are the only ones that
 // can be in the top k; they are rescored from the bf16 rows on the bf16
 // pass's own MFMA chain -- the same score bits -- and the top k of those keys
@@ -3246,8 +3246,6 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, uint32_t* __restrict__ gate, uint32_t* __restrict__ stats) {
   __shared__ uint64_t buf[kMfmaSelBuf];
-  __shared__ uint64_t lmax[kMfmaMaxLists];
-  __shared__ int lmaxd[kMfmaMaxLists];
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint16_t owner[kSelChunk];
   __shared__ uint32_t wtot[kSelThreads / 64];
@@ -3276,23 +3274,16 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     x0 = c0 ? m0 : INT_MIN;
     x1 = c1 ? m1 : INT_MIN;
   }
-  if (tid < kMfmaMaxLists) lmaxd[tid] = INT_MIN, lmax[tid] = 0;
   if (tid == 0) fill = 0, spill = 0;
-  __syncthreads();
-  // per workgroup the largest dot -> its lower bound sqS dot - mg (k distinct
-  // rows reach the k-th largest of those, so it bounds the k-th score)
-  if (x0 != INT_MIN) atomicMax(&lmaxd[l0 >> 2], x0);
-  if (x1 != INT_MIN) atomicMax(&lmaxd[(l0 + 1) >> 2], x1);
-  __syncthreads();
-  if (tid < kMfmaMaxLists && lmaxd[tid] != INT_MIN)
-    lmax[tid] = make_key((float)lmaxd[tid] * sqS - mg, 0xFFFFFFFFu);
-  __syncthreads();
+  // Each quarter's largest dot gives its lower bound sqS dot - mg; the
+  // quarters hold disjoint rows, so k rows reach the k-th largest of those,
+  // which bounds the k-th score from below. (The k-th of per-workgroup
+  // maxima, the first form, sat far under the k-th score once k neared the
+  // 256 workgroups: at k = 50, 4578 survivors per query against 2821.)
   uint64_t thr = 0;
   if (k <= 64) {
-    // the k-th largest lower bound over all 4 nwg quarters (disjoint rows):
     // each wave keeps the top 64 of its 128 quarters in registers, wave 0
-    // merges the 8 lists (as many quarters as workgroups passed at k = 50,
-    // whose 50th-largest workgroup maximum sits far under the 50th score)
+    // merges the 8 lists
     const uint64_t y0 = x0 != INT_MIN ? make_key((float)x0 * sqS - mg, 0xFFFFFFFFu) : 0ull;
     const uint64_t y1 = x1 != INT_MIN ? make_key((float)x1 * sqS - mg, 0xFFFFFFFFu) : 0ull;
     buf[w * 64 + lane] = wave_merge_top(wave_sort_desc(y0, (int)lane),
@@ -3308,8 +3299,14 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     __syncthreads();
     thr = thr_sh;
   } else {
-    bitonic_sort_desc_n(lmax, (int)kMfmaMaxLists, kSelThreads);
-    thr = k <= kMfmaMaxLists ? lmax[k - 1] : 0;
+    // k > 64: the same bound from all 4 nwg <= 1024 quarters, sorted in LDS
+    const uint32_t nq4 = 2 * kSelThreads;
+    buf[l0] = x0 != INT_MIN ? make_key((float)x0 * sqS - mg, 0xFFFFFFFFu) : 0ull;
+    buf[l0 + 1] = x1 != INT_MIN ? make_key((float)x1 * sqS - mg, 0xFFFFFFFFu) : 0ull;
+    __syncthreads();
+    bitonic_sort_desc_n(buf, (int)nq4, kSelThreads);
+    thr = k <= nq4 ? buf[k - 1] : 0;
+    __syncthreads();  // buf is the survivors' buffer next
   }
   const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
   const float tl_l = thr ? key_score(thr) : -INFINITY;
