@@ -538,8 +538,9 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
   const uint32_t st = vsk::mfma_sample_tiles(n_rows, dim, f32);
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
-  // int8 prefilter (unfiltered batches of a collection with an int8 copy)
-  const bool q8 = fast && !allow && c.q8 && c.q8_cap >= c.rows && q8_enabled();
+  // int8 prefilter (batches of a collection with an int8 copy; a pre-mask
+  // rides along as in the bf16 pass)
+  const bool q8 = fast && c.q8 && c.q8_cap >= c.rows && q8_enabled();
   // the int8 pass admits ~5x the bf16 pass's rows (7.6k slabs per query at
   // 10M rows, k = 10; fullest quarter 29 -- tools/q8_check.hip stats mode):
   // sized at 8x so a full quarter (and the bf16 hand-back) stays rare
@@ -600,7 +601,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       for (uint32_t s0 = 0; s0 < nv; s0 += P) {
         const uint32_t ns = std::min(P, nv - s0);
         VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k, st,
-                                       tmax, maxl, &L, eng->stream, nullptr),
+                                       tmax, maxl, &L, eng->stream, allow),
                "mfma sample scan");
         VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream),
                "sample bound");
@@ -610,7 +611,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
       VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                       c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
-                                      eng->stream),
+                                      eng->stream, allow),
              "int8 scan");
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
@@ -622,10 +623,10 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
         const uint32_t ns = std::min(P, nv - s0);
         VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k,
                                      bound + s0, slabs, slab_tile, cap, cnt, maxl, &L, eng->stream,
-                                     nullptr, qmax_sel, gate),
+                                     allow, qmax_sel, gate),
                "mfma scan (int8 fallback)");
         VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, cnt, L, cap, ns, k, out + (size_t)s0 * k,
-                                        eng->stream, row_base, nullptr, qmax_sel, gate),
+                                        eng->stream, row_base, allow, qmax_sel, gate),
                "select (int8 fallback)");
       }
       VS_HIP(ev_end(eng, eng->merge_ev), "event");
@@ -1148,12 +1149,12 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
                                   c->data, stg.rows[j].as<uint64_t>(), 0, eng->stream),
            "upsert preprocess");
   }
-  const uint64_t old_rows = c->rows;
   c->rows = expect;
   if (q8_wanted(eng, *c)) {
-    // the tiles this call wrote: one range for rows in ascending order, else
-    // the distinct tiles of the (row-sorted) kept rows
-    if (ascending) {
+    // the tiles this call wrote: one range for dense ascending rows (an
+    // append), else the distinct tiles of the (row-sorted) kept rows
+    const uint64_t span = ascending ? rows[n - 1] / 32 - rows[0] / 32 + 1 : 0;
+    if (ascending && span <= n / 16 + 64) {
       rc = q8_after_write(eng, *c, rows[0], rows[n - 1] + 1);
     } else {
       std::vector<uint32_t> tl;
@@ -1168,7 +1169,6 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
              "tile list H2D");
       rc = q8_after_write(eng, *c, 0, 0, eng->q8_tiles.as<uint32_t>(), (uint32_t)tl.size());
     }
-    (void)old_rows;
     if (rc != VS_OK) return rc;
   }
   VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");

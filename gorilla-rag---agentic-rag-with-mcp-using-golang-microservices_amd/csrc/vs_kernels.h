@@ -223,7 +223,8 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // queries Q8 with per-query {sqS, a, c, sigma} (q8par) and admits every row
 // whose upper bound on its fp32 score reaches the sample bound;
 // launch_select_q8 bounds, rescores the survivors from the bf16 rows and
-// writes the top k. Any overflow (a full quarter, too many survivors) sets
+// writes the top k; `allow` (nullable) is the pre-mask, as the bf16 pass's.
+// Any overflow (a full quarter, too many survivors) sets
 // *gate, and the bf16 pass + select enqueued behind with run_if = gate
 // answer the batch instead. Exact: the answer is the bf16 pass's.
 // dims with an int8 pass: bf16 rows 768 / 1024, fp32 rows 768 (r04)
@@ -233,7 +234,8 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                const float* init_score, const float* q8par, const float* q8glob,
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
                                uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
-                               uint32_t* nlists, uint32_t* gate, hipStream_t st);
+                               uint32_t* nlists, uint32_t* gate, hipStream_t st,
+                               const uint64_t* allow = nullptr);
 // cand_max (same shape as cand_cnt): each quarter's largest appended dot
 // (int32; INT_MIN when empty), so the select reads only the quarters that
 // can hold a top-k row.

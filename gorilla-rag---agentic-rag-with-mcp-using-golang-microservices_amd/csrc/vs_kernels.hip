@@ -2333,7 +2333,8 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     if constexpr (I8 && MODE == 0) {
       // int8 prefilter: a lane whose largest dot of the tile reaches the
       // query's integer threshold appends its 8 dots (int32 bits) -- the
-      // select bounds and rescores them. No filter on this pass.
+      // select bounds and rescores them. Padding and filtered-out rows (the
+      // pre-mask am) are INT_MIN in the slab: never a maximum, never a survivor.
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
@@ -2343,10 +2344,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         int v[8];
 #pragma unroll
         for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
-        if (!full) {
+        if (!full || a.allow) {  // uniform: unfiltered full tiles skip it
 #pragma unroll
           for (int b = 0; b < 8; ++b)
-            if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1) v[b] = INT_MIN;
+            if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1 || !((am >> b) & 1u)) v[b] = INT_MIN;
           acc[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
           acc[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
         }
@@ -2708,7 +2709,8 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                const float* init_score, const float* q8par, const float* q8glob,
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
                                uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
-                               uint32_t* nlists, uint32_t* gate, hipStream_t st) {
+                               uint32_t* nlists, uint32_t* gate, hipStream_t st,
+                               const uint64_t* allow) {
   if (!q8_supported(dim, false) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
       cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate || !cand_max)
     return hipErrorInvalidValue;
@@ -2719,7 +2721,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
   a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.cand_max = cand_max;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
-  a.q8par = q8par, a.q8glob = q8glob, a.gate = gate;
+  a.q8par = q8par, a.q8glob = q8glob, a.gate = gate, a.allow = allow;
   if (dim == 1024) {
     hipLaunchKernelGGL((mfma_topk_kernel<1024, 0, 256, 1, false, true>), dim3(*nlists), dim3(512), 0,
                        st, a);

@@ -112,6 +112,32 @@ def test_prefilter_fp32_rows(pkg, orc, nq, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("density,k", [(0.3, 10), (0.6, 100), (0.2, 1)])
+def test_prefilter_filtered(pair, orc, density, k):
+    """A pre-mask rides along the int8 pass (masked rows never a maximum or a
+    survivor): the bf16 pass's filtered keys, bit for bit, and the oracle's."""
+    a, b = pair
+    rng = np.random.default_rng(int(density * 100) + k)
+    n = 300_000
+    mask = rng.random(n) < density
+    X = orc.generate(77, 0, n, DIM, bf16=True)
+    Q = orc.generate(orc.SEED_QUERY, 600, 256, DIM)
+    s1, r1, c1 = a.search_filtered("p", Q, k, mask)
+    s2, r2, c2 = b.search_filtered("p", Q, k, mask)
+    assert np.array_equal(r1, r2) and np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+    idx = np.flatnonzero(mask)
+    Qp = orc.preprocess(Q, False, True)
+    _, s64, rl, cc = orc.search(X[idx], Qp, k)
+    valid = np.arange(k)[None, :] < cc[:, None]
+    rr = np.where(valid, idx[np.where(valid, rl, 0).astype(np.int64)], 0).astype(np.uint64)
+    assert np.all(mask[r1[np.arange(k)[None, :] < c1[:, None]].astype(np.int64)])
+    pos = np.searchsorted(idx, r1.astype(np.int64)).astype(np.uint64)
+    resc = orc.rescore(X[idx], Qp, pos, c1)
+    bad = orc.check_topk(s1, r1, c1, s64, rr, cc, resc, SCORE_RTOL)
+    assert not bad, bad[:8]
+
+
+@pytest.mark.gpu
 def test_prefilter_follows_every_write(pkg, orc, tmp_path):
     rng = np.random.default_rng(5)
     e = pkg.VectorEngine(device=0)
