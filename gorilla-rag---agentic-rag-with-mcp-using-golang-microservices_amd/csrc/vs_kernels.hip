@@ -3248,10 +3248,12 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, uint32_t* __restrict__ gate, uint32_t* __restrict__ stats) {
   __shared__ uint64_t buf[kMfmaSelBuf];
+  __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
   __shared__ uint16_t owner[kSelChunk];
   __shared__ uint32_t wtot[kSelThreads / 64];
-  __shared__ uint32_t fill, spill;
+  __shared__ uint32_t wscr[kSelThreads / 64][16];  // a wave's group of 16 rows
+  __shared__ uint32_t fill, spill, rfill;
   __shared__ uint64_t thr_sh;
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (*gate) return;  // already handed to the bf16 pass (which rewrites every answer)
@@ -3276,7 +3278,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     x0 = c0 ? m0 : INT_MIN;
     x1 = c1 ? m1 : INT_MIN;
   }
-  if (tid == 0) fill = 0, spill = 0;
+  if (tid == 0) fill = 0, spill = 0, rfill = 0;
   // Each quarter's largest dot gives its lower bound sqS dot - mg; the
   // quarters hold disjoint rows, so k rows reach the k-th largest of those,
   // which bounds the k-th score from below. (The k-th of per-workgroup
@@ -3380,11 +3382,14 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       for (int bb = 0; bb < 8; ++bb) {
         const int dv = v[u][bb >> 2][bb & 3];
         if (dv == INT_MIN) continue;
-        if ((float)dv * sqS + mt >= Tcut) {
+        const float U = (float)dv * sqS + mt;
+        if (U >= Tcut) {
           const uint32_t row = tl[u] - row_base + 16u * (uint32_t)(bb >> 2) + 4u * (ls[u] & 3) +
                                (uint32_t)(bb & 3);
           const uint32_t pos = atomicAdd(&fill, 1u);
-          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = row; else spill = 1u;
+          // survivor entry: the upper bound's order-preserving image, the row
+          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = ((uint64_t)vs::score_ord(U) << 32) | row;
+          else spill = 1u;
         }
       }
     }
@@ -3409,7 +3414,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   constexpr int RBY = D * (F32 ? 4 : 2);  // row bytes
   constexpr int TS = RBY / 64;            // 64-B steps per row
   // rows past 24 steps (bf16 D = 1024, fp32): the query's fragments come from
-  // LDS, and fp32 rows are read in halves of 24 steps (96 VGPRs each)
+  // LDS, and rows are read in rounds of 16 / 24 steps
   constexpr bool kQL = TS > 24;
   constexpr int HS = TS % 24 == 0 ? 24 : (TS % 16 == 0 ? 16 : TS);  // steps held per round
   static_assert(TS % HS == 0, "whole rounds of steps");
@@ -3426,10 +3431,9 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       for (int t = 0; t < TS; ++t) qf[t] = qrow[4 * t + kq];
     }
   }
-  const uint32_t ngroups = (ns + 15) / 16;
-  for (uint32_t gi = w; gi < ngroups; gi += kSelThreads / 64) {
-    const uint32_t e = gi * 16 + (uint32_t)col;
-    const uint32_t r = (uint32_t)buf[e < ns ? e : gi * 16];
+  // the score of row r (lane col's) by the pass's chain; C[4 kq + i][col] =
+  // the score of the group's row 4 kq + i (every column alike)
+  auto score16 = [&](uint32_t r) -> f32x4_t {
     const uint4* xrow = (const uint4*)((const unsigned char*)X + (size_t)r * RBY);
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -3451,31 +3455,90 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
         }
       }
     }
-    // C[4 kq + i][col] = score of group row 4 kq + i (every column alike)
-    uint32_t rr[4];
+    return acc;
+  };
+  // Rescore the survivors buf[0, ns) whose entry passes `pred` into res: each
+  // wave takes 64 entries at a time and runs the passing ones in groups of
+  // 16 (ballot ranks place them in its wscr row), one slot reservation per
+  // group.
+  auto rescore_where = [&](auto pred) {
+    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
+      const uint32_t i = base + lane;
+      const uint64_t e = i < ns ? buf[i] : 0ull;
+      const bool pass = i < ns && pred(e);
+      const uint64_t bal = __ballot(pass);
+      const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      const uint32_t total = (uint32_t)__popcll(bal);
+      for (uint32_t g0 = 0; g0 < total; g0 += 16) {
+        if (pass && rank >= g0 && rank < g0 + 16) wscr[w][rank - g0] = (uint32_t)e;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t cnt16 = total - g0 < 16 ? total - g0 : 16;
+        const uint32_t r = wscr[w][(uint32_t)col < cnt16 ? col : 0];
+        const f32x4_t acc = score16(r);
+        uint32_t slot = 0;
+        if (lane == 0) slot = atomicAdd(&rfill, cnt16);
+        slot = (uint32_t)__shfl((int)slot, 0, 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t ei = gi * 16 + 4 * (uint32_t)kq + (uint32_t)i;
-      rr[i] = (uint32_t)__shfl((int)r, 4 * kq + i, 64);  // lane 4kq+i (col = 4kq+i, kq = 0) holds that row
-      if (col == 0 && ei < ns) buf[ei] = make_key(acc[i], row_base + rr[i]);
+        for (int ii = 0; ii < 4; ++ii) {
+          const uint32_t j = 4 * (uint32_t)kq + (uint32_t)ii;
+          const uint32_t rj = (uint32_t)__shfl((int)r, (int)j, 64);  // lane j (kq = 0) has row j
+          if (col == 0 && j < cnt16) res[slot + j] = make_key(acc[ii], row_base + rj);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
+  };
+  if (k <= 64 && ns > 64) {
+    // Two rounds (r04): the k survivors with the largest upper bounds first;
+    // the k-th best exact score among them, Sk, is at most the k-th score, so
+    // only survivors whose upper bound reaches Sk can still enter -- about
+    // half of them (the bound window shrinks from 2m to m)
+    uint64_t R = 0;
+    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
+      const uint64_t x = base + lane < ns ? buf[base + lane] : 0ull;
+      R = wave_merge_top(R, wave_sort_desc(x, (int)lane), (int)lane);
+    }
+    res[w * 64 + lane] = R;  // scratch: res is filled only after the barrier below
+    __syncthreads();
+    if (w == 0) {
+      uint64_t R0 = res[lane];
+#pragma unroll 1
+      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, res[v * 64 + lane], (int)lane);
+      const uint64_t uk = readlane64(R0, (int)k - 1);
+      if (lane == 0) thr_sh = uk;
+    }
+    __syncthreads();
+    const uint64_t Uk = thr_sh;  // survivor entries are distinct: exactly k reach it
+    rescore_where([&](uint64_t e) { return e >= Uk; });
+    __syncthreads();
+    if (w == 0) {
+      const uint32_t na = rfill;
+      const uint64_t x = wave_sort_desc((uint32_t)lane < na ? res[lane] : 0ull, (int)lane);
+      const uint64_t sk = readlane64(x, (int)k - 1);
+      if (lane == 0) thr_sh = sk;
+    }
+    __syncthreads();
+    const float Sk = key_score(thr_sh);
+    rescore_where([&](uint64_t e) { return e < Uk && vs::ord_score((uint32_t)(e >> 32)) >= Sk; });
+  } else {
+    rescore_where([&](uint64_t) { return true; });
   }
   if constexpr (SV == 3) return;
   __syncthreads();
-  if (ns <= 64) {
-    if (w == 0) sel_finish_wave(buf, ns, k, (int)lane, out + (size_t)q * k);
+  const uint32_t nr = rfill;
+  if (nr <= 64) {
+    if (w == 0) sel_finish_wave(res, nr, k, (int)lane, out + (size_t)q * k);
     return;
   }
   if (k <= 64) {
     // each wave keeps the top 64 of its share in registers (64 keys sorted
     // and merged at a time, no barrier), then wave 0 merges the 8 lists
     uint64_t R = 0;
-    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
-      const uint64_t x = base + lane < ns ? buf[base + lane] : 0ull;
+    for (uint32_t base = w * 64; base < nr; base += kSelThreads) {
+      const uint64_t x = base + lane < nr ? res[base + lane] : 0ull;
       R = wave_merge_top(R, wave_sort_desc(x, (int)lane), (int)lane);
     }
-    __syncthreads();  // every read of buf done
-    buf[w * 64 + lane] = R;
+    buf[w * 64 + lane] = R;  // buf is free
     __syncthreads();
     if (w == 0) {
       uint64_t R0 = buf[lane];
@@ -3486,11 +3549,11 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     return;
   }
   int p2 = 1;
-  while ((uint32_t)p2 < ns) p2 <<= 1;
-  for (uint32_t i = ns + tid; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+  while ((uint32_t)p2 < nr) p2 <<= 1;
+  for (uint32_t i = nr + tid; i < (uint32_t)p2; i += kSelThreads) res[i] = 0;
   __syncthreads();
-  bitonic_sort_desc_n(buf, p2, kSelThreads);
-  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < ns ? buf[j] : 0;
+  bitonic_sort_desc_n(res, p2, kSelThreads);
+  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nr ? res[j] : 0;
 }
 
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
