@@ -514,6 +514,16 @@ bool select_qmax() {
   return v;
 }
 
+// VS_Q8_SAMPLE=<factor>: overrides the int8 path's sample-tile factor (read
+// once; ablation only; 0 = the k-dependent default in search_mfma)
+double q8_sample_scale() {
+  static const double v = [] {
+    const char* e = std::getenv("VS_Q8_SAMPLE");
+    return e ? std::atof(e) : 0.0;
+  }();
+  return v;
+}
+
 // Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
 // queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
 //  1. sample pass over 1/128 of every workgroup's tiles -> tile maxima ->
@@ -536,15 +546,26 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
   const bool fast = tpw >= 8;
   if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
-  const uint32_t st = vsk::mfma_sample_tiles(n_rows, dim, f32);
-  const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   // int8 prefilter (batches of a collection with an int8 copy; a pre-mask
   // rides along as in the bf16 pass)
   const bool q8 = fast && c.q8 && c.q8_cap >= c.rows && q8_enabled();
+  // The int8 path's sample grows with k: its admission window (2m) is wider
+  // than the bf16 pass's, so a tighter k-th bound pays for more sample tiles
+  // sooner (r04 sweep, profiles/r04_q8_sample_sweep.jsonl: x2 for k in 17..64,
+  // x4 above; k = 50 at 10M +6%, k = 100 +7%; k <= 16 flat)
+  const uint32_t st0 = vsk::mfma_sample_tiles(n_rows, dim, f32);
+  uint32_t st = st0;
+  if (q8) {
+    const double f = q8_sample_scale() > 0 ? q8_sample_scale() : (k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0);
+    st = (uint32_t)std::max(1.0, std::min({(double)vsk::kMfmaMaxSampleTiles, (double)tpw, st * f}));
+  }
+  const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
   // the int8 pass admits ~5x the bf16 pass's rows (7.6k slabs per query at
   // 10M rows, k = 10; fullest quarter 29 -- tools/q8_check.hip stats mode):
   // sized at 8x so a full quarter (and the bf16 hand-back) stays rare
-  const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st, 8.0) : 0;
+  // (at the unscaled sample size: a tighter bound shrinks the bf16-like part
+  // of the admissions, not the window's)
+  const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st0, 8.0) : 0;
   const uint32_t capx = std::max(cap, cap8);
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds
