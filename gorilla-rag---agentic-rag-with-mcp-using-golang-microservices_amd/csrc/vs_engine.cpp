@@ -524,6 +524,15 @@ double q8_sample_scale() {
   return v;
 }
 
+// VS_SAMPLE_SCALE=<factor>: the same for the bf16 / f32 pass (ablation only)
+double plain_sample_scale() {
+  static const double v = [] {
+    const char* e = std::getenv("VS_SAMPLE_SCALE");
+    return e ? std::atof(e) : 0.0;
+  }();
+  return v;
+}
+
 // Batched scan on MFMA: bf16 rows on 16x16x32 bf16 MFMA (256
 // queries per pass at dim <= 768), fp32 rows on 16x16x4 f32 MFMA (128):
 //  1. sample pass over 1/128 of every workgroup's tiles -> tile maxima ->
@@ -555,8 +564,10 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   // x4 above; k = 50 at 10M +6%, k = 100 +7%; k <= 16 flat)
   const uint32_t st0 = vsk::mfma_sample_tiles(n_rows, dim, f32);
   uint32_t st = st0;
-  if (q8) {
-    const double f = q8_sample_scale() > 0 ? q8_sample_scale() : (k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0);
+  if (q8 || plain_sample_scale() > 0) {
+    const double f = !q8 ? plain_sample_scale()
+                         : q8_sample_scale() > 0 ? q8_sample_scale()
+                                                 : (k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0);
     st = (uint32_t)std::max(1.0, std::min({(double)vsk::kMfmaMaxSampleTiles, (double)tpw, st * f}));
   }
   const uint32_t cap = vsk::mfma_cand_cap(n_rows, k, st);
