@@ -524,6 +524,16 @@ double q8_sample_scale() {
   return v;
 }
 
+// VS_Q8_PREP_APART=1: the int8 queries in their own launch (the r04 form
+// before the fused bound + query launch; ablation only, read once)
+bool q8_prep_apart() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_PREP_APART");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // VS_SAMPLE_SCALE=<factor>: the same for the bf16 / f32 pass (ablation only)
 double plain_sample_scale() {
   static const double v = [] {
@@ -627,16 +637,25 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       const uint32_t nv = std::min(P8, nq - q0);
       uint64_t* out = d_keys + (size_t)q0 * k;
       uint32_t L = 0;
-      VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream),
-             "int8 queries");
-      // 1. sample pass(es) -> per-query lower bounds on the k-th score
+      // 1. sample pass(es) -> per-query lower bounds on the k-th score; the
+      // first bound launch also makes the batch's int8 queries and zeroes *gate
       for (uint32_t s0 = 0; s0 < nv; s0 += P) {
         const uint32_t ns = std::min(P, nv - s0);
         VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k, st,
                                        tmax, maxl, &L, eng->stream, allow),
                "mfma sample scan");
-        VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream),
-               "sample bound");
+        if (s0 == 0 && !q8_prep_apart()) {
+          VS_HIP(vsk::launch_sample_bound_q8(tmax, L * st, ns, k, bound, qptr(q0), f32, nv, dim,
+                                             c.q8_glob, q8q, q8par, gate, eng->stream),
+                 "sample bound + int8 queries");
+        } else {
+          if (s0 == 0)
+            VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate,
+                                        eng->stream),
+                   "int8 queries");
+          VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream),
+                 "sample bound");
+        }
       }
       // 2. int8 pass -> bounded candidates -> rescored top k; the bf16 / f32
       // pass and select behind it run only if the int8 pass overflowed (*gate)

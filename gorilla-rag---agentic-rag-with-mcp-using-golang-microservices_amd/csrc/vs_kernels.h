@@ -264,6 +264,14 @@ hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t
 // Also zeroes *gate (the batch's overflow word) ahead of the int8 pass.
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st);
+// launch_sample_bound (nq_bound queries) and launch_q8_query (nq queries) as
+// one launch: the int8 path's per-batch prep, one dispatch fewer (r04).
+hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,
+                                  float* bound, const void* q, bool f32, uint32_t nq,
+                                  uint32_t dim, const float* glob, int8_t* q8, float* q8par,
+                                  uint32_t* gate, hipStream_t st);
+// Radix passes of the sample bound (VS_BOUND_PASSES, read once; default 2).
+int sample_bound_passes();
 // Sample tiles per workgroup, and the main pass's candidate capacity per
 // (workgroup, query) sized from the expected survivors of the sample bound.
 uint32_t mfma_sample_tiles(uint32_t n_rows, uint32_t dim = 768, bool f32 = false);

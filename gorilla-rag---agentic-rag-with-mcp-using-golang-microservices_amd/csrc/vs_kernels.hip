@@ -23,6 +23,7 @@
 #include <math.h>
 
 #include "vs_common.h"
+#include "vs_bound_dev.h"
 #include "vs_kernels.h"
 
 namespace vsk {
@@ -3125,66 +3126,16 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
 // rows and did not make the main pass faster, so two stay the default).
 // Fewer than k maxima give -inf: every row is then admitted.
 // ---------------------------------------------------------------------------
-constexpr int kBoundThreads = 256;
-
-__device__ __forceinline__ uint32_t ord_f32(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float unord_f32(uint32_t u) {
-  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
-}
-
 __global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
     const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound,
     int passes) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t wsum[kBoundThreads / 64];
-  __shared__ uint32_t pick, above;
-  const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (m < k) {
-    if (tid == 0) bound[q] = -INFINITY;
-    return;
-  }
-  const float* v = tmax + (size_t)q * m;
-  uint32_t prefix = 0, kk = k;  // the kk-th largest of the values matching prefix
-#pragma unroll 1
-  for (int pass = 0; pass < passes; ++pass) {
-    const int shift = 24 - 8 * pass;
-    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-    hist[tid] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < m; i += kBoundThreads) {
-      const uint32_t u = ord_f32(v[i]);
-      if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    // inclusive scan over the digits in descending order (thread t: digit 255 - t)
-    const uint32_t c = hist[255 - tid];
-    uint32_t x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    for (uint32_t j = 0; j < w; ++j) x += wsum[j];
-    // exactly one digit has (count above) < kk <= (count above + its own)
-    if (x >= kk && x - c < kk) pick = tid, above = x - c;
-    __syncthreads();
-    prefix |= (uint32_t)(255 - pick) << shift;
-    kk -= above;
-    __syncthreads();  // pick / above / wsum / hist are rewritten by the next pass
-  }
-  // the bucket of -inf starts below ord(-inf), in the negative-NaN codes
-  if (tid == 0) bound[q] = prefix <= ord_f32(-INFINITY) ? -INFINITY : unord_f32(prefix);
+  sample_bound_block(tmax, m, k, bound, passes, blockIdx.x);  // vs_bound_dev.h
 }
 
 // Radix passes of the sample bound (VS_BOUND_PASSES, read once; 2 = the
 // 16-bit bucket floor, up to 2^-7 relative under the k-th maximum; 4 = the
 // k-th maximum exactly, a tighter bound: fewer main-pass candidates)
-static int bound_passes() {
+int sample_bound_passes() {
   static const int v = [] {
     const char* e = getenv("VS_BOUND_PASSES");
     const int x = e ? atoi(e) : 2;
@@ -3197,7 +3148,7 @@ hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint3
                                float* bound, hipStream_t st) {
   if (nq == 0 || nq > kMfmaQueries || k == 0 || k > kMfmaMaxK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_bound_kernel, dim3(nq), dim3(kBoundThreads), 0, st, tmax, m, k, bound,
-                     bound_passes());
+                     sample_bound_passes());
   return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "vs_bound_dev.h"
 #include "vs_common.h"
 #include "vs_kernels.h"
 
@@ -147,13 +148,13 @@ __global__ __launch_bounds__(256) void q8_quantize_kernel(
 // One wave per query (bf16 queries of a bf16 collection, or the fp32
 // preprocessed queries of an fp32 one).
 template <bool F32>
-__global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ qb, uint32_t nq,
-                                                       uint32_t dim, const float* __restrict__ glob,
-                                                       int8_t* __restrict__ q8,
-                                                       float* __restrict__ q8par,
-                                                       uint32_t* __restrict__ gate) {
-  if (gate && blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
-  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restrict__ qb,
+                                               uint32_t nq, uint32_t dim,
+                                               const float* __restrict__ glob,
+                                               int8_t* __restrict__ q8, float* __restrict__ q8par,
+                                               uint32_t* __restrict__ gate) {
+  if (gate && blk == 0 && threadIdx.x == 0) *gate = 0u;
+  const uint32_t i = blk * 4 + (threadIdx.x >> 6);
   if (i >= nq) return;
   const int lane = threadIdx.x & 63;
   const uint64_t x = (uint64_t)i * dim;
@@ -194,6 +195,29 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ 
     p[2] = norm_up(cc);
     p[3] = sigma;
   }
+}
+
+template <bool F32>
+__global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ qb, uint32_t nq,
+                                                       uint32_t dim, const float* __restrict__ glob,
+                                                       int8_t* __restrict__ q8,
+                                                       float* __restrict__ q8par,
+                                                       uint32_t* __restrict__ gate) {
+  q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate);
+}
+
+// Workgroups [0, nq_bound): the sample bound of query blockIdx.x; the rest:
+// four queries' int8 image each (the two never share data).
+template <bool F32>
+__global__ __launch_bounds__(kBoundThreads) void sample_bound_q8_kernel(
+    const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound, int passes,
+    uint32_t nq_bound, const void* __restrict__ qb, uint32_t nq, uint32_t dim,
+    const float* __restrict__ glob, int8_t* __restrict__ q8, float* __restrict__ q8par,
+    uint32_t* __restrict__ gate) {
+  if (blockIdx.x < nq_bound)
+    sample_bound_block(tmax, m, k, bound, passes, blockIdx.x);
+  else
+    q8_query_block<F32>(blockIdx.x - nq_bound, qb, nq, dim, glob, q8, q8par, gate);
 }
 
 }  // namespace
@@ -242,6 +266,25 @@ hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, c
   else
     hipLaunchKernelGGL(q8_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
                        glob, q8, q8par, gate);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,
+                                  float* bound, const void* q, bool f32, uint32_t nq,
+                                  uint32_t dim, const float* glob, int8_t* q8, float* q8par,
+                                  uint32_t* gate, hipStream_t st) {
+  static_assert(kBoundThreads == 256, "four query waves per workgroup");
+  if (dim % 128 || dim == 0 || nq == 0 || nq_bound == 0 || nq_bound > kMfmaQueries || k == 0 ||
+      k > kMfmaMaxK)
+    return hipErrorInvalidValue;
+  const dim3 grid(nq_bound + (nq + 3) / 4);
+  const int passes = sample_bound_passes();
+  if (f32)
+    hipLaunchKernelGGL(sample_bound_q8_kernel<true>, grid, dim3(kBoundThreads), 0, st, tmax, m, k,
+                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate);
+  else
+    hipLaunchKernelGGL(sample_bound_q8_kernel<false>, grid, dim3(kBoundThreads), 0, st, tmax, m, k,
+                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate);
   return hipGetLastError();
 }
 
