@@ -3206,6 +3206,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t wscr[kSelThreads / 64][16];  // a wave's group of 16 rows
   __shared__ uint32_t fill, spill, rfill;
   __shared__ uint64_t thr_sh;
+  __shared__ uint32_t hist[256], hws[4], hpick, habove;  // kth_floor's radix state
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (*gate) return;  // already handed to the bf16 pass (which rewrites every answer)
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
@@ -3339,7 +3340,9 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
                                (uint32_t)(bb & 3);
           const uint32_t pos = atomicAdd(&fill, 1u);
           // survivor entry: the upper bound's order-preserving image, the row
-          if (pos < (uint32_t)kMfmaSelBuf) buf[pos] = ((uint64_t)vs::score_ord(U) << 32) | row;
+          // (-0 as +0, as make_key ranks it: images compare across the two)
+          if (pos < (uint32_t)kMfmaSelBuf)
+            buf[pos] = ((uint64_t)vs::score_ord(U == 0.0f ? 0.0f : U) << 32) | row;
           else spill = 1u;
         }
       }
@@ -3439,7 +3442,61 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       }
     }
   };
-  if (k <= 64 && ns > 64) {
+  // (k > 64) The floor P of the 24-bit bucket holding the kk-th largest high
+  // word (an order-preserving score image) of v[0, n), n >= kk: at least kk
+  // entries have a high word >= P. Three 8-bit radix passes as the sample
+  // bound (vs_bound_dev.h), over LDS.
+  auto kth_floor = [&](const uint64_t* v, uint32_t n, uint32_t kk) -> uint32_t {
+    uint32_t prefix = 0;
+#pragma unroll 1
+    for (int pass = 0; pass < 3; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < n; i += kSelThreads) {
+        const uint32_t u = (uint32_t)(v[i] >> 32);
+        if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      uint32_t c = 0, x = 0;
+      if (tid < 256) {
+        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
+        x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) hws[w] = x;
+      }
+      __syncthreads();
+      if (tid < 256) {
+        for (uint32_t j = 0; j < w; ++j) x += hws[j];
+        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
+      }
+      __syncthreads();
+      prefix |= (255u - hpick) << shift;
+      kk -= habove;
+      __syncthreads();  // hist / hws / hpick are rewritten by the next pass
+    }
+    return prefix;
+  };
+  if (k > 64 && ns > k + 64) {
+    // Two rounds for k > 64 (r04): the same as below with radix floors for
+    // the two k-th values -- survivors whose U image reaches P1 (>= k of
+    // them) first; P2, the floor of the k-th best exact score among those,
+    // is at most the k-th score, so only survivors under P1 whose U reaches
+    // P2 can still enter.
+    const uint32_t P1 = kth_floor(buf, ns, k);
+    rescore_where([&](uint64_t e) { return (uint32_t)(e >> 32) >= P1; });
+    __syncthreads();
+    const uint32_t P2 = kth_floor(res, rfill, k);
+    rescore_where([&](uint64_t e) {
+      const uint32_t u = (uint32_t)(e >> 32);
+      return u < P1 && u >= P2;
+    });
+  } else if (k <= 64 && ns > 64) {
     // Two rounds (r04): the k survivors with the largest upper bounds first;
     // the k-th best exact score among them, Sk, is at most the k-th score, so
     // only survivors whose upper bound reaches Sk can still enter -- about
@@ -3499,12 +3556,29 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     }
     return;
   }
+  // k > 64: the keys whose score image reaches the floor of the k-th (at
+  // least k, a few more in its bucket) into buf, sorted there
+  const uint64_t* fin = res;
+  uint32_t nf = nr;
+  if (nr > 256) {
+    const uint32_t P3 = kth_floor(res, nr, k);
+    if (tid == 0) fill = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < nr; i += kSelThreads) {
+      const uint64_t e = res[i];
+      if ((uint32_t)(e >> 32) >= P3) buf[atomicAdd(&fill, 1u)] = e;
+    }
+    __syncthreads();
+    fin = buf;
+    nf = fill;
+  }
+  uint64_t* srt = const_cast<uint64_t*>(fin);
   int p2 = 1;
-  while ((uint32_t)p2 < nr) p2 <<= 1;
-  for (uint32_t i = nr + tid; i < (uint32_t)p2; i += kSelThreads) res[i] = 0;
+  while ((uint32_t)p2 < nf) p2 <<= 1;
+  for (uint32_t i = nf + tid; i < (uint32_t)p2; i += kSelThreads) srt[i] = 0;
   __syncthreads();
-  bitonic_sort_desc_n(res, p2, kSelThreads);
-  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nr ? res[j] : 0;
+  bitonic_sort_desc_n(srt, p2, kSelThreads);
+  for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nf ? srt[j] : 0;
 }
 
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
