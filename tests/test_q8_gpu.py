@@ -225,3 +225,30 @@ def test_prefilter_flag_and_symbol(pkg):
     hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "vsearch.h")).read()
     assert re.search(r"#define VS_FLAG_NO_PREFILTER 32u", hdr)
     assert "vs_collection_prefilter_bytes" in hdr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [65, 100, 128])
+def test_prefilter_large_k_ties(pkg, orc, k):
+    """k > 64 (radix floors for the two rounds and the final sort): 700
+    copies of one row that the queries favour make the k-th bucket all ties;
+    the keys must still be the bf16 pass's (ties ordered by row)."""
+    a = pkg.VectorEngine(device=0)
+    b = pkg.VectorEngine(device=0, prefilter=False)
+    try:
+        n = 200_000
+        X = orc.generate(41, 0, n, DIM, bf16=True)
+        X[50_000:50_700] = X[7]
+        for e in (a, b):
+            e.create_collection("t", DIM, pkg.METRIC_DOT, pkg.DTYPE_BF16)
+            e.upsert("t", np.arange(n), X)
+        assert a.prefilter_bytes("t") > 0
+        Q = orc.generate(orc.SEED_QUERY, 1200, 130, DIM)
+        Q[::2] += 0.5 * X[7]
+        s1, r1, c1 = a.search("t", Q, k)
+        _parity(orc, X, orc.preprocess(Q, False, True), s1, r1, c1, k)
+        s2, r2, c2 = b.search("t", Q, k)
+        assert np.array_equal(r1, r2) and np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+    finally:
+        a.close()
+        b.close()
