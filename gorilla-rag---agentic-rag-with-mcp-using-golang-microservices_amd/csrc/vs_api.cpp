@@ -718,7 +718,8 @@ int sharded_create(vs_engine* E, const char* name, uint32_t dim, int metric, int
     // the whole collection on the device with the fewest reserved bytes
     // (then the fewest collections, then the lowest index)
     sc->iname.push_back(std::string(name) + "\x1fp");
-    sc->reserved = capacity_hint * dim * (dtype == VS_DTYPE_BF16 ? 2u : 4u);
+    sc->reserved = capacity_hint * dim * (dtype == VS_DTYPE_BF16 ? 2u : 4u) +
+                   vsd::q8_reserve_bytes(E->dev[0]->flags, dim, dtype, capacity_hint);
     {
       std::lock_guard<std::mutex> g(E->map_mu);
       if (E->colls.count(name))

@@ -375,5 +375,9 @@ bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered);
 int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, uint32_t k,
                 uint64_t* d_keys, const uint64_t* allow = nullptr, uint64_t allowed = 0,
                 const uint32_t* allow_list = nullptr, HostDirect* direct = nullptr);
+// Bytes of the int8 copy a collection of `rows` rows would keep on an engine
+// opened with `flags` (0 when it keeps none): placement reserves them beside
+// the rows.
+uint64_t q8_reserve_bytes(int flags, uint32_t dim, int dtype, uint64_t rows);
 
 }  // namespace vsd

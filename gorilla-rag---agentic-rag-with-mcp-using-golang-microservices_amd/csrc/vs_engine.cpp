@@ -149,6 +149,13 @@ constexpr uint32_t kF32MfmaMinQueries = 4;
 // Grows a collection to hold `need` rows (writer lock held by the caller).
 int grow(DevEngine* eng, Collection& c, uint64_t need) {
   if (need <= c.cap) return VS_OK;
+  // The int8 copy is rebuilt at the new capacity anyway (q8_after_write:
+  // q8_cap < cap), so free it first: the peak of a grow stays old + new rows,
+  // not old + new + the old copy. No pass may still read it.
+  if (c.q8) {
+    VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+    c.q8_free();
+  }
   uint64_t ncap = std::max<uint64_t>({need, c.cap + c.cap / 2, 1024});
   void* nd = nullptr;
   hipError_t e = hipMalloc(&nd, (ncap + kPadRows) * c.row_bytes());
@@ -194,6 +201,13 @@ bool q8_wanted(const DevEngine* eng, const Collection& c) {
          c.rows < 0xFFFFFFFFull && vsk::mfma_tiles_per_wg((uint32_t)c.rows) >= 8;
 }
 
+uint64_t q8_reserve_bytes(int flags, uint32_t dim, int dtype, uint64_t rows) {
+  if (!q8_enabled() || (flags & VS_FLAG_NO_PREFILTER) || rows >= 0xFFFFFFFFull ||
+      !vsk::q8_supported(dim, dtype == VS_DTYPE_F32) || vsk::mfma_tiles_per_wg((uint32_t)rows) < 8)
+    return 0;
+  return (rows + kPadRows) * dim + ((rows + kPadRows) / 32 + 1) * 8;
+}
+
 // Brings the int8 copy up to date after a store-side write of rows [r0, r1)
 // (or, with d_tiles, of the nt tiles listed there), on eng->stream, the
 // writer lock and work_mu held, c.rows already counting the new rows. The
@@ -202,8 +216,35 @@ bool q8_wanted(const DevEngine* eng, const Collection& c) {
 // S was chosen (rows quantised with an older S stay exact: their error
 // bounds are measured, not assumed). No memory for the copy: none is kept,
 // and batched searches read the bf16 rows.
+int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
+                        const uint32_t* d_tiles, uint32_t nt);
+
+// Any failure after the rows were written leaves the copy behind the rows, and
+// its bounds would no longer cover them: drop it (batched searches then take
+// the bf16 / f32 pass until the next full rebuild).
+// VS_Q8_FAIL_AFTER_WRITE=1 (tests only, read once) injects such a failure.
+bool q8_fail_injected() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_FAIL_AFTER_WRITE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
                    const uint32_t* d_tiles = nullptr, uint32_t nt = 0) {
+  int rc = q8_fail_injected() && c.q8
+               ? fail(VS_ERR_DEVICE, "int8 copy: injected failure (VS_Q8_FAIL_AFTER_WRITE)")
+               : q8_after_write_impl(eng, c, r0, r1, d_tiles, nt);
+  if (rc != VS_OK && c.q8) {
+    (void)hipStreamSynchronize(eng->stream);
+    c.q8_free();
+  }
+  return rc;
+}
+
+int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
+                        const uint32_t* d_tiles, uint32_t nt) {
   if (!q8_wanted(eng, c)) return VS_OK;
   const uint32_t dim = c.dim;
   const uint32_t rows = (uint32_t)c.rows;
@@ -1201,6 +1242,9 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
            "upsert preprocess");
   }
   c->rows = expect;
+  // the tile list outlives the final synchronize: its H2D copy reads pageable
+  // memory, which HIP may still be consuming after hipMemcpyAsync returns
+  std::vector<uint32_t> tl;
   if (q8_wanted(eng, *c)) {
     // the tiles this call wrote: one range for dense ascending rows (an
     // append), else the distinct tiles of the (row-sorted) kept rows
@@ -1208,17 +1252,22 @@ int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim_in,
     if (ascending && span <= n / 16 + 64) {
       rc = q8_after_write(eng, *c, rows[0], rows[n - 1] + 1);
     } else {
-      std::vector<uint32_t> tl;
       for (uint64_t t = 0; t < m; ++t) {
         const uint32_t ti = (uint32_t)(row_of(t) / 32);
         if (tl.empty() || tl.back() != ti) tl.push_back(ti);
       }
-      VS_HIP(hipStreamSynchronize(eng->stream), "upsert sync");  // q8_tiles is free
-      VS_HIP(eng->q8_tiles.ensure(tl.size() * 4), "alloc tile list");
-      VS_HIP(hipMemcpyAsync(eng->q8_tiles.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice,
-                            eng->stream),
-             "tile list H2D");
-      rc = q8_after_write(eng, *c, 0, 0, eng->q8_tiles.as<uint32_t>(), (uint32_t)tl.size());
+      hipError_t e = hipStreamSynchronize(eng->stream);  // q8_tiles is free
+      if (e == hipSuccess) e = eng->q8_tiles.ensure(tl.size() * 4);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(eng->q8_tiles.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice,
+                           eng->stream);
+      rc = e != hipSuccess ? fail_hip(e, "int8 copy: tile list")
+                           : q8_after_write(eng, *c, 0, 0, eng->q8_tiles.as<uint32_t>(),
+                                            (uint32_t)tl.size());
+      if (rc != VS_OK && c->q8) {  // the rows are written; the copy is now stale
+        (void)hipStreamSynchronize(eng->stream);
+        c->q8_free();
+      }
     }
     if (rc != VS_OK) return rc;
   }

@@ -1943,7 +1943,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // candidate passes keep each lane's per-group append counters in LDS (a
   // register each would push the kernel past 256 VGPRs, and the compiler
   // then drops the A-fragment prefetch of the streaming loop: r01)
-  constexpr int kCntBytes = MODE == 0 ? 64 * WAVES * G * 4 : 0;
+  // VAR 131072 (ablation): counters in LDS, and each lane's running quarter
+  // maximum beside them (a second set), so cand_max is written in that form too
+  constexpr bool kLdsCnt = MODE == 0 && (VAR & 131072) != 0;
+  constexpr int kCntBytes = MODE == 0 ? 64 * WAVES * G * 4 * (kLdsCnt ? 2 : 1) : 0;
   using S = MfShape<D, kBigRing ? 144 * 1024 : kMfRingBytes,
                     MODE == 8 ? kMfListBytes : 16 + kCntBytes, WAVES, kCsx, EB>;
   constexpr bool kDma = MODE != 4 && MODE != 5;  // ablation modes without the stream
@@ -2090,6 +2093,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     // (the register-count main pass keeps each lane's running quarter maximum
     // here instead: score_ord of the largest admitted score, 0 = none)
     if constexpr (kCntBytes > 0) cntl[g * THREADS + threadIdx.x] = 0u;
+    if constexpr (kLdsCnt) cntl[(G + g) * THREADS + threadIdx.x] = 0u;
     if constexpr (kRegCnt) {
       cnt_r[g] = 0u;
       slot0[g] = (uint32_t)(((size_t)blockIdx.x * kMfmaQueries +
@@ -2462,6 +2466,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
             cntl[g * THREADS + threadIdx.x] = cg + 1;
+            mf_quarter_max(cntl, (G + g) * THREADS, mx);
           }
         }
         continue;
@@ -2528,10 +2533,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     if constexpr (MODE == 0) {
       a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
           kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
-      if constexpr (kRegCnt)
-        if (a.cand_max)
-          a.cand_max[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
-              I8 ? (uint32_t)qmx_r[g] : cntl[g * THREADS + threadIdx.x];
+      if (a.cand_max)
+        a.cand_max[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
+            kRegCnt ? (I8 ? (uint32_t)qmx_r[g] : cntl[g * THREADS + threadIdx.x])
+                    : cntl[(G + g) * THREADS + threadIdx.x];
     } else if constexpr (MODE == 3) {
       // a workgroup with fewer tiles than max_tiles: the rest are empty
       for (uint32_t t = ntiles + kq; t < a.max_tiles; t += 4)

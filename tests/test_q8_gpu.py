@@ -252,3 +252,58 @@ def test_prefilter_large_k_ties(pkg, orc, k):
     finally:
         a.close()
         b.close()
+
+
+_FAIL_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+e = pkg.VectorEngine(device=0)
+n0, dim = 200_000, 768
+e.create_collection("f", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16)
+e.generate("f", n0, 41)  # first copy: built (nothing to be stale yet)
+assert e.prefilter_bytes("f") > 0
+rng = np.random.default_rng(3)
+Q = (rng.standard_normal((16, dim)) / np.sqrt(dim)).astype(np.float32)
+ids = np.array([7, 150_001, 99_999], dtype=np.uint64)
+V = np.stack([3.0 * Q[0], 3.0 * Q[1], 3.0 * Q[2]]).astype(np.float32)
+failed = False
+try:
+    e.upsert("f", ids, V)  # the rows are written, the int8 refresh fails
+except Exception as ex:
+    failed = "injected" in str(ex)
+assert failed, "the injected failure did not surface"
+assert e.prefilter_bytes("f") == 0, "stale int8 copy kept after a failed refresh"
+X = orc.generate(41, 0, n0, dim, bf16=True)
+X[ids.astype(np.int64)] = orc.preprocess(V, False, True)
+Qp = orc.preprocess(Q, False, True)
+s, r, c = e.search("f", Q, 10)
+_, s64, rows, cnt = orc.search(X, Qp, 10)
+bad = orc.check_topk(s, r, c, s64, rows, cnt, orc.rescore(X, Qp, r, c), 1e-5)
+assert not bad, bad[:4]
+for i in range(3):
+    assert int(ids[i]) == int(r[i, 0])
+e.close()
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+def test_prefilter_dropped_on_failed_refresh(tmp_path):
+    """a failure after the store-side write (here injected with
+    VS_Q8_FAIL_AFTER_WRITE=1, read once per process, so in a child process)
+    must not leave a stale int8 copy whose bounds miss the new rows: the copy
+    is dropped and batched searches answer from the bf16 pass."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "fail_refresh.py"
+    script.write_text(_FAIL_SCRIPT)
+    env = dict(os.environ, VS_Q8_FAIL_AFTER_WRITE="1")
+    p = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout[-2000:] + p.stderr[-2000:]

@@ -1,7 +1,7 @@
 """Builds profiles/pmc_traffic.json from rocprofv3 --pmc FETCH_SIZE runs of bench.py.
 
     python tools/pmc_traffic.py TAG c3=gpurun_out/pmc_c3/run_counter_collection.csv \
-        c3b1=... c2=...
+        c3b1=... c2=... c3_i8@1250000=...   (cfg@ROWS: a run with --rows ROWS)
 
 HBM bytes per launch = FETCH_SIZE (KB) x 1024 x 2 (the gfx950 correction,
 MI355X_MICROARCH.md HBM/rocprofv3 section), averaged over the scan kernel's
@@ -24,6 +24,12 @@ SCAN = {"c3": "mfma_topk_kernel<768, 0, 2304, 2, false, false>",
         "c4b1": "gemv_topk_kernel<768, true, 2", "c5b256": "mfma_topk_kernel<1024, 0,"}
 
 
+# each config's corpus rows (bench.py CONFIGS) for entries measured at N = 1
+DEFAULT_ROWS = {"c3": 10_000_000, "c3b1": 10_000_000, "c2": 1_000_000, "c2b256": 1_000_000,
+                "c3f32": 10_000_000, "c3f32b1": 10_000_000, "c5b256": 5_000_000,
+                "c4": 100_000_000, "c4b1": 100_000_000}
+
+
 def main():
     tag, specs = sys.argv[1], sys.argv[2:]
     # entries for configs not re-measured this time are kept
@@ -34,7 +40,8 @@ def main():
                    "of `python bench.py --config <cfg> --steps 5 --warmup 2`; each entry names "
                    "its build")
     for spec in specs:
-        cfg, path = spec.split("=", 1)
+        key, path = spec.split("=", 1)
+        cfg, _, rows = key.partition("@")
         vals, name = [], None
         for r in csv.DictReader(open(path)):
             if SCAN[cfg] in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
@@ -43,8 +50,11 @@ def main():
         if not vals:
             raise SystemExit(f"no FETCH_SIZE rows for {SCAN[cfg]} in {path}")
         kb = sum(vals) / len(vals)
-        out[cfg] = {"kernel": name, "launches": len(vals), "fetch_size_kb_avg": round(kb, 1),
-                    "hbm_bytes_per_launch": int(kb * 1024 * 2), "build": tag}
+        # rows one launch scanned: bench.py reports the entry only for a run
+        # whose rows_per_gpu equals it (an N > 1 share is a different launch)
+        n = int(rows) if rows else DEFAULT_ROWS[cfg.replace("_i8", "")]
+        out[key] = {"kernel": name, "launches": len(vals), "fetch_size_kb_avg": round(kb, 1),
+                    "hbm_bytes_per_launch": int(kb * 1024 * 2), "rows": n, "build": tag}
     json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
