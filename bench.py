@@ -152,6 +152,28 @@ def int8_roofline(rows_local, dim, batch, k, t_ms, queries_per_pass=256):
             "bytes_per_launch": int(bytes_), "ops_per_launch": int(ops)}
 
 
+def q8_gemv_roofline(rows_local, dim, k, t_ms):
+    """One query on the int8 copy (r05): the scan launch streams
+    the int8 rows (D bytes per row) and the query; HBM-bound. The rescore of
+    the bracketed survivors (a few hundred rows) is its own, much shorter
+    launch and is not priced here."""
+    bytes_ = rows_local * dim + dim * 4 + k * 12
+    t = t_ms / 1e3
+    gbs = bytes_ / t / 1e9
+    return {"bound": "hbm", "kernel": "int8 single-query scan (v_dot4_i32_i8)",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(t_ms, 4),
+            "bytes_per_launch": int(bytes_)}
+
+
+def q8_gemv_used(prefilter_bytes, dim, k):
+    """Whether a one-query search takes the int8 copy (the engine's rule in
+    vs_engine.cpp q8_gemv_path: a copy exists, dim 768 / 1024, k <= 128,
+    VS_Q8_GEMV not 0)."""
+    return (prefilter_bytes > 0 and dim in (768, 1024) and 1 <= k <= 128
+            and os.environ.get("VS_Q8_GEMV", "1") != "0")
+
+
 def pmc_traffic(workload, rows):
     """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/),
     or None. An entry describes ONE launch over a given number of rows (its
@@ -176,13 +198,18 @@ def queries_per_pass(dim, dtype):
     return 256 if (dtype == "bf16" and dim <= 768) or (dtype == "f32" and dim <= 384) else 128
 
 
-def scan_roofline(config, rows_local, dim, dtype, batch, k, scan_ms, int8):
+def scan_roofline(config, rows_local, dim, dtype, batch, k, scan_ms, int8, q8_b1=False):
     """The bench line's `roofline` for the dominant kernel of this rank's
     scan over `rows_local` rows: algorithmic bytes (or flops) of one launch
     over the rank's share / its measured duration, and `traffic` = the PMC
     HBM bytes of a launch over exactly that share (null when none was
     measured at that size)."""
     elem = 2 if dtype == "bf16" else 4
+    if q8_b1:  # one query on the int8 copy
+        roof = q8_gemv_roofline(rows_local, dim, k, scan_ms)
+        roof["traffic"] = pmc_traffic(config + "_i8", rows_local)
+        roof["traffic_rows"] = rows_local if roof["traffic"] is not None else None
+        return roof
     if int8:  # the int8 pass takes 256 queries a launch up to 768-d, 128 above
         roof = int8_roofline(rows_local, dim, batch, k, scan_ms, 256 if dim <= 768 else 128)
     else:
@@ -454,8 +481,9 @@ def main():
     # batched bf16 searches of a collection with an int8 copy run the int8
     # prefilter pass (the engine's default; VS_FLAG_NO_PREFILTER turns it off)
     int8 = batch > 1 and eng.prefilter_bytes(coll) > 0
+    q8_b1 = batch == 1 and q8_gemv_used(eng.prefilter_bytes(coll), dim, k)
     qpp = queries_per_pass(dim, dtype)
-    roof = scan_roofline(args.config, hi - lo, dim, dtype, batch, k, tm["scan_ms"], int8)
+    roof = scan_roofline(args.config, hi - lo, dim, dtype, batch, k, tm["scan_ms"], int8, q8_b1)
     roof["kernel_launches_timed"] = tm["scan_n"]
 
     result = {
@@ -470,12 +498,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         # int8 pass + rescoring of its survivors on the bf16 / f32 pass's chain
-        "dtype": f"i8+{dtype}" if int8 else dtype,
+        "dtype": f"i8+{dtype}" if (int8 or q8_b1) else dtype,
         "data": "synthetic (counter-based unit-norm generator, seeds 0x5EED / 0xC0FFEE)",
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
                    "rows_per_gpu": hi - lo, "collective": collective,
-                   "int8_prefilter": int8, "build_id": pkg.build_id()},
+                   "int8_prefilter": int8, "int8_single_query": q8_b1,
+                   "build_id": pkg.build_id()},
         "roofline": roof,
         "steps_verified": steps_verified,
     }
@@ -488,7 +517,8 @@ def main():
         steps1 = max(100, args.steps)
         el1, tm1, outs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 10, dist_on,
                                     stream_fn, 1000)
-        r1 = kernel_roofline(hi - lo, dim, elem, 1, k, tm1["scan_ms"], "hbm")
+        r1 = scan_roofline(args.config + "b1", hi - lo, dim, dtype, 1, k, tm1["scan_ms"], False,
+                           q8_gemv_used(eng.prefilter_bytes(coll), dim, k))
         result["secondary"] = {"workload": "same corpus, single query (GEMV path)",
                                "value": round(steps1 / el1, 2), "unit": "queries/s",
                                "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1,

@@ -19,6 +19,20 @@ __device__ __forceinline__ float unord_f32(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
 
+// int8 prefilter bounds (vs_q8.hip; r05 also the single-query scan on the
+// int8 copy, vs_kernels.hip): sqrt of a non-negative fp64 sum, rounded up to
+// float with a relative margin for the sum's own fp64 rounding (dim <= 2^11
+// terms: far below 2^-30)
+__device__ __forceinline__ float q8_norm_up(double s) {
+  return __double2float_ru(sqrt(s) * (1.0 + 0x1p-30));
+}
+// sigma per unit of |x|: the fp32 evaluation error of any score of the scans
+// or of a rescore (<= 2 dim u |q| |x| each, u = 2^-24) on both sides of a
+// bound, and the float rounding of sqS * dot, m and the comparisons
+__device__ __forceinline__ float q8_sigma(uint32_t dim, float q_norm_up) {
+  return (float)((4.0 * dim + 64.0) * 0x1p-24 * (double)q_norm_up * (1.0 + 0x1p-20));
+}
+
 // One workgroup of kBoundThreads: bound[q] = the radix-select lower bound on
 // the k-th largest of the m values at tmax + q * m (`passes` 8-bit digits).
 __device__ __forceinline__ void sample_bound_block(const float* __restrict__ tmax, uint32_t m,

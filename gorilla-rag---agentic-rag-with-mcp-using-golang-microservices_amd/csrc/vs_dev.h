@@ -272,6 +272,7 @@ struct DevEngine {
   // small-collection search spread over workgroups: their keys + the
   // completion counter (zeroed at allocation; each launch leaves it zero)
   DevBuf small_part;
+  DevBuf q8g;  // one query on the int8 copy: workgroup lists, wave bounds, candidates
   std::vector<uint64_t> h_keys;
   std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing

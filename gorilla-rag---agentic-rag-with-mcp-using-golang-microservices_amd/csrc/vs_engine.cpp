@@ -766,6 +766,22 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
 int gemv_one();
 uint32_t large_k_from();
 
+// One query on the int8 copy (r05; on unless VS_Q8_GEMV=0, read
+// once): a collection with an int8 copy streams it instead of its rows, and
+// the bracketed survivors are rescored on the GEMV's own arithmetic.
+bool q8_gemv_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_GEMV");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+bool q8_gemv_path(const Collection& c, uint32_t nq, uint32_t k) {
+  return nq == 1 && q8_gemv_enabled() && q8_enabled() && c.q8 && c.q8_cap >= c.rows &&
+         c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull && vsk::gemv_q8_ok(c.dim, k) &&
+         k < large_k_from();
+}
+
 bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered) {
   return nq == 1 && !filtered && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
          vsk::gemv_small_ok(c.dim, (uint32_t)c.rows, k);
@@ -776,7 +792,7 @@ bool small_path(const Collection& c, uint32_t nq, uint32_t k, bool filtered) {
 bool gemv_one_path(const Collection& c, uint32_t nq, uint32_t k) {
   return nq == 1 && c.rows > 0 && c.row_base + c.rows < 0xFFFFFFFFull &&
          !small_path(c, nq, k, false) && k < large_k_from() && gemv_one() == 2 &&
-         vsk::gemv_one_ok(c.dim, k);
+         vsk::gemv_one_ok(c.dim, k) && !q8_gemv_path(c, nq, k);
 }
 
 // Core search on device data. d_q: nq x dim fp32 on this device, ordered on
@@ -849,6 +865,30 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
                       (!use_mfma || (double)nq * (double)(allowed * rbytes + kGatherCallBytes) <=
                                         (double)c.rows * (double)rbytes);
   if (gather) use_mfma = false;
+  // one query on the int8 copy (r05): scan + finishing launch, the GEMV's keys
+  if (!use_mfma && !gather && q8_gemv_path(c, nq, k)) {
+    const int rc0 = ensure_counters();
+    if (rc0 != VS_OK) return rc0;
+    const size_t sb = vsk::gemv_q8_scratch_bytes((uint32_t)c.rows, k);
+    if (eng->q8g.bytes < sb) {
+      VS_HIP(hipStreamSynchronize(eng->stream), "sync");
+      VS_HIP(eng->q8g.ensure(sb), "alloc int8 single-query scratch");
+    }
+    uint32_t* ctr = (uint32_t*)((char*)eng->small_part.p + kPartBytes + 8);
+    for (int part = 1; part <= 2; ++part) {
+      auto& ev = part == 1 ? eng->scan_ev : eng->merge_ev;
+      VS_HIP(ev_begin(eng, ev), "event");
+      VS_HIP(vsk::launch_gemv_q8(part, c.data, bf16, (const int8_t*)c.q8, c.q8_meta, c.q8_glob,
+                                 dim, (uint32_t)c.rows, (uint32_t)c.row_base, d_q, cosine, allow,
+                                 k, eng->q8g.p, eng->q8g.bytes, ctr,
+                                 direct ? direct->keys : d_keys, eng->stream,
+                                 direct ? direct->flag : nullptr, direct ? direct->seq : 0),
+             part == 1 ? "int8 single-query scan" : "int8 single-query rescore");
+      VS_HIP(ev_end(eng, ev), "event");
+    }
+    if (direct) direct->used = true;
+    return VS_OK;
+  }
   // one query on the GEMV list path: query prep, scan and merge in one launch
   // (the last workgroup merges), the answer straight to the host with `direct`
   if (nq == 1 && !use_mfma && !gather && k < large_k_from() && gemv_one() != 0 &&

@@ -152,6 +152,27 @@ hipError_t launch_gemv_one(const void* X, bool bf16, uint32_t dim, uint32_t n_ro
 
 // Upper bound on the lists launch_gemv writes for these sizes.
 uint32_t gemv_max_lists(uint32_t dim, bool bf16, uint32_t n_rows, uint32_t k);
+// Single query on the int8 copy (r05): the int8 rows X8 (the
+// batched prefilter's copy: tile bounds `meta`, scale `glob`) are scanned for
+// every row's bracket L <= s <= U, then the rows whose U reaches a lower bound
+// on the k-th score are rescored on the GEMV's own arithmetic from X: the keys
+// equal launch_gemv_one's bit for bit. Two launches; `q_raw` is the raw query
+// (prepped in the kernels as the one-launch GEMV does). dim 768 / 1024, k <=
+// 128. scratch >= gemv_q8_scratch_bytes; ctr = 2 u32, zero between launches
+// (left zero). dst receives k keys (mapped host memory with `flag`: seq is
+// stored there once they are visible). stats (nullable, tests): [0] += rows
+// rescored, [1] += workgroup lists replaced by all their rows. part: 1 = the
+// scan launch, 2 = the finishing launch, 3 = both (the engine brackets them
+// with separate timing events).
+bool gemv_q8_ok(uint32_t dim, uint32_t k);
+uint32_t gemv_q8_lists(uint32_t n_rows);
+size_t gemv_q8_scratch_bytes(uint32_t n_rows, uint32_t k);
+hipError_t launch_gemv_q8(int part, const void* X, bool bf16, const int8_t* X8, const float* meta,
+                          const float* glob, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                          const float* q_raw, bool cosine, const uint64_t* allow, uint32_t k,
+                          void* scratch, size_t scratch_bytes, uint32_t* ctr, uint64_t* dst,
+                          hipStream_t st, uint64_t* flag = nullptr, uint64_t seq = 0,
+                          uint32_t* stats = nullptr);
 
 // Batched scan on MFMA with fused top-k: bf16 rows on
 // v_mfma_f32_16x16x32_bf16, or fp32 rows (f32) on v_mfma_f32_16x16x4_f32.

@@ -4087,4 +4087,445 @@ hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// single query on the int8 copy (r05; DESIGN.md §5 "Single query on the int8
+// copy")
+// ---------------------------------------------------------------------------
+// A one-query search streams D * e bytes per row through the GEMV; the
+// collection's int8 copy (the batched path's prefilter, vs_q8.hip) holds the
+// same rows in D bytes (1/2 of bf16, 1/4 of fp32). The bracket is the batched
+// int8 path's (select_q8_kernel): with the query's int8 image {sqS, a, c,
+// sigma} and the row's tile {dt, nt}, L = sqS dot - mt <= s <= U = sqS dot +
+// mt, mt = a dt + (c + sigma) nt, where dot = q8 . x8 is an exact int32 and s
+// is the row's fp32 GEMV score (sigma covers any fp32 summation order).
+//  1. gemv_q8_scan_kernel: every row's dot on v_dot4_i32_i8 (16 B of a row
+//     per lane, 4 rows per wave step, waves interleaved over the rows as the
+//     GEMV's), its U and L; per wave the KP = 64 KPL largest U keys (a
+//     register list, merged per workgroup by rank: gemv_emit) and the largest
+//     L key's score image.
+//  2. gemv_q8_finish_kernel: P = the floor of the 24-bit bucket holding the
+//     k-th largest of the waves' L images (k distinct rows reach it, so it is
+//     at most the k-th GEMV score); each workgroup list's entries whose U
+//     reaches P are rescored on the GEMV's own per-row arithmetic
+//     (gemv_row_score: the same loads, chunk_dot, order and wave_sum, hence
+//     the same bits); a list that dropped a key whose U reaches P is replaced
+//     by every row of its scan workgroup. Each finishing workgroup appends its
+//     waves' top k, and the last one (agent-scope hand-off, as
+//     gemv_one_finish) merges them.
+// Every row of the GEMV's top k has U >= s >= k-th score >= P, so it is
+// rescored and its key is the GEMV's: the answer equals the GEMV's bit for bit.
+constexpr int kQ8gLists = 4;  // scan-workgroup lists per finishing workgroup
+
+template <int D>
+struct Q8GemvShape {
+  static constexpr int CPR = D / 16;          // 16-B chunks per int8 row
+  static constexpr int RB = 4;                // rows per wave step: one tile (4 | 32)
+  static constexpr int J = RB * CPR / 64;     // chunks per lane per step
+  static_assert((RB * CPR) % 64 == 0, "whole chunks per lane");
+};
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+// exact int32 wave sum (any order), as wave_sum_dpp: rows of 16 lanes by DPP,
+// then four readlanes
+__device__ __forceinline__ int wave_isum(int v) {
+  v += dpp_i<0xB1>(v);
+  v += dpp_i<0x4E>(v);
+  v += dpp_i<0x141>(v);
+  v += dpp_i<0x140>(v);
+  return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+         (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
+
+// 16 int8 products of a chunk on v_dot4_i32_i8 (exact)
+__device__ __forceinline__ int chunk_dot8(const uint4& x, const int4& q) {
+  int d = __builtin_amdgcn_sdot4((int)x.x, q.x, 0, false);
+  d = __builtin_amdgcn_sdot4((int)x.y, q.y, d, false);
+  d = __builtin_amdgcn_sdot4((int)x.z, q.z, d, false);
+  return __builtin_amdgcn_sdot4((int)x.w, q.w, d, false);
+}
+
+// Wave 0: the prepped query qs (LDS, fp32) -> its int8 image q8s and {sqS, a,
+// c, sigma} in par (the formulas of vs_q8.hip q8_query_block; S = the
+// collection's scale). Each lane reads only the qs entries it wrote.
+template <int D>
+__device__ __forceinline__ void q8_query_wave(const float* qs, int8_t* q8s, float* par, float S,
+                                              int lane) {
+  constexpr int PJ = D / 64;
+  float v[PJ];
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    v[j] = qs[lane + 64 * j];
+    amax = fmaxf(amax, fabsf(v[j]));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) amax = fmaxf(amax, __shfl_xor(amax, m, 64));
+  const float sq = amax > 0.f ? amax / 127.f : 0.f;
+  double aa = 0.0, cc = 0.0, nn = 0.0;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const float y = sq > 0.f ? fminf(fmaxf(rintf(v[j] / sq), -127.f), 127.f) : 0.f;
+    const double sy = (double)sq * (double)y, e = (double)v[j] - sy;
+    aa = aa + sy * sy;
+    cc = cc + e * e;
+    nn = nn + (double)v[j] * (double)v[j];
+    q8s[lane + 64 * j] = (int8_t)(int)y;
+  }
+  aa = wave_sum_f64(aa);
+  cc = wave_sum_f64(cc);
+  nn = wave_sum_f64(nn);
+  if (lane == 0) {
+    par[0] = sq * S;
+    par[1] = q8_norm_up(aa);
+    par[2] = q8_norm_up(cc);
+    par[3] = q8_sigma(D, q8_norm_up(nn));
+  }
+}
+
+template <int D, int KPL>
+__global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
+    const int8_t* __restrict__ X8, uint32_t n_rows, uint32_t row_base,
+    const float* __restrict__ q_raw, int prep, const float* __restrict__ meta,
+    const float* __restrict__ glob, const uint64_t* __restrict__ allow,
+    uint64_t* __restrict__ ulist, uint32_t* __restrict__ lbest) {
+  using S = Q8GemvShape<D>;
+  constexpr int KP = 64 * KPL;
+  __shared__ float qs[D];
+  __shared__ __attribute__((aligned(16))) int8_t q8s[D];
+  __shared__ float par[4];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t gw = blockIdx.x * kGemvWaves + w, nw = gridDim.x * kGemvWaves;
+  const uint32_t stride = nw * S::RB;
+  int rowsel[S::J], coff[S::J];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) {
+    const int c = lane + 64 * j;
+    rowsel[j] = c / S::CPR;
+    coff[j] = c % S::CPR;
+  }
+  uint4 buf[2][S::J];
+  auto load = [&](uint4* dst, uint32_t r0) {
+#pragma unroll
+    for (int j = 0; j < S::J; ++j) {
+      uint32_t row = r0 + rowsel[j];
+      row = row < n_rows ? row : n_rows - 1;
+      const u32x4_t v = __builtin_nontemporal_load(
+          (const u32x4_t*)(X8 + (size_t)row * D + (size_t)coff[j] * 16));
+      dst[j] = uint4{v[0], v[1], v[2], v[3]};
+    }
+  };
+  const uint32_t lo = gw * S::RB;
+  if (lo < n_rows) load(buf[0], lo);  // the first rows' loads go out before the query is ready
+  if (w == 0) {
+    prep_query_wave<D>(q_raw, prep, qs, lane);  // the GEMV's query, bit for bit
+    q8_query_wave<D>(qs, q8s, par, glob[3], lane);
+  }
+  __syncthreads();
+  int4 qv[S::J];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) qv[j] = *(const int4*)(q8s + coff[j] * 16);
+  const float sqS = par[0], pa = par[1], pc = par[2] + par[3];
+  WaveList<KPL> Lst;
+  Lst.init();
+  uint64_t theta = 0, lmax = 0;
+  for (uint32_t r = lo; r < n_rows; r += stride) {
+    const uint32_t rn = r + stride;
+    load(buf[1], rn < n_rows ? rn : r);
+    int p[S::RB];
+#pragma unroll
+    for (int b = 0; b < S::RB; ++b) p[b] = 0;
+#pragma unroll
+    for (int j = 0; j < S::J; ++j) {
+      const int d = chunk_dot8(buf[0][j], qv[j]);
+#pragma unroll
+      for (int b = 0; b < S::RB; ++b) p[b] += rowsel[j] == b ? d : 0;
+    }
+    // the step's rows share one tile (r % 4 == 0): its {dt, nt}
+    const float2 tm = ((const float2*)meta)[r >> 5];
+    const float mt = pa * tm.x + pc * tm.y;
+#pragma unroll
+    for (int b = 0; b < S::RB; ++b) {
+      const int dot = wave_isum(p[b]);
+      const uint32_t row = r + b;
+      if (row < n_rows && row_allowed(allow, row)) {
+        const float xs = (float)dot * sqS;  // |dot| < 2^24: exact in fp32
+        const uint64_t ku = make_key(xs + mt, row_base + row);
+        if (ku > theta) {
+          Lst.insert(ku, KP, lane);
+          theta = Lst.kth(KP);
+        }
+        const uint64_t kl = make_key(xs - mt, row_base + row);
+        lmax = kl > lmax ? kl : lmax;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S::J; ++j) buf[0][j] = buf[1][j];
+  }
+  gemv_emit<KPL>(Lst, theta, KP, lane, w, ulist);
+  if (lane == 0) lbest[gw] = (uint32_t)(lmax >> 32);
+}
+
+// The score of local row `row` exactly as the GEMV scan computes it (its
+// step's lane layout: the row is row % RB of a step starting at a multiple of
+// RB; the lane's chunks of that row in j order, wave_sum): the same bits.
+// Lanes without a chunk of the row add nothing (p stays +0, as the scan's
+// zero addends leave it). qs: the prepped query (LDS).
+template <int D, bool BF16>
+__device__ __forceinline__ float gemv_row_score(const void* __restrict__ Xv, uint32_t row,
+                                                const float* qs, int lane) {
+  using S = GemvShape<D, BF16>;
+  const uint32_t b = S::RB == 1 ? 0u : row % (uint32_t)S::RB, r0 = row - b;
+  const char* X = (const char*)Xv;
+  uint4 c[S::J];
+  bool mine[S::J];
+  int co[S::J];
+#pragma unroll
+  for (int j = 0; j < S::J; ++j) {
+    const int cc = lane + 64 * j;
+    const uint32_t rs = S::RB == 1 ? 0u : (uint32_t)(cc / S::CPR);
+    co[j] = cc % S::CPR;
+    mine[j] = rs == b;
+    c[j] = mine[j] ? *(const uint4*)(X + (size_t)(r0 + rs) * S::RBYTES + (size_t)co[j] * 16)
+                   : uint4{0u, 0u, 0u, 0u};
+  }
+  float p = 0.f;
+#pragma unroll
+  for (int j = 0; j < S::J; ++j)
+    if (mine[j]) {
+      float qv[S::EPC];
+#pragma unroll
+      for (int e = 0; e < S::EPC; ++e) qv[e] = qs[co[j] * S::EPC + e];
+      p += chunk_dot<BF16>(c[j], qv);
+    }
+  return wave_sum(p);
+}
+
+template <int D, bool BF16, int KPL>
+__global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
+    const void* __restrict__ X, uint32_t n_rows, uint32_t row_base,
+    const float* __restrict__ q_raw, int prep, const uint64_t* __restrict__ allow, uint32_t k,
+    const uint64_t* __restrict__ ulist, const uint32_t* __restrict__ lbest, uint32_t nscan,
+    uint64_t* __restrict__ cand, uint32_t* __restrict__ ctr, uint64_t* __restrict__ dst,
+    uint64_t* flag, uint64_t seq, uint32_t* __restrict__ stats) {
+  using SQ = Q8GemvShape<D>;
+  constexpr int KP = 64 * KPL;
+  __shared__ float qs[D];
+  __shared__ uint32_t hist[256], hws[4], hpick, habove, nz_sh;
+  __shared__ uint64_t surv[kQ8gLists * KP];
+  __shared__ uint32_t ns_sh, fb_sh;
+  const int lane = threadIdx.x & 63;
+  const uint32_t tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  if (w == 0) prep_query_wave<D>(q_raw, prep, qs, lane);
+  if (tid == 0) ns_sh = 0, fb_sh = 0, nz_sh = 0;
+  __syncthreads();
+  // 1. P: radix floor of the k-th largest wave L image (0 = a wave without rows)
+  const uint32_t m = nscan * kGemvWaves;
+  uint32_t prefix = 0, kk = k;
+  {
+    uint32_t nz = 0;
+    for (uint32_t i = tid; i < m; i += kGemvThreads) nz += lbest[i] != 0u;
+    if (nz) atomicAdd(&nz_sh, nz);  // complete at the first pass's barrier
+  }
+#pragma unroll 1
+  for (int pass = 0; pass < 3; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    if (nz_sh < k) break;  // uniform: fewer than k rows scanned -> P = 0
+    for (uint32_t i = tid; i < m; i += kGemvThreads) {
+      const uint32_t u = lbest[i];
+      if (u && (u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    uint32_t c = 0, x = 0;
+    if (tid < 256) {
+      c = hist[255 - tid];  // thread t: digit 255 - t (descending)
+      x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) hws[w] = x;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      for (int j = 0; j < w; ++j) x += hws[j];
+      if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
+    }
+    __syncthreads();
+    prefix |= (255u - hpick) << shift;
+    kk -= habove;
+    __syncthreads();
+  }
+  const uint32_t P = nz_sh < k ? 0u : prefix;
+  // 2. the lists' entries whose U reaches P; a list whose dropped keys may
+  // reach P (its last entry does) is replaced by all of its workgroup's rows
+  const uint32_t l0 = blockIdx.x * kQ8gLists;
+  for (uint32_t i = tid; i < (uint32_t)(kQ8gLists * KP); i += kGemvThreads) {
+    const uint32_t l = l0 + i / KP, j = i % KP;
+    if (l >= nscan) continue;
+    const uint64_t e = ulist[(size_t)l * KP + j];
+    if (j == KP - 1 && e != 0 && (uint32_t)(e >> 32) >= P) atomicOr(&fb_sh, 1u << (l - l0));
+    if (e != 0 && (uint32_t)(e >> 32) >= P) surv[atomicAdd(&ns_sh, 1u)] = e;
+  }
+  __syncthreads();
+  // 3. rescore: wave w takes survivors w, w + 8, ... (those of fallback lists
+  // are rescored below with every row of their workgroup)
+  const uint32_t fb = fb_sh, ns = ns_sh;
+  WaveList<KPL> R;
+  R.init();
+  uint64_t theta = 0;
+  auto offer = [&](uint32_t row) {  // local row
+    const float s = gemv_row_score<D, BF16>(X, row, qs, lane);
+    const uint64_t key = make_key(s, row_base + row);
+    if (key > theta) {
+      R.insert(key, k, lane);
+      theta = R.kth(k);
+    }
+  };
+  uint32_t rescored = 0;
+  for (uint32_t i = (uint32_t)w; i < ns; i += kGemvWaves) {
+    const uint64_t e = surv[i];
+    const uint32_t row = vs::key_row(e) - row_base;
+    // the scan workgroup this row belongs to (interleaved 4-row steps)
+    const uint32_t l = ((row / SQ::RB) % (nscan * kGemvWaves)) / kGemvWaves;
+    if ((fb >> (l - l0)) & 1u) continue;
+    offer(row);
+    ++rescored;
+  }
+  if (fb) {
+    // every row of each fallback list's workgroup: wave w takes its scan wave w
+    const uint32_t stride = nscan * kGemvWaves * SQ::RB;
+    for (int li = 0; li < kQ8gLists; ++li) {
+      if (!((fb >> li) & 1u)) continue;
+      const uint32_t gw = (l0 + li) * kGemvWaves + w;
+      for (uint32_t r = gw * SQ::RB; r < n_rows; r += stride)
+        for (uint32_t b = 0; b < (uint32_t)SQ::RB; ++b) {
+          const uint32_t row = r + b;
+          if (row < n_rows && row_allowed(allow, row)) {
+            offer(row);
+            ++rescored;
+          }
+        }
+    }
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], rescored);
+    if (w == 0) atomicAdd(&stats[1], (uint32_t)__popc(fb));
+  }
+  // 4. this wave's top k -> the candidate array
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) cnt += (uint32_t)__popcll(__ballot(R.e[i] != 0));
+  cnt = cnt < k ? cnt : k;
+  if (cnt) {
+    uint32_t base = 0;
+    if (lane == 0) base = __hip_atomic_fetch_add(&ctr[1], cnt, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    base = (uint32_t)__shfl((int)base, 0, 64);
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const uint32_t idx = (uint32_t)(i * 64 + lane);
+      if (idx < cnt) cand[base + idx] = R.e[i];
+    }
+  }
+  // 5. hand-off: the last workgroup merges every appended key
+  __shared__ uint64_t mbuf[kMergeCap];
+  __shared__ uint64_t red[kMergeThreads / 64];
+  __shared__ uint32_t mcnt;
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t prev =
+        __hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      mcnt = __hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const uint32_t N = mcnt;
+  __syncthreads();
+  if (N == 0) {
+    for (uint32_t j = tid; j < k; j += kGemvThreads) dst[j] = 0;
+  } else {
+    merge_query(cand, N, 1, 0, 1, k, 0, dst, mbuf, red, mcnt, false);
+  }
+  if (tid == 0) {
+    __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (flag) publish_host(flag, seq);
+}
+
+bool gemv_q8_ok(uint32_t dim, uint32_t k) { return (dim == 768 || dim == 1024) && k >= 1 && k <= 128; }
+
+uint32_t gemv_q8_lists(uint32_t n_rows) { return gemv_grid(n_rows, 4).nwg; }
+
+size_t gemv_q8_scratch_bytes(uint32_t n_rows, uint32_t k) {
+  const uint64_t nscan = gemv_q8_lists(n_rows);
+  const uint64_t kp = k <= 64 ? 64 : 128;
+  const uint64_t nfin = (nscan + kQ8gLists - 1) / kQ8gLists;
+  return (size_t)(nscan * kp * 8 + (nscan * kGemvWaves * 4 + 7) / 8 * 8 + nfin * kGemvWaves * k * 8);
+}
+
+template <int D, bool BF16, int KPL>
+static void gemv_q8_launch(int part, const void* X, const int8_t* X8, const float* meta,
+                           const float* glob, uint32_t n_rows, uint32_t row_base,
+                           const float* q_raw, int prep, const uint64_t* allow, uint32_t k,
+                           uint32_t nscan, uint64_t* ulist, uint32_t* lbest, uint64_t* cand,
+                           uint32_t* ctr, uint64_t* dst, uint64_t* flag, uint64_t seq,
+                           uint32_t* stats, hipStream_t st) {
+  if (part & 1)
+    hipLaunchKernelGGL((gemv_q8_scan_kernel<D, KPL>), dim3(nscan), dim3(kGemvThreads), 0, st, X8,
+                       n_rows, row_base, q_raw, prep, meta, glob, allow, ulist, lbest);
+  if (part & 2)
+    hipLaunchKernelGGL((gemv_q8_finish_kernel<D, BF16, KPL>),
+                     dim3((nscan + kQ8gLists - 1) / kQ8gLists), dim3(kGemvThreads), 0, st, X,
+                     n_rows, row_base, q_raw, prep, allow, k, ulist, lbest, nscan, cand, ctr, dst,
+                     flag, seq, stats);
+}
+
+hipError_t launch_gemv_q8(int part, const void* X, bool bf16, const int8_t* X8, const float* meta,
+                          const float* glob, uint32_t dim, uint32_t n_rows, uint32_t row_base,
+                          const float* q_raw, bool cosine, const uint64_t* allow, uint32_t k,
+                          void* scratch, size_t scratch_bytes, uint32_t* ctr, uint64_t* dst,
+                          hipStream_t st, uint64_t* flag, uint64_t seq, uint32_t* stats) {
+  if (!gemv_q8_ok(dim, k) || n_rows == 0 || !X || !X8 || !meta || !glob || !q_raw || !ctr ||
+      !dst || scratch_bytes < gemv_q8_scratch_bytes(n_rows, k))
+    return hipErrorInvalidValue;
+  const uint32_t nscan = gemv_q8_lists(n_rows);
+  const uint32_t kp = k <= 64 ? 64 : 128;
+  uint64_t* ulist = (uint64_t*)scratch;
+  uint32_t* lbest = (uint32_t*)(ulist + (size_t)nscan * kp);
+  uint64_t* cand =
+      (uint64_t*)((char*)lbest + ((size_t)nscan * kGemvWaves * 4 + 7) / 8 * 8);
+  const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
+#define VS_Q8G(DD, BB, KK)                                                                    \
+  gemv_q8_launch<DD, BB, KK>(part, X, X8, meta, glob, n_rows, row_base, q_raw, prep, allow, k,  \
+                             nscan, ulist, lbest, cand, ctr, dst, flag, seq, stats, st)
+  if (dim == 768) {
+    if (bf16) { if (kp == 64) VS_Q8G(768, true, 1); else VS_Q8G(768, true, 2); }
+    else { if (kp == 64) VS_Q8G(768, false, 1); else VS_Q8G(768, false, 2); }
+  } else {
+    if (bf16) { if (kp == 64) VS_Q8G(1024, true, 1); else VS_Q8G(1024, true, 2); }
+    else { if (kp == 64) VS_Q8G(1024, false, 1); else VS_Q8G(1024, false, 2); }
+  }
+#undef VS_Q8G
+  return hipGetLastError();
+}
+
 }  // namespace vsk

@@ -31,11 +31,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
   return v;
 }
-// sqrt of a non-negative fp64 sum, rounded up to float with a relative margin
-// for the sum's own fp64 rounding (dim <= 2^11 terms: far below 2^-30)
-__device__ __forceinline__ float norm_up(double s) {
-  return __double2float_ru(sqrt(s) * (1.0 + 0x1p-30));
-}
+__device__ __forceinline__ float norm_up(double s) { return q8_norm_up(s); }  // vs_bound_dev.h
 __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
   // non-negative floats order as their bit patterns
   atomicMax((unsigned int*)p, __float_as_uint(v));
@@ -187,8 +183,7 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
     // sigma covers, per unit of |x|: the fp32 evaluation error of an MFMA or
     // rescore score (<= 2 dim u |q| |x| each, u = 2^-24) on both sides of a
     // bound, and the float rounding of sqS * dot, m and the comparisons
-    const float nq_up = norm_up(nn);
-    const float sigma = (float)((4.0 * dim + 64.0) * 0x1p-24 * (double)nq_up * (1.0 + 0x1p-20));
+    const float sigma = q8_sigma(dim, norm_up(nn));
     float* p = q8par + 4 * (size_t)i;
     p[0] = sq * glob[3];
     p[1] = norm_up(aa);
