@@ -628,7 +628,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   // (at the unscaled sample size: a tighter bound shrinks the bf16-like part
   // of the admissions, not the window's)
   const uint32_t cap8 = q8 ? vsk::mfma_cand_cap(n_rows, k, st0, 8.0) : 0;
-  const uint32_t capx = std::max(cap, cap8);
+  const uint32_t capx = q8 ? cap8 : cap;  // (r05: no bf16 pass behind the int8 one)
   const size_t lbytes = fast ? 0 : (size_t)maxl * PS * k * 8;
   const size_t sbytes = (size_t)PS * 4;  // per-query sample bounds
   // main pass slabs: 32 B of scores + a 4-B tile row per slot
@@ -698,8 +698,9 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                  "sample bound");
         }
       }
-      // 2. int8 pass -> bounded candidates -> rescored top k; the bf16 / f32
-      // pass and select behind it run only if the int8 pass overflowed (*gate)
+      // 2. int8 pass -> bounded candidates -> rescored top k (r05: the select
+      // recomputes a quarter the pass overflowed and streams a survivor spill
+      // itself; no gated bf16 launches behind it)
       VS_HIP(ev_begin(eng, eng->scan_ev), "event");
       VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                       c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
@@ -708,19 +709,9 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       VS_HIP(ev_end(eng, eng->scan_ev), "event");
       VS_HIP(ev_begin(eng, eng->merge_ev), "event");
       VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
-                                   qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, gate,
-                                   eng->stream),
+                                   qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
+                                   q8q, allow, n_rows, eng->stream),
              "int8 select");
-      for (uint32_t s0 = 0; s0 < nv; s0 += P) {
-        const uint32_t ns = std::min(P, nv - s0);
-        VS_HIP(vsk::launch_mfma_cand(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k,
-                                     bound + s0, slabs, slab_tile, cap, cnt, maxl, &L, eng->stream,
-                                     allow, qmax_sel, gate),
-               "mfma scan (int8 fallback)");
-        VS_HIP(vsk::launch_select_slabs(slabs, slab_tile, cnt, L, cap, ns, k, out + (size_t)s0 * k,
-                                        eng->stream, row_base, allow, qmax_sel, gate),
-               "select (int8 fallback)");
-      }
       VS_HIP(ev_end(eng, eng->merge_ev), "event");
     }
     return VS_OK;

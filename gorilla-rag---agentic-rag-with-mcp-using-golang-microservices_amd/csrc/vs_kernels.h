@@ -245,9 +245,11 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // whose upper bound on its fp32 score reaches the sample bound;
 // launch_select_q8 bounds, rescores the survivors from the bf16 rows and
 // writes the top k; `allow` (nullable) is the pre-mask, as the bf16 pass's.
-// Any overflow (a full quarter, too many survivors) sets
-// *gate, and the bf16 pass + select enqueued behind with run_if = gate
-// answer the batch instead. Exact: the answer is the bf16 pass's.
+// A full quarter keeps counting (its count then passes its capacity) and its
+// largest dot stays exact; the select recomputes such a quarter's rows from
+// the int8 copy X8 with the queries' images Q8 and streams more survivors
+// than its buffer through a running top k (r05; r04 handed the batch to a
+// gated bf16 pass instead). Exact: the answer is the bf16 pass's.
 // dims with an int8 pass: bf16 rows 768 / 1024, fp32 rows 768 (r04)
 bool q8_supported(uint32_t dim, bool f32);
 hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, uint32_t row_base,
@@ -267,8 +269,10 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             uint32_t k, uint64_t* out,
                             uint32_t row_base, const void* X, const void* qb, bool f32, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
-                            const float* bound, uint32_t* gate, hipStream_t st,
-                            uint32_t* stats = nullptr);  // (tools) += slabs read, survivors
+                            const float* bound, const void* X8, const void* Q8,
+                            const uint64_t* allow, uint32_t n_rows, hipStream_t st,
+                            uint32_t* stats = nullptr,  // (tools) += slabs read, survivors, slow paths
+                            uint64_t* clk = nullptr);   // (tools) [nq][8] stage wall clocks
 // Store side (vs_q8.hip; X: bf16 rows, or fp32 rows when f32): glob[0] = max
 // |x| over n values (atomic max; zero it first); glob[3] = S = glob[0] / 127
 // (1 when 0).

@@ -2365,17 +2365,18 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
           const uint32_t sub = a.cand_cap >> 2;
           const uint32_t cg = cnt_r[g];
-          if (cg >= sub) {
-            if (a.gate) a.gate[0] = 1u;  // a full quarter: the bf16 pass answers
-          } else {
+          // r05: a full quarter keeps counting (a count past its capacity
+          // marks it lossy: select_q8 recomputes its rows from the int8
+          // copy) and its largest dot stays exact; no hand-back
+          if (cg < sub) {
             const size_t slot = (size_t)slot0[g] + cg;
             f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
             sp[0] = acc[0][g];
             sp[1] = acc[1][g];
             a.cand_tile[slot] = a.row_base + trow0;
-            cnt_r[g] = cg + 1;
-            qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
           }
+          cnt_r[g] = cg + 1;
+          qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
         }
       }
       return;
@@ -2531,10 +2532,13 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if constexpr (MODE == 0) {
-      a.cand_cnt[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
-          kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
+      // the int8 pass writes its counts and maxima query-major ([query][wg][4],
+      // r05: select_q8 reads a query's 4 nwg quarters in one coalesced load)
+      const size_t ci = I8 ? ((size_t)ql[g] * gridDim.x + blockIdx.x) * 4 + kq
+                           : ((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq;
+      a.cand_cnt[ci] = kRegCnt ? cnt_r[g] : cntl[g * THREADS + threadIdx.x];
       if (a.cand_max)
-        a.cand_max[((size_t)blockIdx.x * kMfmaQueries + ql[g]) * 4 + kq] =
+        a.cand_max[ci] =
             kRegCnt ? (I8 ? (uint32_t)qmx_r[g] : cntl[g * THREADS + threadIdx.x])
                     : cntl[(G + g) * THREADS + threadIdx.x];
     } else if constexpr (MODE == 3) {
@@ -3195,6 +3199,63 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // SV (timing ablation, VS_Q8_SEL_SV): return after stage SV. F32: fp32 rows
 // and queries, survivors rescored on the f32 pass's v_mfma_f32_16x16x4_f32
 // chain (four MFMAs per 16-B fragment, as that pass), so again its bits.
+// The int8 copy's rows, the queries' int8 images and what the select's slow
+// path needs to recompute a lossy quarter (r05): its workgroup's rows
+// [wg * rows_per_wg, ...) of the static split (mfma_grid), the pre-mask.
+struct Q8Rows {
+  const int8_t* x8;
+  const int8_t* q8;        // [query][dim] int8 images (vs_q8.hip)
+  const uint64_t* allow;   // nullable: bit r admits local row r
+  uint32_t n_rows, rows_per_wg, row_base;
+};
+
+// A zero query: every score is exactly 0 (products of 0, -0 ranked as +0), so
+// the top k are the k lowest allowed rows. Wave-level; k <= kMfmaMaxK.
+__device__ __forceinline__ void q8_zero_query(const Q8Rows& r8, uint32_t k, uint32_t lane,
+                                              uint64_t* __restrict__ out) {
+  uint32_t found = 0;
+  for (uint32_t w0 = 0; found < k && (uint64_t)w0 * 64 < r8.n_rows; w0 += 64) {
+    const uint32_t wi = w0 + lane;  // this lane's 64-row word
+    uint64_t bits = 0;
+    if ((uint64_t)wi * 64 < r8.n_rows) {
+      bits = r8.allow ? r8.allow[wi] : ~0ull;
+      const uint32_t left = r8.n_rows - wi * 64;
+      if (left < 64) bits &= (1ull << left) - 1ull;
+    }
+    const uint32_t pc = (uint32_t)__popcll(bits);
+    uint32_t incl = pc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    uint32_t pos = found + incl - pc;
+    while (bits && pos < k) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+      out[pos++] = make_key(0.0f, r8.row_base + wi * 64 + b);
+      bits &= bits - 1;
+    }
+    found += (uint32_t)__shfl((int)incl, 63, 64);
+  }
+  for (uint32_t j = found + lane; j < k; j += 64) out[j] = 0;
+}
+
+// The exact int32 dot of an int8 row with an int8 query image in LDS (D bytes).
+template <int D>
+__device__ __forceinline__ int q8_row_dot(const int8_t* __restrict__ xr, const int8_t* qs) {
+  int d = 0;
+#pragma unroll 4
+  for (int c = 0; c < D / 16; ++c) {
+    const uint4 x = *(const uint4*)(xr + 16 * c);
+    const int4 y = *(const int4*)(qs + 16 * c);
+    d = __builtin_amdgcn_sdot4((int)x.x, y.x, d, false);
+    d = __builtin_amdgcn_sdot4((int)x.y, y.y, d, false);
+    d = __builtin_amdgcn_sdot4((int)x.z, y.z, d, false);
+    d = __builtin_amdgcn_sdot4((int)x.w, y.w, d, false);
+  }
+  return d;
+}
+
 template <int D, int SV = 0, bool F32 = false>
 __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
@@ -3202,7 +3263,8 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
     const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
-    const float* __restrict__ bound, uint32_t* __restrict__ gate, uint32_t* __restrict__ stats) {
+    const float* __restrict__ bound, const Q8Rows r8, uint32_t* __restrict__ stats,
+    uint64_t* __restrict__ clk) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -3210,72 +3272,113 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t wtot[kSelThreads / 64];
   __shared__ uint32_t wscr[kSelThreads / 64][16];  // a wave's group of 16 rows
   __shared__ uint32_t fill, spill, rfill;
-  __shared__ uint64_t thr_sh;
   __shared__ uint32_t hist[256], hws[4], hpick, habove;  // kth_floor's radix state
+  // (tools/share_pipe.hip) per-workgroup wall clock at the stage boundaries:
+  // start, bound, survivors, rescore, end
+  auto tick = [&](int i) {
+    if (clk && threadIdx.x == 0) clk[(size_t)blockIdx.x * 8 + i] = wall_clock64();
+  };
+  tick(0);
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (*gate) return;  // already handed to the bf16 pass (which rewrites every answer)
   const uint32_t sub = cap >> 2, nl = 4 * nwg;
   const f32x4_t par = q8par[q];  // sqS, a, c, sigma
   const float sqS = par[0], pa = par[1], pc = par[2], sig = par[3];
   const float dmax = q8glob[1], nmax = q8glob[2];
   const float mg = pa * dmax + (pc + sig) * nmax;  // m + sigma n of any row
   const float b = bound[q];
-  // lists 2 tid, 2 tid + 1: counts and largest appended dots
+  // quarter lists 2 tid, 2 tid + 1 (l = 4 wg + kq): counts and largest
+  // appended dots, query-major ([query][wg][4], r05: one coalesced load each)
   const uint32_t l0 = 2 * tid;
   uint32_t c0 = 0, c1 = 0;
   int x0 = INT_MIN, x1 = INT_MIN;
-  {
-    const uint32_t a0 = l0 < nl ? l0 : 0u, a1 = l0 + 1 < nl ? l0 + 1 : 0u;
-    const size_t i0 = ((size_t)(a0 >> 2) * kMfmaQueries + q) * 4 + (a0 & 3);
-    const size_t i1 = ((size_t)(a1 >> 2) * kMfmaQueries + q) * 4 + (a1 & 3);
-    const uint32_t r0 = cnt[i0], r1 = cnt[i1];
-    const int m0 = cmax[i0], m1 = cmax[i1];
-    c0 = l0 < nl ? (r0 < sub ? r0 : sub) : 0u;
-    c1 = l0 + 1 < nl ? (r1 < sub ? r1 : sub) : 0u;
-    x0 = c0 ? m0 : INT_MIN;
-    x1 = c1 ? m1 : INT_MIN;
+  bool lossy0 = false, lossy1 = false;  // the pass dropped slabs of the quarter
+  if (l0 < nl) {  // nl is even: l0 + 1 < nl too
+    const uint2 cc = *(const uint2*)(cnt + (size_t)q * nl + l0);
+    const int2 mm = *(const int2*)(cmax + (size_t)q * nl + l0);
+    c0 = cc.x < sub ? cc.x : sub;
+    c1 = cc.y < sub ? cc.y : sub;
+    lossy0 = cc.x > sub;
+    lossy1 = cc.y > sub;
+    x0 = c0 ? mm.x : INT_MIN;
+    x1 = c1 ? mm.y : INT_MIN;
   }
   if (tid == 0) fill = 0, spill = 0, rfill = 0;
+  // a zero query (a = |sq q8| = 0 and c = |q - sq q8| = 0): every score is
+  // exactly 0, so the answer is the k lowest allowed rows (the tie rule)
+  if (pa == 0.0f && pc == 0.0f) {
+    if (w == 0) q8_zero_query(r8, k, lane, out + (size_t)q * k);
+    tick(4);
+    return;
+  }
+  // The floor P of the 24-bit bucket holding the kk-th largest high word (an
+  // order-preserving score image) of v[0, n), n >= kk: at least kk entries
+  // have a high word >= P. Three 8-bit radix passes as the sample bound
+  // (vs_bound_dev.h), over LDS. (r05: every k; the register sorts and wave
+  // merges it replaced cost ~4 us per use in the select's latency chain.)
+  auto kth_floor = [&](const uint64_t* v, uint32_t n, uint32_t kk) -> uint32_t {
+    uint32_t prefix = 0;
+#pragma unroll 1
+    for (int pass = 0; pass < 3; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < n; i += kSelThreads) {
+        const uint32_t u = (uint32_t)(v[i] >> 32);
+        if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      uint32_t c = 0, x = 0;
+      if (tid < 256) {
+        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
+        x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) hws[w] = x;
+      }
+      __syncthreads();
+      if (tid < 256) {
+        for (uint32_t j = 0; j < w; ++j) x += hws[j];
+        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
+      }
+      __syncthreads();
+      prefix |= (255u - hpick) << shift;
+      kk -= habove;
+      __syncthreads();  // hist / hws / hpick are rewritten by the next pass
+    }
+    return prefix;
+  };
   // Each quarter's largest dot gives its lower bound sqS dot - mg; the
   // quarters hold disjoint rows, so k rows reach the k-th largest of those,
-  // which bounds the k-th score from below. (The k-th of per-workgroup
-  // maxima, the first form, sat far under the k-th score once k neared the
-  // 256 workgroups: at k = 50, 4578 survivors per query against 2821.)
-  uint64_t thr = 0;
-  if (k <= 64) {
-    // each wave keeps the top 64 of its 128 quarters in registers, wave 0
-    // merges the 8 lists
-    const uint64_t y0 = x0 != INT_MIN ? make_key((float)x0 * sqS - mg, 0xFFFFFFFFu) : 0ull;
-    const uint64_t y1 = x1 != INT_MIN ? make_key((float)x1 * sqS - mg, 0xFFFFFFFFu) : 0ull;
-    buf[w * 64 + lane] = wave_merge_top(wave_sort_desc(y0, (int)lane),
-                                        wave_sort_desc(y1, (int)lane), (int)lane);
-    __syncthreads();
-    if (w == 0) {
-      uint64_t R0 = buf[lane];
-#pragma unroll 1
-      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, buf[v * 64 + lane], (int)lane);
-      const uint64_t bb = readlane64(R0, (int)k - 1);
-      if (lane == 0) thr_sh = bb;
-    }
-    __syncthreads();
-    thr = thr_sh;
-  } else {
-    // k > 64: the same bound from all 4 nwg <= 1024 quarters, sorted in LDS
-    const uint32_t nq4 = 2 * kSelThreads;
-    buf[l0] = x0 != INT_MIN ? make_key((float)x0 * sqS - mg, 0xFFFFFFFFu) : 0ull;
-    buf[l0 + 1] = x1 != INT_MIN ? make_key((float)x1 * sqS - mg, 0xFFFFFFFFu) : 0ull;
-    __syncthreads();
-    bitonic_sort_desc_n(buf, (int)nq4, kSelThreads);
-    thr = k <= nq4 ? buf[k - 1] : 0;
-    __syncthreads();  // buf is the survivors' buffer next
-  }
+  // which bounds the k-th score from below (its radix floor, P0, as well).
+  // (The k-th of per-workgroup maxima, the first form, sat far under the
+  // k-th score once k neared the 256 workgroups: at k = 50, 4578 survivors
+  // per query against 2821.)
+  auto lo_img = [&](int x) -> uint32_t {
+    if (x == INT_MIN) return 0u;
+    const float L = (float)x * sqS - mg;
+    return vs::score_ord(L == 0.0f ? 0.0f : L);
+  };
+  const uint32_t y0 = lo_img(x0), y1 = lo_img(x1);
+  buf[l0] = (uint64_t)y0 << 32;
+  buf[l0 + 1] = (uint64_t)y1 << 32;
+  const uint32_t nzq = (uint32_t)__syncthreads_count(y0 != 0) + (uint32_t)__syncthreads_count(y1 != 0);
+  const uint32_t P0 = nzq >= k ? kth_floor(buf, 2 * kSelThreads, k) : 0u;
   const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
-  const float tl_l = thr ? key_score(thr) : -INFINITY;
+  const float tl_l = P0 ? vs::ord_score(P0) : -INFINITY;
   const float Tcut = tl_b > tl_l ? tl_b : tl_l;
+  tick(1);
   if constexpr (SV == 1) return;
   // only quarters whose largest dot can reach Tcut hold survivors
-  if (c0 && (float)x0 * sqS + mg < Tcut) c0 = 0;
-  if (c1 && (float)x1 * sqS + mg < Tcut) c1 = 0;
+  if (c0 && (float)x0 * sqS + mg < Tcut) c0 = 0, lossy0 = false;
+  if (c1 && (float)x1 * sqS + mg < Tcut) c1 = 0, lossy1 = false;
+  // a lossy quarter that can reach Tcut: its rows are recomputed (slow path)
+  const bool slow = __syncthreads_or(lossy0 || lossy1) != 0;
+  if (lossy0) c0 = 0;
+  if (lossy1) c1 = 0;
   uint32_t incl = c0 + c1;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3314,7 +3417,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     return lo;
   };
   // the passing quarters' slabs: rows whose upper bound (the tile's m) reaches Tcut
-  for (uint32_t base = 0; base < T; base += kSelChunk) {
+  for (uint32_t base = 0; base < (slow ? 0u : T); base += kSelChunk) {
     i32x4_t v[kSelHeld][2];
     uint32_t tl[kSelHeld], ls[kSelHeld];
     bool ok[kSelHeld];
@@ -3354,11 +3457,8 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     }
   }
   __syncthreads();
+  tick(2);
   if constexpr (SV == 2) return;
-  if (spill) {  // uniform
-    if (tid == 0) *gate = 1u;
-    return;
-  }
   const uint32_t ns = fill;
   if (stats && tid == 0) {  // (tools/q8_check.hip) slabs read, survivors
     atomicAdd(stats, T);
@@ -3420,11 +3520,11 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   // wave takes 64 entries at a time and runs the passing ones in groups of
   // 16 (ballot ranks place them in its wscr row), one slot reservation per
   // group.
-  auto rescore_where = [&](auto pred) {
-    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
+  auto rescore_n = [&](uint32_t nb, auto pred) {
+    for (uint32_t base = w * 64; base < nb; base += kSelThreads) {
       const uint32_t i = base + lane;
-      const uint64_t e = i < ns ? buf[i] : 0ull;
-      const bool pass = i < ns && pred(e);
+      const uint64_t e = i < nb ? buf[i] : 0ull;
+      const bool pass = i < nb && pred(e);
       const uint64_t bal = __ballot(pass);
       const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       const uint32_t total = (uint32_t)__popcll(bal);
@@ -3447,52 +3547,126 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       }
     }
   };
-  // (k > 64) The floor P of the 24-bit bucket holding the kk-th largest high
-  // word (an order-preserving score image) of v[0, n), n >= kk: at least kk
-  // entries have a high word >= P. Three 8-bit radix passes as the sample
-  // bound (vs_bound_dev.h), over LDS.
-  auto kth_floor = [&](const uint64_t* v, uint32_t n, uint32_t kk) -> uint32_t {
-    uint32_t prefix = 0;
-#pragma unroll 1
-    for (int pass = 0; pass < 3; ++pass) {
-      const int shift = 24 - 8 * pass;
-      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-      if (tid < 256) hist[tid] = 0;
-      __syncthreads();
-      for (uint32_t i = tid; i < n; i += kSelThreads) {
-        const uint32_t u = (uint32_t)(v[i] >> 32);
-        if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      uint32_t c = 0, x = 0;
-      if (tid < 256) {
-        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
-        x = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) hws[w] = x;
-      }
-      __syncthreads();
-      if (tid < 256) {
-        for (uint32_t j = 0; j < w; ++j) x += hws[j];
-        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
-      }
-      __syncthreads();
-      prefix |= (255u - hpick) << shift;
-      kk -= habove;
-      __syncthreads();  // hist / hws / hpick are rewritten by the next pass
+  auto rescore_where = [&](auto pred) { rescore_n(ns, pred); };
+  // (r05) Slow path -- a passing lossy quarter (the pass dropped slabs: its
+  // rows are recomputed from the int8 copy) or more survivors than the
+  // buffer: an exact streaming top k over the same candidates. Rounds of at
+  // most 4096 rows whose U image reaches the cutoff (the passing quarters'
+  // slabs, one per thread; then the lossy quarters' rows, a tile's 8 rows of
+  // the quarter per thread) are rescored on the pass's chain; the running
+  // top k stays in res[0, rfill) and the cutoff rises to its k-th exact score
+  // (no row under it can enter). Replaces r04's hand-back of the whole batch
+  // to a gated bf16 pass, whose two launches every batch paid ~5-8 us for.
+  if (slow || spill) {  // uniform
+    __shared__ uint32_t cut_sh, nlq;
+    __shared__ uint16_t lq[4 * kMfmaMaxLists];
+    __shared__ __attribute__((aligned(16))) int8_t q8s[D];
+    for (uint32_t i = tid; i < D / 16; i += kSelThreads)
+      ((uint4*)q8s)[i] = ((const uint4*)(r8.q8 + (size_t)q * D))[i];
+    if (tid == 0) {
+      cut_sh = Tcut == -INFINITY ? 0u : vs::score_ord(Tcut == 0.0f ? 0.0f : Tcut);
+      rfill = 0, nlq = 0, fill = 0;
     }
-    return prefix;
-  };
-  if (k > 64 && ns > k + 64) {
-    // Two rounds for k > 64 (r04): the same as below with radix floors for
-    // the two k-th values -- survivors whose U image reaches P1 (>= k of
-    // them) first; P2, the floor of the k-th best exact score among those,
-    // is at most the k-th score, so only survivors under P1 whose U reaches
-    // P2 can still enter.
+    __syncthreads();
+    if (lossy0) lq[atomicAdd(&nlq, 1u)] = (uint16_t)l0;
+    if (lossy1) lq[atomicAdd(&nlq, 1u)] = (uint16_t)(l0 + 1);
+    auto push = [&](float U, uint32_t row) {  // row: local
+      const uint32_t img = vs::score_ord(U == 0.0f ? 0.0f : U);
+      if (img >= cut_sh) buf[atomicAdd(&fill, 1u)] = ((uint64_t)img << 32) | row;
+    };
+    auto round_end = [&]() {
+      __syncthreads();
+      const uint32_t nb = fill;
+      if (nb == 0) return;  // uniform
+      rescore_n(nb, [](uint64_t) { return true; });
+      __syncthreads();
+      const uint32_t nr = rfill;
+      if (nr > k) {
+        // keep the top k: the keys in or above the k-th's bucket, sorted
+        const uint32_t P = kth_floor(res, nr, k);
+        if (tid == 0) fill = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < nr; i += kSelThreads)
+          if ((uint32_t)(res[i] >> 32) >= P) buf[atomicAdd(&fill, 1u)] = res[i];
+        __syncthreads();
+        const uint32_t nf = fill;
+        int p2 = 1;
+        while ((uint32_t)p2 < nf) p2 <<= 1;
+        for (uint32_t i = nf + tid; i < (uint32_t)p2; i += kSelThreads) buf[i] = 0;
+        __syncthreads();
+        bitonic_sort_desc_n(buf, p2, kSelThreads);
+        for (uint32_t j = tid; j < k; j += kSelThreads) res[j] = buf[j];
+        __syncthreads();
+        if (tid == 0) {
+          rfill = k;
+          const uint32_t sk = (uint32_t)(res[k - 1] >> 32);  // the k-th exact score's image
+          cut_sh = sk > cut_sh ? sk : cut_sh;
+        }
+      }
+      if (tid == 0) fill = 0;
+      __syncthreads();
+    };
+    for (uint32_t base = 0; base < T; base += kSelThreads) {
+      const uint32_t i = base + tid;
+      if (i < T) {
+        const uint32_t l = list_of(i);
+        const size_t e = slab_at(l, i - pre[l]);
+        const i32x4_t v0 = __builtin_bit_cast(i32x4_t, slabs[2 * e]);
+        const i32x4_t v1 = __builtin_bit_cast(i32x4_t, slabs[2 * e + 1]);
+        const uint32_t lr0 = tiles[e] - row_base, lt = lr0 >> 5;
+        const float mt = pa * meta[2 * (size_t)lt] + (pc + sig) * meta[2 * (size_t)lt + 1];
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+          const int dv = bb < 4 ? v0[bb] : v1[bb - 4];
+          if (dv != INT_MIN)
+            push((float)dv * sqS + mt,
+                 lr0 + 16u * (uint32_t)(bb >> 2) + 4u * (l & 3) + (uint32_t)(bb & 3));
+        }
+      }
+      round_end();
+    }
+    const uint32_t nlossy = nlq;
+    for (uint32_t j = 0; j < nlossy; ++j) {
+      const uint32_t l = lq[j], wg = l >> 2, kql = l & 3;
+      const uint32_t wr0 = wg * r8.rows_per_wg;
+      const uint32_t wr1 = (uint64_t)wr0 + r8.rows_per_wg < r8.n_rows ? wr0 + r8.rows_per_wg : r8.n_rows;
+      const uint32_t t0 = wr0 / 32, t1 = (wr1 + 31) / 32;
+      for (uint32_t base = t0; base < t1; base += kSelThreads) {
+        const uint32_t tt = base + tid;
+        if (tt < t1) {
+          const float mt = pa * meta[2 * (size_t)tt] + (pc + sig) * meta[2 * (size_t)tt + 1];
+#pragma unroll 1
+          for (int bb = 0; bb < 8; ++bb) {
+            const uint32_t row = tt * 32 + 16u * (uint32_t)(bb >> 2) + 4u * kql + (uint32_t)(bb & 3);
+            if (row < wr1 && row_allowed(r8.allow, row))
+              push((float)q8_row_dot<D>(r8.x8 + (size_t)row * D, q8s) * sqS + mt, row);
+          }
+        }
+        round_end();
+      }
+    }
+    // the running top k (sorted once a round compacted it)
+    const uint32_t nr = rfill;
+    if (nr <= 64) {
+      if (w == 0) sel_finish_wave(res, nr, k, (int)lane, out + (size_t)q * k);
+    } else {
+      int p2 = 1;
+      while ((uint32_t)p2 < nr) p2 <<= 1;
+      for (uint32_t i = nr + tid; i < (uint32_t)p2; i += kSelThreads) res[i] = 0;
+      __syncthreads();
+      bitonic_sort_desc_n(res, p2, kSelThreads);
+      for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nr ? res[j] : 0;
+    }
+    if (stats && tid == 0) atomicAdd(stats + 2, 1u);  // (tools) slow-path queries
+    tick(4);
+    return;
+  }
+  if (ns > k + 64) {
+    // Two rounds (r04; r05: radix floors for every k): the survivors whose U
+    // image reaches P1 (the floor of the bucket of the k-th largest U: at
+    // least k of them) first; P2, the floor of the k-th best exact score
+    // among those, is at most the k-th score, so only survivors under P1
+    // whose U reaches P2 can still enter -- the window shrinks from ~2m to ~m.
     const uint32_t P1 = kth_floor(buf, ns, k);
     rescore_where([&](uint64_t e) { return (uint32_t)(e >> 32) >= P1; });
     __syncthreads();
@@ -3501,71 +3675,18 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       const uint32_t u = (uint32_t)(e >> 32);
       return u < P1 && u >= P2;
     });
-  } else if (k <= 64 && ns > 64) {
-    // Two rounds (r04): the k survivors with the largest upper bounds first;
-    // the k-th best exact score among them, Sk, is at most the k-th score, so
-    // only survivors whose upper bound reaches Sk can still enter -- about
-    // half of them (the bound window shrinks from 2m to m)
-    uint64_t R = 0;
-    for (uint32_t base = w * 64; base < ns; base += kSelThreads) {
-      const uint64_t x = base + lane < ns ? buf[base + lane] : 0ull;
-      R = wave_merge_top(R, wave_sort_desc(x, (int)lane), (int)lane);
-    }
-    res[w * 64 + lane] = R;  // scratch: res is filled only after the barrier below
-    __syncthreads();
-    if (w == 0) {
-      uint64_t R0 = res[lane];
-#pragma unroll 1
-      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, res[v * 64 + lane], (int)lane);
-      const uint64_t uk = readlane64(R0, (int)k - 1);
-      if (lane == 0) thr_sh = uk;
-    }
-    __syncthreads();
-    const uint64_t Uk = thr_sh;  // survivor entries are distinct: exactly k reach it
-    rescore_where([&](uint64_t e) { return e >= Uk; });
-    __syncthreads();
-    if (w == 0) {
-      const uint32_t na = rfill;
-      const uint64_t x = wave_sort_desc((uint32_t)lane < na ? res[lane] : 0ull, (int)lane);
-      const uint64_t sk = readlane64(x, (int)k - 1);
-      if (lane == 0) thr_sh = sk;
-    }
-    __syncthreads();
-    const float Sk = key_score(thr_sh);
-    rescore_where([&](uint64_t e) { return e < Uk && vs::ord_score((uint32_t)(e >> 32)) >= Sk; });
   } else {
     rescore_where([&](uint64_t) { return true; });
   }
   if constexpr (SV == 3) return;
   __syncthreads();
+  tick(3);
+  // the final top k: the keys whose score image reaches the floor of the
+  // k-th (at least k, a few more in its bucket), sorted
   const uint32_t nr = rfill;
-  if (nr <= 64) {
-    if (w == 0) sel_finish_wave(res, nr, k, (int)lane, out + (size_t)q * k);
-    return;
-  }
-  if (k <= 64) {
-    // each wave keeps the top 64 of its share in registers (64 keys sorted
-    // and merged at a time, no barrier), then wave 0 merges the 8 lists
-    uint64_t R = 0;
-    for (uint32_t base = w * 64; base < nr; base += kSelThreads) {
-      const uint64_t x = base + lane < nr ? res[base + lane] : 0ull;
-      R = wave_merge_top(R, wave_sort_desc(x, (int)lane), (int)lane);
-    }
-    buf[w * 64 + lane] = R;  // buf is free
-    __syncthreads();
-    if (w == 0) {
-      uint64_t R0 = buf[lane];
-#pragma unroll 1
-      for (int v = 1; v < kSelThreads / 64; ++v) R0 = wave_merge_top(R0, buf[v * 64 + lane], (int)lane);
-      if (lane < k) out[(size_t)q * k + lane] = R0;
-    }
-    return;
-  }
-  // k > 64: the keys whose score image reaches the floor of the k-th (at
-  // least k, a few more in its bucket) into buf, sorted there
   const uint64_t* fin = res;
   uint32_t nf = nr;
-  if (nr > 256) {
+  if (nr > 64) {
     const uint32_t P3 = kth_floor(res, nr, k);
     if (tid == 0) fill = 0;
     __syncthreads();
@@ -3577,6 +3698,11 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     fin = buf;
     nf = fill;
   }
+  if (nf <= 64) {
+    if (w == 0) sel_finish_wave(fin, nf, k, (int)lane, out + (size_t)q * k);
+    tick(4);
+    return;
+  }
   uint64_t* srt = const_cast<uint64_t*>(fin);
   int p2 = 1;
   while ((uint32_t)p2 < nf) p2 <<= 1;
@@ -3584,6 +3710,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __syncthreads();
   bitonic_sort_desc_n(srt, p2, kSelThreads);
   for (uint32_t j = tid; j < k; j += kSelThreads) out[(size_t)q * k + j] = j < nf ? srt[j] : 0;
+  tick(4);
 }
 
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
@@ -3591,8 +3718,14 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             uint32_t k, uint64_t* out,
                             uint32_t row_base, const void* X, const void* qb, bool f32, uint32_t dim,
                             const float* q8par, const float* q8glob, const float* meta,
-                            const float* bound, uint32_t* gate, hipStream_t st, uint32_t* stats) {
-  if (!select_args_ok(nwg, cap, nq, k) || !cand_max) return hipErrorInvalidValue;
+                            const float* bound, const void* X8, const void* Q8,
+                            const uint64_t* allow, uint32_t n_rows, hipStream_t st, uint32_t* stats,
+                            uint64_t* clk) {
+  if (!select_args_ok(nwg, cap, nq, k) || !cand_max || !X8 || !Q8) return hipErrorInvalidValue;
+  uint32_t gwg = 0, rpw = 0;
+  mfma_grid(n_rows, &gwg, &rpw);
+  if (gwg != nwg) return hipErrorInvalidValue;  // the pass's static split
+  const Q8Rows r8{(const int8_t*)X8, (const int8_t*)Q8, allow, n_rows, rpw, row_base};
   static const int sv = [] {
     const char* e = getenv("VS_Q8_SEL_SV");
     return e ? atoi(e) : 0;
@@ -3609,7 +3742,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
                      cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
-                     (const f32x4_t*)q8par, q8glob, meta, bound, gate, stats);
+                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, stats, clk);
   return hipGetLastError();
 }
 

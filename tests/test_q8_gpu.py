@@ -307,3 +307,40 @@ def test_prefilter_dropped_on_failed_refresh(tmp_path):
     p = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True,
                        text=True, timeout=240)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout[-2000:] + p.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("copies,spread", [(3000, False), (20000, True), (500, True)])
+def test_select_recomputes_lossy_quarters_and_streams_spills(pkg, orc, copies, spread):
+    """r05: a quarter the int8 pass overflowed (its count past its capacity)
+    is recomputed from the int8 copy by the select, and more survivors than
+    the select's buffer stream through a running top k -- no gated bf16 pass
+    behind the batch. Duplicated rows (RAG corpora repeat boilerplate chunks)
+    force both: copies of one row, contiguous (one workgroup's quarters) or
+    spread over the collection, with queries aligned to them and random ones.
+    Keys equal the bf16 pass's bit for bit, and the oracle's."""
+    n, dim = 300_000, DIM
+    rng = np.random.default_rng(copies)
+    X = orc.generate(61, 0, n, dim, bf16=True)
+    dst = (rng.choice(n, copies, replace=False) if spread else np.arange(40_000, 40_000 + copies))
+    X[dst] = X[11]
+    a = pkg.VectorEngine(device=0)
+    b = pkg.VectorEngine(device=0, prefilter=False)
+    try:
+        for e in (a, b):
+            e.create_collection("o", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16)
+            e.upsert("o", np.arange(n), X)
+        assert a.prefilter_bytes("o") > 0
+        Q = orc.generate(orc.SEED_QUERY, 3300, 40, dim)
+        Q[:8] = X[11] * np.linspace(0.5, 2.0, 8)[:, None]  # the copies lead
+        Q[8:12] = X[11] * 0.7 + Q[8:12] * 0.3
+        Qp = orc.preprocess(Q, False, True)
+        for k in (10, 64, 100):
+            s1, r1, c1 = a.search("o", Q, k)
+            s2, r2, c2 = b.search("o", Q, k)
+            assert np.array_equal(c1, c2) and np.array_equal(r1, r2)
+            assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+            _parity(orc, X, Qp, s1, r1, c1, k)
+    finally:
+        a.close()
+        b.close()

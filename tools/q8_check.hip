@@ -58,8 +58,8 @@ int stats_mode(uint32_t n, uint32_t nq, uint32_t dim, uint32_t k) {
   CK(hipMalloc(&tiles, slots * 4));
   CK(hipMalloc(&cnt, (size_t)nwg * 256 * 16));
   CK(hipMalloc(&cmx, (size_t)nwg * 256 * 16));
-  CK(hipMalloc(&stats, 8));
-  CK(hipMemset(stats, 0, 8));
+  CK(hipMalloc(&stats, 16));
+  CK(hipMemset(stats, 0, 16));
   CK(hipMalloc(&tmax, (size_t)256 * nwg * st * 4));
   CK(hipMalloc(&bound, 256 * 4));
   uint64_t* out;
@@ -70,7 +70,7 @@ int stats_mode(uint32_t n, uint32_t nq, uint32_t dim, uint32_t k) {
   CK(vsk::launch_mfma_cand_q8(dX8, dim, n, 0, dQ8, nq, k, bound, par, glob, slabs, tiles, cap, cnt,
                               cmx, nwg, &L, gate, 0));
   CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, false, dim, par, glob,
-                           meta, bound, gate, 0, stats));
+                           meta, bound, dX8, dQ8, nullptr, n, 0, stats));
   CK(hipDeviceSynchronize());
   std::vector<uint32_t> hc((size_t)nwg * 256 * 4);
   CK(hipMemcpy(hc.data(), cnt, hc.size() * 4, hipMemcpyDeviceToHost));
@@ -261,7 +261,7 @@ int main(int argc, char** argv) {
                 mn, mxall, best);
   }
   CK(vsk::launch_select_q8(slabs, tiles, cnt, cmx, nwg, cap, nq, k, out, 0, dX, dQ, false, dim, par, glob, meta,
-                           bound, gate, 0));
+                           bound, dX8, dQ8, nullptr, n, 0));
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(&hgate, gate, 4, hipMemcpyDeviceToHost));
   std::vector<uint64_t> ho(nq * k);

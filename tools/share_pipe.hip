@@ -1,0 +1,171 @@
+// share_pipe.hip — the batched int8 path's per-batch stages at one shard's
+// size, timed back to back (r05; VERDICT r04 item 1: the N = 8 share's fixed
+// cost). Replays vs_engine.cpp search_mfma's int8 branch with the library's
+// launchers on one resident corpus and times R batches per arm (events only
+// around the whole loop, so the arms see the serving regime):
+//   full      query prep + sample pass + bound/int8 queries + int8 pass +
+//             select (the product's sequence since r05)
+//   r04gate   full + r04's two gated launches (stand-downs)
+//   noselect  without the select (and gates)
+//   pass      the int8 pass alone (bound precomputed)
+//   front     query prep + sample pass + bound only
+// then one batch with select_q8's per-workgroup stage clocks (start, bound,
+// survivors, rescore, end; medians over the queries, us).
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/share_pipe.hip -o tools/share_pipe \
+//     -I<pkg>/csrc -L<pkg>/lib -lvsearch -Wl,-rpath,<pkg>/lib
+//   share_pipe [ROWS=1250000] [K=10] [REPS=200] [DIM=768]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "vs_kernels.h"
+
+#define CK(x)                                                                           \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      std::exit(1);                                                                     \
+    }                                                                                   \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const uint32_t n = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1250000;
+  const uint32_t k = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 10;
+  const int reps = argc > 3 ? std::atoi(argv[3]) : 200;
+  const uint32_t dim = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 768;
+  const uint32_t nq = 256, PS = 256;
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  uint16_t *X, *qb;
+  int8_t *X8, *q8q;
+  float *meta, *glob, *qf, *qp, *q8par, *tmax, *bound, *slabs;
+  CK(hipMalloc(&X, (size_t)(n + 32) * dim * 2));
+  CK(hipMemset(X, 0, (size_t)(n + 32) * dim * 2));
+  CK(hipMalloc(&X8, (size_t)(n + 32) * dim));
+  CK(hipMemset(X8, 0, (size_t)(n + 32) * dim));
+  CK(hipMalloc(&meta, (size_t)((n + 32) / 32 + 1) * 8));
+  CK(hipMalloc(&glob, 16));
+  CK(hipMalloc(&qf, (size_t)PS * dim * 4));
+  CK(hipMalloc(&qp, (size_t)PS * dim * 4));
+  CK(hipMalloc(&qb, (size_t)PS * dim * 2));
+  CK(hipMalloc(&q8q, (size_t)PS * dim));
+  CK(hipMalloc(&q8par, PS * 16 + 64));
+  uint32_t* gate = (uint32_t*)(q8par + 4 * PS);
+  CK(vsk::launch_generate(0x5EED, 0, n, dim, true, X, 0, st));
+  CK(vsk::launch_generate(0xC0FFEE, 0, nq, dim, false, qf, 0, st, 1));
+  CK(hipMemsetAsync(glob, 0, 16, st));
+  CK(vsk::launch_q8_absmax(X, false, (uint64_t)n * dim, glob, st));
+  CK(vsk::launch_q8_set_scale(glob, st));
+  CK(vsk::launch_q8_quantize(X, false, n, dim, nullptr, 0, (n + 31) / 32, X8, meta, glob, st));
+  const uint32_t maxl = vsk::mfma_max_lists(n);
+  const uint32_t st0 = vsk::mfma_sample_tiles(n, dim, false);
+  const uint32_t tpw = vsk::mfma_tiles_per_wg(n);
+  const double f = k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0;
+  const uint32_t stl = (uint32_t)std::max(1.0, std::min({(double)vsk::kMfmaMaxSampleTiles, (double)tpw,
+                                                          st0 * f}));
+  const uint32_t cap = vsk::mfma_cand_cap(n, k, stl);
+  const uint32_t cap8 = vsk::mfma_cand_cap(n, k, st0, 8.0);
+  const uint32_t capx = std::max(cap, cap8);
+  const size_t slots = (size_t)maxl * PS * capx;
+  CK(hipMalloc(&slabs, slots * 36));
+  uint32_t* slab_tile = (uint32_t*)((char*)slabs + slots * 32);
+  uint32_t* cnt;
+  CK(hipMalloc(&cnt, (size_t)maxl * PS * 4 * 4 * 2));
+  uint32_t* qmax = cnt + (size_t)maxl * PS * 4;
+  CK(hipMalloc(&tmax, (size_t)maxl * stl * PS * 4));
+  CK(hipMalloc(&bound, PS * 4));
+  uint64_t *out, *clk;
+  CK(hipMalloc(&out, (size_t)nq * k * 8));
+  CK(hipMalloc(&clk, (size_t)nq * 8 * 8));
+  CK(hipMemset(clk, 0, (size_t)nq * 8 * 8));
+
+  uint32_t L = 0;
+  auto prep = [&]() { CK(vsk::launch_query_prep(qf, nq, dim, false, true, nullptr, qb, st)); };
+  auto sample = [&]() {
+    CK(vsk::launch_mfma_sample(X, false, dim, n, 0, qb, nq, k, stl, tmax, maxl, &L, st, nullptr));
+  };
+  auto boundq8 = [&]() {
+    CK(vsk::launch_sample_bound_q8(tmax, L * stl, nq, k, bound, qb, false, nq, dim, glob, q8q, q8par,
+                                   gate, st));
+  };
+  auto pass = [&]() {
+    CK(vsk::launch_mfma_cand_q8(X8, dim, n, 0, q8q, nq, k, bound, q8par, glob, slabs, slab_tile, cap8,
+                                cnt, qmax, maxl, &L, gate, st, nullptr));
+  };
+  auto select = [&](uint64_t* c) {
+    CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim,
+                             q8par, glob, meta, bound, X8, q8q, nullptr, n, st, nullptr, c));
+  };
+  // r04's two gated launches (the bf16 pass + select behind every int8
+  // batch, standing down unless *gate): kept as an arm to price them
+  auto gated = [&]() {
+    CK(vsk::launch_mfma_cand(X, false, dim, n, 0, qb, nq, k, bound, slabs, slab_tile, cap, cnt, maxl, &L,
+                             st, nullptr, qmax, gate));
+    CK(vsk::launch_select_slabs(slabs, slab_tile, cnt, L, cap, nq, k, out, st, 0, nullptr, qmax, gate));
+  };
+  // one full batch first: bounds and int8 queries for the "pass" arm
+  prep(), sample(), boundq8(), pass(), select(nullptr);
+  CK(hipStreamSynchronize(st));
+  uint32_t hg = 0;
+  CK(hipMemcpy(&hg, gate, 4, hipMemcpyDeviceToHost));
+
+  struct Arm {
+    const char* name;
+    std::function<void()> f;
+  };
+  std::vector<Arm> arms = {
+      {"full", [&] { prep(), sample(), boundq8(), pass(), select(nullptr); }},
+      {"r04gate", [&] { prep(), sample(), boundq8(), pass(), select(nullptr), gated(); }},
+      {"noselect", [&] { prep(), sample(), boundq8(), pass(); }},
+      {"pass", [&] { pass(); }},
+      {"front", [&] { prep(), sample(), boundq8(); }},
+  };
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  std::printf("{\"rows\": %u, \"k\": %u, \"dim\": %u, \"reps\": %d, \"sample_tiles\": %u, \"cap8\": %u, "
+              "\"gate\": %u", n, k, dim, reps, stl, cap8, hg);
+  // arms interleaved over rounds (clock drift spreads evenly); medians
+  const int rounds = 5;
+  std::vector<std::vector<float>> t(arms.size());
+  for (int r = 0; r < rounds; ++r)
+    for (size_t i = 0; i < arms.size(); ++i) {
+      for (int w = 0; w < 5; ++w) arms[i].f();
+      CK(hipEventRecord(a, st));
+      for (int j = 0; j < reps; ++j) arms[i].f();
+      CK(hipEventRecord(b, st));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      t[i].push_back(ms * 1e3f / reps);
+    }
+  for (size_t i = 0; i < arms.size(); ++i) {
+    std::sort(t[i].begin(), t[i].end());
+    std::printf(", \"%s_us\": %.2f", arms[i].name, t[i][rounds / 2]);
+  }
+  // select stage clocks (wall_clock64: 100 MHz)
+  prep(), sample(), boundq8(), pass(), select(clk);
+  CK(hipStreamSynchronize(st));
+  std::vector<uint64_t> h((size_t)nq * 8);
+  CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
+  uint64_t t0 = ~0ull;
+  for (uint32_t q = 0; q < nq; ++q) t0 = std::min(t0, h[(size_t)q * 8]);
+  const char* names[5] = {"start", "bound", "survivors", "rescore", "end"};
+  for (int s = 0; s < 5; ++s) {
+    std::vector<double> v;
+    for (uint32_t q = 0; q < nq; ++q)
+      if (h[(size_t)q * 8 + s]) v.push_back((h[(size_t)q * 8 + s] - t0) * 0.01);
+    std::sort(v.begin(), v.end());
+    if (!v.empty())
+      std::printf(", \"sel_%s_us_med\": %.2f, \"sel_%s_us_max\": %.2f", names[s], v[v.size() / 2], names[s],
+                  v.back());
+  }
+  std::printf("}\n");
+  return 0;
+}
