@@ -1878,6 +1878,10 @@ template <bool B>
 struct MfFull {
   static constexpr bool value = B;
 };
+template <int V>
+struct MfSet {
+  static constexpr int value = V;
+};
 
 // Byte geometry of the streamed rows (EB = element bytes: 2 bf16, 4 fp32).
 // A step is 64 bytes of a row: 32 k of bf16 (one 16x16x32 MFMA per row half
@@ -2068,9 +2072,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // ~25 GB/s per CU) overlaps the ~6 us of B-fragment loads from L2 that every
   // launch starts with; the prologue's vmcnt(0) drain then covers both.
   constexpr bool kEarlyFill = (VAR & 8388608) != 0;
+  // VAR 33554432 (r05, int8 pass): one barrier per PAIR of chunks (tiles: a
+  // 24 KiB chunk is one 32-row tile of 768-B int8 rows) instead of one per
+  // chunk, and the two freed slots refilled at once. With 6 slots: before the
+  // barrier of the pair (c, c + 1) chunks up to c + 2 have landed (c + 3 may
+  // pend), the barrier frees the previous pair's slots, and chunks c + 4,
+  // c + 5 are issued into them (4 chunks ahead instead of 5). The per-tile
+  // fixed cost (wait, barrier, DMA issue) is half the int8 pass's 48 MFMAs
+  // per wave and tile where the bf16 pass had 96.
+  constexpr bool kPair = (VAR & 33554432) != 0 && kBF && S::CPT == 1 && S::NSLOT == 6 &&
+                         (VAR & 1048576) == 0 && kDma;
+  constexpr uint32_t kFill = kPair ? (uint32_t)S::AHEAD - 1 : (uint32_t)S::AHEAD;
   if constexpr (kDma && kBF && kEarlyFill) {
 #pragma unroll
-    for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
+    for (uint32_t c = 0; c < kFill; ++c) issue_next_bf(c < nchunks);
   }
   // B operand of group g: Q[query 32w+16g+col][32t + 8kq + j], j = 0..7.
   bf16x8_t qf[G][S::T];
@@ -2143,9 +2158,9 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   if constexpr (kDma && kBF) {
     if constexpr (!kEarlyFill) {
 #pragma unroll
-      for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c) issue_next_bf(c < nchunks);
+      for (uint32_t c = 0; c < kFill; ++c) issue_next_bf(c < nchunks);
     }
-    wait_vmcnt<PPW * (S::AHEAD - 1)>();
+    wait_vmcnt<PPW * (kFill - 1)>();
   } else {
     if constexpr (kDma)
       for (uint32_t c = 0; c < (uint32_t)S::AHEAD; ++c)
@@ -2185,10 +2200,70 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // their LDS-read bursts and barriers half a chunk apart instead of in
   // lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9).
   constexpr bool kStag = (VAR & 1048576) != 0 && kBF && WAVES == 8;
-  auto tile = [&](uint32_t t, auto full_tag, auto stag_tag) {
+  // int8 pass epilogue of one tile (accumulators ac, first row trow0): a lane
+  // whose largest dot of the tile reaches the query's integer threshold
+  // appends its 8 dots (int32 bits) -- the select bounds and rescores them.
+  // Padding and filtered-out rows (the pre-mask) are INT_MIN in the slab:
+  // never a maximum, never a survivor.
+  auto q8_epi = [&](f32x4_t (&ac)[2][G], uint32_t trow0, bool full) {
+    uint32_t am = 0xFFu;
+    if (a.allow) {
+      const uint32_t tw = (uint32_t)(a.allow[trow0 >> 6] >> (trow0 & 32)) >> (4 * kq);
+      am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
+      // one ext_vector element (it reads element 0; tools/q8_check.hip found it)
+      const i32x4_t a0 = __builtin_bit_cast(i32x4_t, ac[0][g]);
+      const i32x4_t a1 = __builtin_bit_cast(i32x4_t, ac[1][g]);
+      int v[8];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
+      if (!full || a.allow) {  // uniform: unfiltered full tiles skip it
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1 || !((am >> b) & 1u)) v[b] = INT_MIN;
+        ac[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
+        ac[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
+      }
+      const int mx = imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
+      // VAR 16777216 (timing ablation only, wrong answers): never append
+      if ((VAR & 16777216) != 0) {
+        asm volatile("" ::"v"(mx >= th_i[g]));
+        continue;
+      }
+      if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
+        const uint32_t sub = a.cand_cap >> 2;
+        const uint32_t cg = cnt_r[g];
+        // r05: a full quarter keeps counting (a count past its capacity
+        // marks it lossy: select_q8 recomputes its rows from the int8
+        // copy) and its largest dot stays exact; no hand-back
+        if (cg < sub) {
+          const size_t slot = (size_t)slot0[g] + cg;
+          f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
+          sp[0] = ac[0][g];
+          sp[1] = ac[1][g];
+          a.cand_tile[slot] = a.row_base + trow0;
+        }
+        cnt_r[g] = cg + 1;
+        qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
+      }
+    }
+  };
+  // VAR 67108864 (r05, int8 pass): the epilogue of tile t runs after the first
+  // step's MFMAs of tile t + 1, on the other of two accumulator sets, so its
+  // VALU work and its wait for the tile's last MFMA results overlap the
+  // matrix pipe instead of stalling it at every tile's end
+  constexpr bool kEpiPipe = I8 && MODE == 0 && (VAR & 67108864) != 0;
+  f32x4_t accq[kEpiPipe ? 2 : 1][2][G];
+  uint32_t prow0 = 0;
+  bool pfull = true, have_prev = false;
+  auto tile = [&](uint32_t t, auto full_tag, auto stag_tag, auto set_tag) {
     constexpr bool STAG = decltype(stag_tag)::value;
+    constexpr int SET = decltype(set_tag)::value;
     constexpr int SYNC_STEP = STAG ? S::CT / 2 : 0;
-    f32x4_t acc[2][G];  // [row half][query group]
+    f32x4_t (&acc)[2][G] = accq[kEpiPipe ? SET : 0];  // [row half][query group]
 #pragma unroll
     for (int hr = 0; hr < 2; ++hr)
 #pragma unroll
@@ -2211,7 +2286,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       auto sync_chunk = [&]() {
         __builtin_amdgcn_sched_barrier(0);
         // chunk c+1 landed for this wave: chunks c+2 .. c+AHEAD-1 may pend
-        if constexpr (kDma && kBF) {
+        // (pairs: chunks up to c+2 landed, c+3 may pend)
+        if constexpr (kPair) {
+          wait_vmcnt<PPW>();
+        } else if constexpr (kDma && kBF) {
           wait_vmcnt<PPW * (S::AHEAD - 2)>();
         } else if constexpr (kDma) {
           if (c + S::AHEAD <= nchunks)
@@ -2224,12 +2302,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         if constexpr (MODE != 5 && (VAR & 134217728) == 0)
           __builtin_amdgcn_s_barrier();  // chunk c+1 visible; slot c-1 free
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (kDma && kBF)
+        if constexpr (kPair) {
+          issue_next_bf(c + 4 < nchunks);
+          issue_next_bf(c + 5 < nchunks);
+        } else if constexpr (kDma && kBF) {
           issue_next_bf(refill);
-        else if (!kSpread && refill)
+        } else if (!kSpread && refill) {
           issue_next();
+        }
       };
-      if constexpr (!STAG || MODE == 2) sync_chunk();
+      if constexpr (kPair) {
+        if ((c & 1u) == 0) sync_chunk();  // uniform
+      } else if constexpr (!STAG || MODE == 2) {
+        sync_chunk();
+      }
       if constexpr (MODE != 2) {
 #pragma unroll
         for (int s = 0; s < S::CT; ++s) {
@@ -2291,6 +2377,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             }
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+          if constexpr (kEpiPipe) {
+            if (u == 0 && s == 0 && have_prev) {
+              q8_epi(accq[1 - SET], prow0, pfull);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
           if constexpr (kSpread) {
             // piece i after step i * CT / PPW (the last one also advances)
 #pragma unroll
@@ -2319,7 +2411,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     // (trow0 % 32 == 0); a lane's rows 4kq+i and 16+4kq+i are bits i and 4+i
     // of am. Masked rows score -inf and never pass.
     uint32_t am = 0xFFu;
-    if (a.allow) {
+    if (a.allow && !(I8 && MODE == 0)) {
       const uint32_t tw = (uint32_t)(a.allow[trow0 >> 6] >> (trow0 & 32)) >> (4 * kq);
       am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
       // the main pass leaves its accumulators as they are (the slab's masked
@@ -2336,48 +2428,10 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       }
     }
     if constexpr (I8 && MODE == 0) {
-      // int8 prefilter: a lane whose largest dot of the tile reaches the
-      // query's integer threshold appends its 8 dots (int32 bits) -- the
-      // select bounds and rescores them. Padding and filtered-out rows (the
-      // pre-mask am) are INT_MIN in the slab: never a maximum, never a survivor.
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
-        // one ext_vector element (it reads element 0; tools/q8_check.hip found it)
-        const i32x4_t a0 = __builtin_bit_cast(i32x4_t, acc[0][g]);
-        const i32x4_t a1 = __builtin_bit_cast(i32x4_t, acc[1][g]);
-        int v[8];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
-        if (!full || a.allow) {  // uniform: unfiltered full tiles skip it
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-            if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1 || !((am >> b) & 1u)) v[b] = INT_MIN;
-          acc[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
-          acc[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
-        }
-        const int mx = imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
-        // VAR 16777216 (timing ablation only, wrong answers): never append
-        if ((VAR & 16777216) != 0) {
-          asm volatile("" ::"v"(mx >= th_i[g]));
-          continue;
-        }
-        if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
-          const uint32_t sub = a.cand_cap >> 2;
-          const uint32_t cg = cnt_r[g];
-          // r05: a full quarter keeps counting (a count past its capacity
-          // marks it lossy: select_q8 recomputes its rows from the int8
-          // copy) and its largest dot stays exact; no hand-back
-          if (cg < sub) {
-            const size_t slot = (size_t)slot0[g] + cg;
-            f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
-            sp[0] = acc[0][g];
-            sp[1] = acc[1][g];
-            a.cand_tile[slot] = a.row_base + trow0;
-          }
-          cnt_r[g] = cg + 1;
-          qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
-        }
+      if constexpr (kEpiPipe) {  // run after the next tile's first step (or at the end)
+        prow0 = trow0, pfull = full, have_prev = true;
+      } else {
+        q8_epi(acc, trow0, full);
       }
       return;
     } else if constexpr (I8) {
@@ -2510,12 +2564,31 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   };
   uint32_t nfull = (wr1 - wr0) / 32;
   if (nfull > ntiles) nfull = ntiles;
+  // (kEpiPipe) tiles alternate between the two accumulator sets
+  auto tile_p = [&](uint32_t t, auto full_tag, auto stag_tag) {
+    if constexpr (kEpiPipe) {
+      if (t & 1u)
+        tile(t, full_tag, stag_tag, MfSet<1>{});
+      else
+        tile(t, full_tag, stag_tag, MfSet<0>{});
+    } else {
+      tile(t, full_tag, stag_tag, MfSet<0>{});
+    }
+  };
   auto run_tiles = [&](auto stag_tag) {
     if constexpr (kPeel) {
-      for (uint32_t t = 0; t < nfull; ++t) tile(t, MfFull<true>{}, stag_tag);
-      for (uint32_t t = nfull; t < ntiles; ++t) tile(t, MfFull<false>{}, stag_tag);
+      for (uint32_t t = 0; t < nfull; ++t) tile_p(t, MfFull<true>{}, stag_tag);
+      for (uint32_t t = nfull; t < ntiles; ++t) tile_p(t, MfFull<false>{}, stag_tag);
     } else {
-      for (uint32_t t = 0; t < ntiles; ++t) tile(t, MfFull<false>{}, stag_tag);
+      for (uint32_t t = 0; t < ntiles; ++t) tile_p(t, MfFull<false>{}, stag_tag);
+    }
+    if constexpr (kEpiPipe) {  // the last tile's epilogue
+      if (have_prev) {
+        if ((ntiles - 1) & 1u)
+          q8_epi(accq[1], prow0, pfull);
+        else
+          q8_epi(accq[0], prow0, pfull);
+      }
     }
   };
   if constexpr (kStag) {
@@ -3274,7 +3347,8 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t fill, spill, rfill;
   __shared__ uint32_t hist[256], hws[4], hpick, habove;  // kth_floor's radix state
   // (tools/share_pipe.hip) per-workgroup wall clock at the stage boundaries:
-  // start, bound, survivors, rescore, end
+  // 0 start, 1 bound, 2 survivors, 3 rescore, 4 end; two rounds: 5 first
+  // floor, 6 first round, 7 second floor
   auto tick = [&](int i) {
     if (clk && threadIdx.x == 0) clk[(size_t)blockIdx.x * 8 + i] = wall_clock64();
   };
@@ -3668,9 +3742,12 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     // among those, is at most the k-th score, so only survivors under P1
     // whose U reaches P2 can still enter -- the window shrinks from ~2m to ~m.
     const uint32_t P1 = kth_floor(buf, ns, k);
+    tick(5);
     rescore_where([&](uint64_t e) { return (uint32_t)(e >> 32) >= P1; });
     __syncthreads();
+    tick(6);
     const uint32_t P2 = kth_floor(res, rfill, k);
+    tick(7);
     rescore_where([&](uint64_t e) {
       const uint32_t u = (uint32_t)(e >> 32);
       return u < P1 && u >= P2;

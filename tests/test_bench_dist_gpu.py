@@ -49,6 +49,14 @@ def test_two_ranks_equal_one_rank(tmp_path, config, rows):
     assert r1["config"]["rows_per_gpu"] == rows
     assert k1.shape == k2.shape and k1.shape[1] == 10
     np.testing.assert_array_equal(k1, k2)
+    # each line prices ITS rank's launch, and carries HBM
+    # traffic only when measured on exactly that many rows (none here)
+    for r in (r1, r2):
+        roof = r["roofline"]
+        assert roof["bytes_per_launch"] >= r["config"]["rows_per_gpu"] * r["config"]["dim"]
+        assert roof["bytes_per_launch"] < 1.1 * r["config"]["rows_per_gpu"] * r["config"]["dim"] * 4
+        assert roof["traffic"] is None and roof["traffic_rows"] is None
+    assert r1["roofline"]["bytes_per_launch"] > r2["roofline"]["bytes_per_launch"]
 
 
 @pytest.mark.gpu
@@ -75,4 +83,6 @@ def test_rccl_one_rank_gather_equals_plain(tmp_path, collective):
     r2 = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert r2["n_gpus"] == 1 and r2["config"]["rows_per_gpu"] == 200_000
     assert r2["config"]["collective"] == collective
+    assert r2["roofline"]["traffic"] is None  # no PMC entry at 200k rows
+    assert r2["roofline"]["bytes_per_launch"] == r1["roofline"]["bytes_per_launch"]
     np.testing.assert_array_equal(k1, np.load(out))

@@ -156,8 +156,8 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
   uint64_t t0 = ~0ull;
   for (uint32_t q = 0; q < nq; ++q) t0 = std::min(t0, h[(size_t)q * 8]);
-  const char* names[5] = {"start", "bound", "survivors", "rescore", "end"};
-  for (int s = 0; s < 5; ++s) {
+  const char* names[8] = {"start", "bound", "survivors", "rescore", "end", "p1", "round1", "p2"};
+  for (int s = 0; s < 8; ++s) {
     std::vector<double> v;
     for (uint32_t q = 0; q < nq; ++q)
       if (h[(size_t)q * 8 + s]) v.push_back((h[(size_t)q * 8 + s] - t0) * 0.01);
