@@ -3336,12 +3336,12 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
     const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
-    const float* __restrict__ bound, const Q8Rows r8, uint32_t* __restrict__ stats,
-    uint64_t* __restrict__ clk) {
+    const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from,
+    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
-  __shared__ uint16_t owner[kSelChunk];
+  __shared__ uint16_t owner[2 * kSelChunk];  // (r05) the first 4096 slabs' lists
   __shared__ uint32_t wtot[kSelThreads / 64];
   __shared__ uint32_t wscr[kSelThreads / 64][16];  // a wave's group of 16 rows
   __shared__ uint32_t fill, spill, rfill;
@@ -3473,16 +3473,16 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   pre[l0 + 1] = ex + c0;
   if (tid == 0) pre[2 * kSelThreads] = total;
   for (uint32_t j = 0; j < c0; ++j)
-    if (ex + j < kSelChunk) owner[ex + j] = (uint16_t)l0;
+    if (ex + j < 2 * kSelChunk) owner[ex + j] = (uint16_t)l0;
   for (uint32_t j = 0; j < c1; ++j)
-    if (ex + c0 + j < kSelChunk) owner[ex + c0 + j] = (uint16_t)(l0 + 1);
+    if (ex + c0 + j < 2 * kSelChunk) owner[ex + c0 + j] = (uint16_t)(l0 + 1);
   __syncthreads();
   const uint32_t T = total;
   auto slab_at = [&](uint32_t l, uint32_t j) -> size_t {
     return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub + j;
   };
   auto list_of = [&](uint32_t i) -> uint32_t {
-    if (i < kSelChunk) return owner[i];
+    if (i < 2 * kSelChunk) return owner[i];
     uint32_t lo = 0, hi = 2 * kSelThreads;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -3491,12 +3491,15 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     return lo;
   };
   // the passing quarters' slabs: rows whose upper bound (the tile's m) reaches Tcut
-  for (uint32_t base = 0; base < (slow ? 0u : T); base += kSelChunk) {
-    i32x4_t v[kSelHeld][2];
-    uint32_t tl[kSelHeld], ls[kSelHeld];
-    bool ok[kSelHeld];
+  // (r05: 8 slabs held per thread, so a query's ~3.5k (10M, k = 10) to ~17k
+  // (C5, k = 50) slabs take half the dependent slab -> meta round trips)
+  constexpr int kQ8Held = 2 * kSelHeld;
+  for (uint32_t base = 0; base < (slow ? 0u : T); base += kQ8Held * kSelThreads) {
+    i32x4_t v[kQ8Held][2];
+    uint32_t tl[kQ8Held], ls[kQ8Held];
+    bool ok[kQ8Held];
 #pragma unroll
-    for (int u = 0; u < kSelHeld; ++u) {
+    for (int u = 0; u < kQ8Held; ++u) {
       const uint32_t i = base + tid + (uint32_t)u * kSelThreads;
       ok[u] = i < T;
       const uint32_t l = ok[u] ? list_of(i) : 0u;
@@ -3507,7 +3510,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       tl[u] = ok[u] ? tiles[e] : row_base;
     }
 #pragma unroll
-    for (int u = 0; u < kSelHeld; ++u) {
+    for (int u = 0; u < kQ8Held; ++u) {
       const uint32_t lt = (tl[u] - row_base) >> 5;
       const float dt = meta[2 * (size_t)lt], nt = meta[2 * (size_t)lt + 1];
       const float mt = pa * dt + (pc + sig) * nt;
@@ -3594,7 +3597,26 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   // wave takes 64 entries at a time and runs the passing ones in groups of
   // 16 (ballot ranks place them in its wscr row), one slot reservation per
   // group.
+  // (r05) A wave packs its passing entries across its 64-entry slices into
+  // full groups of 16 (wscr[w][0, pend) carries a partial group from slice
+  // to slice): a sparse pass (round 1 picks ~k of thousands) runs a group per
+  // wave instead of a near-empty group per slice.
+  auto run_group = [&](uint32_t cnt16) {
+    const uint32_t r = wscr[w][(uint32_t)col < cnt16 ? col : 0];
+    const f32x4_t acc = score16(r);
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(&rfill, cnt16);
+    slot = (uint32_t)__shfl((int)slot, 0, 64);
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const uint32_t j = 4 * (uint32_t)kq + (uint32_t)ii;
+      const uint32_t rj = (uint32_t)__shfl((int)r, (int)j, 64);  // lane j (kq = 0) has row j
+      if (col == 0 && j < cnt16) res[slot + j] = make_key(acc[ii], row_base + rj);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
   auto rescore_n = [&](uint32_t nb, auto pred) {
+    uint32_t pend = 0;  // rows waiting in wscr[w][0, pend) (wave-uniform)
     for (uint32_t base = w * 64; base < nb; base += kSelThreads) {
       const uint32_t i = base + lane;
       const uint64_t e = i < nb ? buf[i] : 0ull;
@@ -3602,24 +3624,19 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       const uint64_t bal = __ballot(pass);
       const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       const uint32_t total = (uint32_t)__popcll(bal);
-      for (uint32_t g0 = 0; g0 < total; g0 += 16) {
-        if (pass && rank >= g0 && rank < g0 + 16) wscr[w][rank - g0] = (uint32_t)e;
+      for (uint32_t done = 0; done < total;) {
+        const uint32_t take = 16 - pend < total - done ? 16 - pend : total - done;
+        if (pass && rank >= done && rank < done + take) wscr[w][pend + rank - done] = (uint32_t)e;
         __builtin_amdgcn_wave_barrier();
-        const uint32_t cnt16 = total - g0 < 16 ? total - g0 : 16;
-        const uint32_t r = wscr[w][(uint32_t)col < cnt16 ? col : 0];
-        const f32x4_t acc = score16(r);
-        uint32_t slot = 0;
-        if (lane == 0) slot = atomicAdd(&rfill, cnt16);
-        slot = (uint32_t)__shfl((int)slot, 0, 64);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const uint32_t j = 4 * (uint32_t)kq + (uint32_t)ii;
-          const uint32_t rj = (uint32_t)__shfl((int)r, (int)j, 64);  // lane j (kq = 0) has row j
-          if (col == 0 && j < cnt16) res[slot + j] = make_key(acc[ii], row_base + rj);
+        pend += take;
+        done += take;
+        if (pend == 16) {
+          run_group(16);
+          pend = 0;
         }
-        __builtin_amdgcn_wave_barrier();
       }
     }
+    if (pend) run_group(pend);
   };
   auto rescore_where = [&](auto pred) { rescore_n(ns, pred); };
   // (r05) Slow path -- a passing lossy quarter (the pass dropped slabs: its
@@ -3735,7 +3752,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     tick(4);
     return;
   }
-  if (ns > k + 64) {
+  if (ns > k + 64 && ns >= two_from) {
     // Two rounds (r04; r05: radix floors for every k): the survivors whose U
     // image reaches P1 (the floor of the bucket of the k-th largest U: at
     // least k of them) first; P2, the floor of the k-th best exact score
@@ -3803,6 +3820,13 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
   mfma_grid(n_rows, &gwg, &rpw);
   if (gwg != nwg) return hipErrorInvalidValue;  // the pass's static split
   const Q8Rows r8{(const int8_t*)X8, (const int8_t*)Q8, allow, n_rows, rpw, row_base};
+  // VS_Q8_TWO_ROUND_FROM (read once): the survivor count from which the
+  // select rescores in two rounds (the top k by U first, then only survivors
+  // whose U reaches their k-th exact score); below it, one round
+  static const uint32_t two_from = [] {
+    const char* e = getenv("VS_Q8_TWO_ROUND_FROM");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   static const int sv = [] {
     const char* e = getenv("VS_Q8_SEL_SV");
     return e ? atoi(e) : 0;
@@ -3819,7 +3843,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
                      cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
-                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, stats, clk);
+                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, stats, clk);
   return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@
 // survivors, rescore, end; medians over the queries, us).
 //   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/share_pipe.hip -o tools/share_pipe \
 //     -I<pkg>/csrc -L<pkg>/lib -lvsearch -Wl,-rpath,<pkg>/lib
-//   share_pipe [ROWS=1250000] [K=10] [REPS=200] [DIM=768]
+//   share_pipe [ROWS=1250000] [K=10] [REPS=200] [DIM=768] [NQ=256 / 128 above 768-d]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,7 +39,8 @@ int main(int argc, char** argv) {
   const uint32_t k = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 10;
   const int reps = argc > 3 ? std::atoi(argv[3]) : 200;
   const uint32_t dim = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 768;
-  const uint32_t nq = 256, PS = 256;
+  // queries per batch: one int8 launch's worth (256 up to 768-d, 128 above)
+  const uint32_t nq = argc > 5 ? (uint32_t)std::atoi(argv[5]) : (dim <= 768 ? 256u : 128u), PS = 256;
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   uint16_t *X, *qb;
@@ -66,7 +67,8 @@ int main(int argc, char** argv) {
   const uint32_t maxl = vsk::mfma_max_lists(n);
   const uint32_t st0 = vsk::mfma_sample_tiles(n, dim, false);
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n);
-  const double f = k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0;
+  const char* fe = std::getenv("VS_Q8_SAMPLE");  // as vs_engine.cpp: the sample factor override
+  const double f = fe && std::atof(fe) > 0 ? std::atof(fe) : (k <= 16 ? 1.0 : k <= 64 ? 2.0 : 4.0);
   const uint32_t stl = (uint32_t)std::max(1.0, std::min({(double)vsk::kMfmaMaxSampleTiles, (double)tpw,
                                                           st0 * f}));
   const uint32_t cap = vsk::mfma_cand_cap(n, k, stl);
@@ -129,8 +131,8 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  std::printf("{\"rows\": %u, \"k\": %u, \"dim\": %u, \"reps\": %d, \"sample_tiles\": %u, \"cap8\": %u, "
-              "\"gate\": %u", n, k, dim, reps, stl, cap8, hg);
+  std::printf("{\"rows\": %u, \"k\": %u, \"dim\": %u, \"nq\": %u, \"reps\": %d, \"sample_tiles\": %u, "
+              "\"cap8\": %u, \"gate\": %u", n, k, dim, nq, reps, stl, cap8, hg);
   // arms interleaved over rounds (clock drift spreads evenly); medians
   const int rounds = 5;
   std::vector<std::vector<float>> t(arms.size());
