@@ -469,6 +469,10 @@ def main():
                 sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True,
                                                                  ring=ring)
                 sharded.world_size = world
+                # the exchange of batch i overlaps the search of batch i + 1 on a
+                # stream of its own (VS_EXCHANGE_OVERLAP=0: on the search stream)
+                if os.environ.get("VS_EXCHANGE_OVERLAP", "1") != "0":
+                    sharded.exchange_stream = torch.cuda.Stream()
             else:
                 log("[bench] torch.distributed exchange instead of the engine communicator")
                 collective = "torch"
@@ -503,6 +507,7 @@ def main():
         "config": {"workload": desc, "corpus_rows": n_full, "dim": dim, "batch": batch, "k": k,
                    "metric": metric, "parallelism": f"row-shard x{world}",
                    "rows_per_gpu": hi - lo, "collective": collective,
+                   "exchange_overlapped": sharded.exchange_stream is not None,
                    "int8_prefilter": int8, "int8_single_query": q8_b1,
                    "build_id": pkg.build_id()},
         "roofline": roof,

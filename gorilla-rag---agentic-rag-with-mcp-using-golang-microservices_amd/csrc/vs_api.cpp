@@ -137,6 +137,14 @@ struct vs_engine {
   ncclComm_t pcomm = nullptr;
   uint32_t pranks = 0, prank = 0;
   DevBuf pgather;
+  // (r05) the exchange's own stream order: vs_gather_merge_keys touches only
+  // pgather (and, for k <= kMaxK, a scratch-free merge), so it orders itself
+  // after the previous exchange (gm_ev on gm_stream) instead of joining the
+  // primary context's search stream -- an exchange on a side stream then
+  // overlaps the next batch's search
+  std::mutex gm_mu;
+  hipStream_t gm_stream = nullptr;
+  hipEvent_t gm_ev = nullptr;
   uint32_t shards() const { return (uint32_t)shard_dev.size(); }
 };
 
@@ -950,7 +958,9 @@ void destroy(vs_engine* E) {
   if (!E->dev.empty() && E->dev[0]) {
     (void)hipSetDevice(E->dev[0]->device);
     (void)hipStreamSynchronize(E->dev[0]->stream);
+    if (E->gm_ev) (void)hipEventSynchronize(E->gm_ev);  // the last exchange read pgather
     E->pgather.release();
+    if (E->gm_ev) (void)hipEventDestroy(E->gm_ev);
     if (E->pcomm) (void)ncclCommDestroy(E->pcomm);
   }
   E->colls.clear();
@@ -1324,12 +1334,31 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
   if (nq == 0) return VS_OK;
   if (!d_local || !d_out_keys) return fail(VS_ERR_INVALID_ARG, "NULL device pointer");
   DevEngine* d0 = eng->dev[0];
-  std::lock_guard<std::mutex> g(d0->work_mu);
-  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
   hipStream_t cs = (hipStream_t)stream;
-  // the gather buffer is reused: order this call after the last one that read it
-  VS_HIP(vsd::use_stream(d0, cs), "stream order");
   const size_t lbytes = (size_t)nq * k_in * 8;
+  if (k > vsk::kMaxK || k_in > vsk::kMaxK) {
+    // the large-k merge uses the primary context's scratch: its stream order
+    std::lock_guard<std::mutex> g(d0->work_mu);
+    VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+    VS_HIP(vsd::use_stream(d0, cs), "stream order");
+    if (eng->pgather.bytes < lbytes * eng->pranks) {
+      VS_HIP(hipStreamSynchronize(cs), "sync");
+      VS_HIP(eng->pgather.ensure(lbytes * eng->pranks), "alloc gathered keys");
+    }
+    const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
+                                         eng->pcomm, cs);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
+    return vsd::merge_any(d0, eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in,
+                          nq, k_in, k, d_out_keys);
+  }
+  std::lock_guard<std::mutex> g(eng->gm_mu);
+  VS_HIP(vsd::set_dev(d0), "hipSetDevice");
+  if (!eng->gm_ev) VS_HIP(hipEventCreateWithFlags(&eng->gm_ev, hipEventDisableTiming), "event");
+  // the gather buffer is reused: this exchange runs after the previous one
+  // (gm_ev: recorded after every exchange, on its stream)
+  if (eng->gm_stream && eng->gm_stream != cs)
+    VS_HIP(hipStreamWaitEvent(cs, eng->gm_ev, 0), "stream order");
+  eng->gm_stream = cs;
   if (eng->pgather.bytes < lbytes * eng->pranks) {
     VS_HIP(hipStreamSynchronize(cs), "sync");
     VS_HIP(eng->pgather.ensure(lbytes * eng->pranks), "alloc gathered keys");
@@ -1337,8 +1366,11 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
   const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
                                        eng->pcomm, cs);
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-  return vsd::merge_any(d0, eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in,
-                        nq, k_in, k, d_out_keys);
+  VS_HIP(vsk::launch_merge(eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in, nq,
+                           k_in, k, d_out_keys, cs),
+         "merge");
+  VS_HIP(hipEventRecord(eng->gm_ev, cs), "stream order");
+  return VS_OK;
 }
 
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,

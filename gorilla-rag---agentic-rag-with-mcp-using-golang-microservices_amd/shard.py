@@ -51,7 +51,14 @@ class ShardedSearch:
     # merge (engine_gather_merge); replaces the torch all-gather and `merge`
     gather_merge: Optional[Callable] = None
     world_size: int = 1  # ranks of gather_merge's communicator
+    # (r05) a torch.cuda.Stream for gather_merge: each batch's all-gather +
+    # merge then runs on it, after an event on the search's stream, and the
+    # next batch's search does not wait for it (the engine orders exchanges
+    # among themselves only: vs_gather_merge_keys). The returned keys are
+    # ready once that stream is (a device synchronize covers both).
+    exchange_stream: Optional[object] = None
     _gather_bufs: Optional[dict] = None  # all-gather outputs, reused per shape
+    _ev: Optional[object] = None
 
     def search(self, queries, k: int):
         import torch
@@ -61,7 +68,14 @@ class ShardedSearch:
         if self.gather_merge is not None:
             if self.world_size == 1 and not self.always_gather:
                 return local
-            return self.gather_merge(local, k)
+            if self.exchange_stream is None:
+                return self.gather_merge(local, k)
+            if self._ev is None:
+                self._ev = torch.cuda.Event()
+            self._ev.record()  # the local keys, on the search's stream
+            self.exchange_stream.wait_event(self._ev)
+            with torch.cuda.stream(self.exchange_stream):
+                return self.gather_merge(local, k)
         if not dist.is_available() or not dist.is_initialized():
             return local
         if dist.get_world_size(self.group) == 1 and not self.always_gather:
