@@ -469,9 +469,12 @@ def main():
                 sharded.gather_merge = shard.engine_gather_merge(eng, stream_fn, reuse=True,
                                                                  ring=ring)
                 sharded.world_size = world
-                # the exchange of batch i overlaps the search of batch i + 1 on a
-                # stream of its own (VS_EXCHANGE_OVERLAP=0: on the search stream)
-                if os.environ.get("VS_EXCHANGE_OVERLAP", "1") != "0":
+                # VS_EXCHANGE_OVERLAP=1: batch i's exchange on a stream of its own,
+                # overlapping batch i + 1's search. Off by default: at the 1.25M
+                # share it measured slower than the search stream (0.329 vs
+                # 0.322 ms/step, profiles/r05_exchange_overlap.jsonl) -- the
+                # RCCL and merge workgroups hold CUs the next sample pass needs
+                if os.environ.get("VS_EXCHANGE_OVERLAP", "0") == "1":
                     sharded.exchange_stream = torch.cuda.Stream()
             else:
                 log("[bench] torch.distributed exchange instead of the engine communicator")

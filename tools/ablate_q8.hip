@@ -10,6 +10,8 @@
 //   mfma     the same in MODE 4: MFMAs (16x16x32 bf16, 16 cycles each: the
 //            int8 pass's count and cycles) + LDS reads + barriers, no stream
 //   mfma-nb  MODE 5: MODE 4 without barriers
+//   pd2/pd3  VAR 32 / 64: A fragments 2 / 3 steps ahead
+//   stag     VAR 1048576: waves 4-7 half a chunk ahead of their SIMD partners
 //   pair     VAR 33554432: one barrier per pair of tiles (vs_kernels.hip)
 //   epipipe  VAR 67108864: each tile's epilogue deferred into the next tile
 //   pair+epi both
@@ -20,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <string>
 #include <cstdlib>
 #include <vector>
 
@@ -119,10 +122,20 @@ int main(int argc, char** argv) {
       {"stream", run<384, 2, 2304, false>, {}},
       {"mfma", run<384, 4, 2304, false>, {}},
       {"mfma-nb", run<384, 5, 2304, false>, {}},
+      {"pd2", run<768, 0, 2304 + 32, true>, {}},
+      {"pd3", run<768, 0, 2304 + 64, true>, {}},
+      {"stag", run<768, 0, 2304 + 1048576, true>, {}},
       {"pair", run<768, 0, 2304 + 33554432, true>, {}},
       {"epipipe", run<768, 0, 2304 + 67108864, true>, {}},
       {"pair+epi", run<768, 0, 2304 + 33554432 + 67108864, true>, {}},
   };
+  // "prod" as the 4th argument: the product arm alone (PMC passes), R x B launches
+  if (argc > 4 && std::string(argv[4]) == "prod") {
+    for (int r = 0; r < reps; ++r) arms[0].t.push_back(arms[0].fn(c));
+    std::sort(arms[0].t.begin(), arms[0].t.end());
+    printf("{\"rows\": %u, \"prod_ms\": %.4f}\n", n, arms[0].t[arms[0].t.size() / 2]);
+    return 0;
+  }
   for (auto& arm : arms) arm.fn(c);  // warm every arm once
   for (int r = 0; r < reps; ++r)
     for (size_t i = 0; i < arms.size(); ++i) {
@@ -135,6 +148,53 @@ int main(int argc, char** argv) {
     std::sort(arm.t.begin(), arm.t.end());
     const double ms = arm.t[arm.t.size() / 2];
     printf(", \"%s_ms\": %.4f, \"%s_hbm_frac\": %.4f", arm.name, ms, arm.name, bytes / (ms * 1e-3) / 8e12);
+  }
+  // the sample pass (MODE 3, bf16 rows) at 1, 2, 4, 8 tiles per workgroup
+  // (the N = 8 share uses 4), timed in bursts, and one launch with the
+  // per-workgroup clocks (VAR 8192: start, prologue done, tiles done, end)
+  {
+    MfArgs sa{};
+    sa.X = X, sa.Q = Q, sa.tmax = tmax, sa.n_rows = n, sa.rows_per_wg = rpw;
+    sa.nq_valid = 256, sa.k = k;
+    const uint32_t sts[4] = {1, 2, 4, 8};
+    for (uint32_t st2 : sts) {
+      if (st2 > st && st2 > 4) break;  // tmax holds nwg * st tiles per query
+      sa.max_tiles = st2;
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        hipEventRecord(c.a, 0);
+        for (int i = 0; i < burst; ++i)
+          hipLaunchKernelGGL((mfma_topk_kernel<768, 3, 2304, 2, false, false>), dim3(c.nwg), dim3(512), 0, 0,
+                             sa);
+        hipEventRecord(c.b, 0);
+        hipEventSynchronize(c.b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, c.a, c.b);
+        ts.push_back(ms / burst);
+      }
+      std::sort(ts.begin(), ts.end());
+      printf(", \"sample_st%u_us\": %.2f", st2, ts[ts.size() / 2] * 1e3);
+    }
+    uint64_t* clkb;
+    CK(hipMalloc(&clkb, (size_t)c.nwg * 4 * 8));
+    sa.max_tiles = 4 < st ? 4 : st;
+    sa.lists = clkb;
+    for (int i = 0; i < 3; ++i)
+      hipLaunchKernelGGL((mfma_topk_kernel<768, 3, 2304 + 8192, 2, false, false>), dim3(c.nwg), dim3(512), 0, 0,
+                         sa);
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> h((size_t)c.nwg * 4);
+    CK(hipMemcpy(h.data(), clkb, h.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (uint32_t b = 0; b < c.nwg; ++b) t0 = std::min(t0, h[4 * b]);
+    const char* nm[4] = {"start", "prologue", "tiles", "end"};
+    for (int j = 0; j < 4; ++j) {
+      std::vector<double> v;
+      for (uint32_t b = 0; b < c.nwg; ++b) v.push_back((h[4 * b + j] - t0) * 0.01);
+      std::sort(v.begin(), v.end());
+      printf(", \"sample_clk_%s_us_med\": %.2f, \"sample_clk_%s_us_max\": %.2f", nm[j], v[v.size() / 2], nm[j],
+             v.back());
+    }
   }
   // the product variants must append the same slabs: counts and quarter
   // maxima equal to the product's, element for element

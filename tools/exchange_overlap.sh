@@ -3,7 +3,7 @@
 # the N = 8 share (1.25M rows) plain, and with the RCCL all-gather + merge
 # forced at world size 1 (VS_BENCH_FORCE_DIST=1, nccl, the engine's
 # communicator) on the search stream (VS_EXCHANGE_OVERLAP=0) and on a stream
-# of its own (the default: batch i's exchange overlaps batch i + 1's search).
+# of its own (VS_EXCHANGE_OVERLAP=1, off by default since r05: batch i's exchange overlaps batch i + 1's search).
 # Each arm twice, interleaved. One JSON line per run in gpurun_out/xo_<arm>.jsonl.
 #   bash tools/exchange_overlap.sh [ROWS]
 set -u
