@@ -2050,21 +2050,25 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // lgkmcnt(0), before a chunk's first MFMAs). Drained before the exit.
   constexpr bool kBF = (((VAR & 524288) != 0) != (MODE == 0 || MODE == 3 || MODE == 8)) && !kSpread;
   const unsigned char* const xsafe = (const unsigned char*)a.X + (size_t)wr0 * RBY;
-  auto issue_next_bf = [&](bool real) {
+  auto bf_src = [&](bool real) -> const unsigned char* {
     // wave-uniform by construction; readfirstlane keeps it in SGPRs for the
     // asm's "s" operand whatever the divergence analysis concludes
     const uint64_t sp = (uint64_t)(uintptr_t)(real ? xnext : xsafe);
-    const unsigned char* src = (const unsigned char*)(uintptr_t)(
+    return (const unsigned char*)(uintptr_t)(
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sp >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp));
+  };
+  auto bf_piece = [&](const unsigned char* src, int i) {
+    const int b = w + WAVES * i;
+    const int s4l = b >> 2, rg = b & 3;
+    glds16<kNtDma>(src, loff[i],
+                   (uint32_t)__builtin_amdgcn_readfirstlane(
+                       (int)(lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024))));
+  };
+  auto issue_next_bf = [&](bool real) {
+    const unsigned char* src = bf_src(real);
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int b = w + WAVES * i;
-      const int s4l = b >> 2, rg = b & 3;
-      glds16<kNtDma>(src, loff[i],
-                     (uint32_t)__builtin_amdgcn_readfirstlane(
-                         (int)(lds_base + snext + (uint32_t)((s4l * 4 + rg) * 1024))));
-    }
+    for (int i = 0; i < PPW; ++i) bf_piece(src, i);
     advance();
   };
   // VAR 8388608 (r04): the ring's first AHEAD chunks are issued before the
@@ -2083,6 +2087,15 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   constexpr bool kPair = (VAR & 33554432) != 0 && kBF && S::CPT == 1 && S::NSLOT == 6 &&
                          (VAR & 1048576) == 0 && kDma;
   constexpr uint32_t kFill = kPair ? (uint32_t)S::AHEAD - 1 : (uint32_t)S::AHEAD;
+  // VAR 16384 (r05, ablation): the branch-free stream's pieces of a chunk
+  // spread over its steps -- piece 0 after the barrier, piece i after step
+  // i * CT / PPW -- instead of all PPW back to back after the barrier, where
+  // both waves of a SIMD issue theirs while the matrix pipe waits. Same
+  // slots and waits: every piece of chunk c + AHEAD is issued before the
+  // next chunk's vmcnt wait counts them.
+  constexpr bool kBFSpread = (VAR & 16384) != 0 && kBF && !kPair && (VAR & 1048576) == 0 && kDma &&
+                             PPW > 1 && S::CT >= PPW;
+  const unsigned char* bf_cur = xsafe;  // (kBFSpread) the chunk being issued
   if constexpr (kDma && kBF && kEarlyFill) {
 #pragma unroll
     for (uint32_t c = 0; c < kFill; ++c) issue_next_bf(c < nchunks);
@@ -2221,9 +2234,14 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
 #pragma unroll
       for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
       if (!full || a.allow) {  // uniform: unfiltered full tiles skip it
+        // the row base and mask bits are taken opaque inside the branch: the
+        // compiler otherwise hoists their 16 adds/ands into every unfiltered
+        // full tile (r05 ISA: 17 of the epilogue's 38 VALU per tile)
+        uint32_t rb = trow0 + 4 * kq, amv = am;
+        asm volatile("" : "+v"(rb), "+v"(amv));
 #pragma unroll
         for (int b = 0; b < 8; ++b)
-          if (trow0 + 16 * (b >> 2) + 4 * kq + (b & 3) >= wr1 || !((am >> b) & 1u)) v[b] = INT_MIN;
+          if (rb + 16 * (b >> 2) + (b & 3) >= wr1 || !((amv >> b) & 1u)) v[b] = INT_MIN;
         ac[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
         ac[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
       }
@@ -2259,6 +2277,20 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   f32x4_t accq[kEpiPipe ? 2 : 1][2][G];
   uint32_t prow0 = 0;
   bool pfull = true, have_prev = false;
+  // VAR 32768 (r05, ablation): a tile's first PD A-fragment reads are issued
+  // at the end of the previous tile, before its epilogue (the next tile's
+  // first chunk was published by the barrier at the head of this tile's last
+  // chunk), so their LDS latency overlaps the epilogue instead of opening
+  // the next tile after its barrier
+  constexpr bool kPreA = (VAR & 32768) != 0 && MODE != 2 && MODE != 7 && !kStag;
+  constexpr int kAH = MODE == 10 || MODE == 13 ? 1 : 2;
+  bf16x8_t afr_k[NB][2];
+  auto read_first = [&]() {
+#pragma unroll
+    for (int p = 0; p < kPD; ++p)
+#pragma unroll
+      for (int hr = 0; hr < kAH; ++hr) afr_k[p][hr] = lds_a(smem + scur, p, hr);
+  };
   auto tile = [&](uint32_t t, auto full_tag, auto stag_tag, auto set_tag) {
     constexpr bool STAG = decltype(stag_tag)::value;
     constexpr int SET = decltype(set_tag)::value;
@@ -2268,7 +2300,8 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     for (int hr = 0; hr < 2; ++hr)
 #pragma unroll
       for (int g = 0; g < G; ++g) acc[hr][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    bf16x8_t afr[NB][2];
+    bf16x8_t afr_l[NB][2];
+    bf16x8_t(&afr)[NB][2] = *(kPreA ? &afr_k : &afr_l);
 #pragma unroll
     for (int u = 0; u < S::CPT; ++u) {
       const uint32_t c = t * S::CPT + u;
@@ -2276,7 +2309,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
           scur + S::CHUNK_BYTES == (uint32_t)(S::NSLOT * S::CHUNK_BYTES) ? 0 : scur + S::CHUNK_BYTES;
       const unsigned char* sb = smem + scur;
       const unsigned char* sbn = smem + snxt;
-      if (MODE != 2 && u == 0) {
+      if (MODE != 2 && u == 0 && !kPreA) {
 #pragma unroll
         for (int p = 0; p < kPD; ++p)
 #pragma unroll
@@ -2305,6 +2338,9 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
         if constexpr (kPair) {
           issue_next_bf(c + 4 < nchunks);
           issue_next_bf(c + 5 < nchunks);
+        } else if constexpr (kBFSpread) {
+          bf_cur = bf_src(refill);
+          bf_piece(bf_cur, 0);
         } else if constexpr (kDma && kBF) {
           issue_next_bf(refill);
         } else if (!kSpread && refill) {
@@ -2383,6 +2419,14 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
               __builtin_amdgcn_sched_barrier(0);
             }
           }
+          if constexpr (kBFSpread) {
+#pragma unroll
+            for (int i = 1; i < PPW; ++i)
+              if (s == (i * S::CT) / PPW) {
+                bf_piece(bf_cur, i);
+                if (i == PPW - 1) advance();
+              }
+          }
           if constexpr (kSpread) {
             // piece i after step i * CT / PPW (the last one also advances)
 #pragma unroll
@@ -2396,6 +2440,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       }
       scur = snxt;
     }
+    if constexpr (kPreA) read_first();  // the next tile's (past the last: unused)
     if constexpr (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 7 || MODE == 10 ||
                   MODE == 11 || MODE == 13) {
 #pragma unroll
@@ -2562,6 +2607,7 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       }
     }
   };
+  if constexpr (kPreA) read_first();  // tile 0's (chunk 0 published above)
   uint32_t nfull = (wr1 - wr0) / 32;
   if (nfull > ntiles) nfull = ntiles;
   // (kEpiPipe) tiles alternate between the two accumulator sets

@@ -10,13 +10,17 @@
 //   mfma     the same in MODE 4: MFMAs (16x16x32 bf16, 16 cycles each: the
 //            int8 pass's count and cycles) + LDS reads + barriers, no stream
 //   mfma-nb  MODE 5: MODE 4 without barriers
-//   pd2/pd3  VAR 32 / 64: A fragments 2 / 3 steps ahead
-//   stag     VAR 1048576: waves 4-7 half a chunk ahead of their SIMD partners
 //   pair     VAR 33554432: one barrier per pair of tiles (vs_kernels.hip)
 //   epipipe  VAR 67108864: each tile's epilogue deferred into the next tile
-//   pair+epi both
+//   spread   VAR 16384: a chunk's DMA pieces spread over its steps
+//   stream-spread  the stream skeleton with them spread
+//   prea     VAR 32768: a tile's first A-fragment reads before the previous
+//            tile's epilogue (prea+spread both; mfma-prea: the MFMA skeleton)
+// (r05 records of the dropped arms -- pd2/pd3: A fragments 2 / 3 steps
+// ahead, stag: waves 4-7 half a chunk ahead, pair+epi -- all slower than
+// prod: profiles/r05_ablate_q8*.json)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/ablate_q8.hip -o tools/ablate_q8
-//   ablate_q8 [ROWS=10000000] [REPS=5] [BURST=20]
+//   ablate_q8 [ROWS=10000000] [REPS=5] [BURST=20] [ARM: that arm alone]
 #include "../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/csrc/vs_kernels.hip"
 #include "../gorilla-rag---agentic-rag-with-mcp-using-golang-microservices_amd/csrc/vs_q8.hip"
 
@@ -122,19 +126,25 @@ int main(int argc, char** argv) {
       {"stream", run<384, 2, 2304, false>, {}},
       {"mfma", run<384, 4, 2304, false>, {}},
       {"mfma-nb", run<384, 5, 2304, false>, {}},
-      {"pd2", run<768, 0, 2304 + 32, true>, {}},
-      {"pd3", run<768, 0, 2304 + 64, true>, {}},
-      {"stag", run<768, 0, 2304 + 1048576, true>, {}},
       {"pair", run<768, 0, 2304 + 33554432, true>, {}},
       {"epipipe", run<768, 0, 2304 + 67108864, true>, {}},
-      {"pair+epi", run<768, 0, 2304 + 33554432 + 67108864, true>, {}},
+      {"spread", run<768, 0, 2304 + 16384, true>, {}},
+      {"stream-spread", run<384, 2, 2304 + 16384, false>, {}},
+      {"prea", run<768, 0, 2304 + 32768, true>, {}},
+      {"prea+spread", run<768, 0, 2304 + 32768 + 16384, true>, {}},
+      {"mfma-prea", run<384, 4, 2304 + 32768, false>, {}},
   };
-  // "prod" as the 4th argument: the product arm alone (PMC passes), R x B launches
-  if (argc > 4 && std::string(argv[4]) == "prod") {
-    for (int r = 0; r < reps; ++r) arms[0].t.push_back(arms[0].fn(c));
-    std::sort(arms[0].t.begin(), arms[0].t.end());
-    printf("{\"rows\": %u, \"prod_ms\": %.4f}\n", n, arms[0].t[arms[0].t.size() / 2]);
-    return 0;
+  // an arm's name as the 4th argument: that arm alone (PMC passes), R x B launches
+  if (argc > 4) {
+    for (auto& arm : arms) {
+      if (std::string(argv[4]) != arm.name) continue;
+      for (int r = 0; r < reps; ++r) arm.t.push_back(arm.fn(c));
+      std::sort(arm.t.begin(), arm.t.end());
+      printf("{\"rows\": %u, \"%s_ms\": %.4f}\n", n, arm.name, arm.t[arm.t.size() / 2]);
+      return 0;
+    }
+    printf("no arm %s\n", argv[4]);
+    return 1;
   }
   for (auto& arm : arms) arm.fn(c);  // warm every arm once
   for (int r = 0; r < reps; ++r)
@@ -174,6 +184,22 @@ int main(int argc, char** argv) {
       }
       std::sort(ts.begin(), ts.end());
       printf(", \"sample_st%u_us\": %.2f", st2, ts[ts.size() / 2] * 1e3);
+      // VAR 8388608: the ring's first chunks issued before the query-fragment
+      // prologue (its latency then overlaps the ~5.5 us of fragment loads)
+      ts.clear();
+      for (int r = 0; r < reps; ++r) {
+        hipEventRecord(c.a, 0);
+        for (int i = 0; i < burst; ++i)
+          hipLaunchKernelGGL((mfma_topk_kernel<768, 3, 2304 + 8388608, 2, false, false>), dim3(c.nwg), dim3(512),
+                             0, 0, sa);
+        hipEventRecord(c.b, 0);
+        hipEventSynchronize(c.b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, c.a, c.b);
+        ts.push_back(ms / burst);
+      }
+      std::sort(ts.begin(), ts.end());
+      printf(", \"sample_early_st%u_us\": %.2f", st2, ts[ts.size() / 2] * 1e3);
     }
     uint64_t* clkb;
     CK(hipMalloc(&clkb, (size_t)c.nwg * 4 * 8));
@@ -211,10 +237,10 @@ int main(int argc, char** argv) {
   };
   std::vector<uint32_t> ref, got;
   if (snap(run<768, 0, 2304, true>, ref)) return 1;
-  const char* vnames[3] = {"pair", "epipipe", "pair+epi"};
-  float (*vfns[3])(const Ctx&) = {run<768, 0, 2304 + 33554432, true>, run<768, 0, 2304 + 67108864, true>,
-                                  run<768, 0, 2304 + 33554432 + 67108864, true>};
-  for (int v = 0; v < 3; ++v) {
+  const char* vnames[4] = {"pair", "epipipe", "spread", "prea+spread"};
+  float (*vfns[4])(const Ctx&) = {run<768, 0, 2304 + 33554432, true>, run<768, 0, 2304 + 67108864, true>,
+                                  run<768, 0, 2304 + 16384, true>, run<768, 0, 2304 + 32768 + 16384, true>};
+  for (int v = 0; v < 4; ++v) {
     if (snap(vfns[v], got)) return 1;
     size_t diff = 0;
     for (size_t i = 0; i < ref.size(); ++i) diff += ref[i] != got[i];
