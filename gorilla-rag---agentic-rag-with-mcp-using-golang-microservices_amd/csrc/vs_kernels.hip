@@ -2049,7 +2049,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // let hipcc's waitcnt pass keep the fragment reads' order: lgkmcnt(2), not
   // lgkmcnt(0), before a chunk's first MFMAs). Drained before the exit.
   constexpr bool kBF = (((VAR & 524288) != 0) != (MODE == 0 || MODE == 3 || MODE == 8)) && !kSpread;
-  const unsigned char* const xsafe = (const unsigned char*)a.X + (size_t)wr0 * RBY;
+  // The dummy pieces past the last chunk all read the pass's FIRST chunk (the
+  // same bytes for every workgroup: L2 hits after one miss per XCD). r05: each
+  // workgroup re-read its own first chunk, which the stream had long evicted:
+  // AHEAD x 24 KiB x 256 workgroups of HBM re-reads, +2.2% of the traffic at
+  // the N = 8 share (profiles/pmc_traffic.json c3_i8@1250000, build 67398432).
+  const unsigned char* const xsafe = (const unsigned char*)a.X;
   auto bf_src = [&](bool real) -> const unsigned char* {
     // wave-uniform by construction; readfirstlane keeps it in SGPRs for the
     // asm's "s" operand whatever the divergence analysis concludes
@@ -3382,7 +3387,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
     const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
-    const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from,
+    const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from, uint32_t opts,
     uint32_t* __restrict__ stats, uint64_t* __restrict__ clk) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
@@ -3486,10 +3491,12 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   buf[l0] = (uint64_t)y0 << 32;
   buf[l0 + 1] = (uint64_t)y1 << 32;
   const uint32_t nzq = (uint32_t)__syncthreads_count(y0 != 0) + (uint32_t)__syncthreads_count(y1 != 0);
-  const uint32_t P0 = nzq >= k ? kth_floor(buf, 2 * kSelThreads, k) : 0u;
+  // opts bit 0 (VS_Q8_SEL_P0=0, ablation): no quarter bound, the sample's alone
+  const uint32_t P0 = nzq >= k && !(opts & 1u) ? kth_floor(buf, 2 * kSelThreads, k) : 0u;
   const float tl_b = b == -INFINITY ? -INFINITY : b - sig * nmax;
   const float tl_l = P0 ? vs::ord_score(P0) : -INFINITY;
   const float Tcut = tl_b > tl_l ? tl_b : tl_l;
+  if (stats && tid == 0 && tl_l > tl_b) atomicAdd(stats + 3, 1u);  // (tools) the quarter bound won
   tick(1);
   if constexpr (SV == 1) return;
   // only quarters whose largest dot can reach Tcut hold survivors
@@ -3877,6 +3884,10 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
     const char* e = getenv("VS_Q8_SEL_SV");
     return e ? atoi(e) : 0;
   }();
+  static const uint32_t opts = [] {
+    const char* e = getenv("VS_Q8_SEL_P0");
+    return e && atoi(e) == 0 ? 1u : 0u;
+  }();
   decltype(&select_q8_kernel<768, 0, false>) kern;
   if (f32 && dim == 768)
     kern = select_q8_kernel<768, 0, true>;
@@ -3889,7 +3900,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
                      cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
-                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, stats, clk);
+                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, opts, stats, clk);
   return hipGetLastError();
 }
 

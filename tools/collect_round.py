@@ -87,7 +87,10 @@ def main():
         if os.path.exists(f):
             dst = os.path.join(P, f"{tag}_{cfg}_{bid}_pmc_fetch.csv")
             shutil.copy(f, dst)
-            key = cfg + ("_i8" if cfg == "c3" and "true" in kname else "")
+            if cfg == "c3":
+                key = cfg + ("_i8" if "true" in kname else "")
+            else:  # (r05) B = 1 runs the int8 copy's scan when the collection keeps one
+                key = cfg + ("_i8" if "gemv_q8_scan" in open(f).read() else "")
             fetch.append(f"{key}={dst}")
     if fetch:
         import subprocess

@@ -32,6 +32,9 @@ if [ "${PMC:-1}" = 1 ]; then
     -- python3 "$R/bench.py" $B --no-secondary > "$R/gpurun_out/${TAG}_pmc_fetch_c3.log" 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch_c3b1" -o run --output-format csv \
     -- python3 "$R/bench.py" $B --config c3b1 > "$R/gpurun_out/${TAG}_pmc_fetch_c3b1.log" 2>&1 || exit 1
+  # (r05) the int8 pass at the N = 8 share's size (rows_per_gpu 1.25M)
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch_c3_s125" -o run --output-format csv \
+    -- python3 "$R/bench.py" $B --no-secondary --rows 1250000 > "$R/gpurun_out/${TAG}_pmc_fetch_c3_s125.log" 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
     -d "$R/gpurun_out/${TAG}_pmc_mfma_c3" -o run --output-format csv \
     -- python3 "$R/bench.py" $B --no-secondary > "$R/gpurun_out/${TAG}_pmc_mfma_c3.log" 2>&1 || exit 1

@@ -20,6 +20,8 @@ SCAN = {"c3": "mfma_topk_kernel<768, 0, 2304, 2, false, false>",
         "c3_i8": "mfma_topk_kernel<768, 0, 2304, 2, false, true>",
         "c5b256_i8": "mfma_topk_kernel<1024, 0, 256, 1, false, true>",
         "c3b1": "gemv_topk_kernel<768, true, 1",
+        # (r05) one query on the int8 copy: its scan kernel
+        "c3b1_i8": "gemv_q8_scan_kernel<768, 1>", "c2_i8": "gemv_q8_scan_kernel<768, 1>",
         "c2": "gemv_topk_kernel<768, false, 1", "c4": "mfma_topk_kernel<768, 0,",
         "c4b1": "gemv_topk_kernel<768, true, 2", "c5b256": "mfma_topk_kernel<1024, 0,"}
 

@@ -151,8 +151,14 @@ int main(int argc, char** argv) {
     std::sort(t[i].begin(), t[i].end());
     std::printf(", \"%s_us\": %.2f", arms[i].name, t[i][rounds / 2]);
   }
-  // select stage clocks (wall_clock64: 100 MHz)
-  prep(), sample(), boundq8(), pass(), select(clk);
+  // select stage clocks (wall_clock64: 100 MHz) and counts (slabs read,
+  // survivors, slow-path queries, queries whose quarter bound beat the sample's)
+  uint32_t* stats;
+  CK(hipMalloc(&stats, 16));
+  CK(hipMemset(stats, 0, 16));
+  prep(), sample(), boundq8(), pass();
+  CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim, q8par,
+                           glob, meta, bound, X8, q8q, nullptr, n, st, stats, clk));
   CK(hipStreamSynchronize(st));
   std::vector<uint64_t> h((size_t)nq * 8);
   CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
@@ -168,6 +174,10 @@ int main(int argc, char** argv) {
       std::printf(", \"sel_%s_us_med\": %.2f, \"sel_%s_us_max\": %.2f", names[s], v[v.size() / 2], names[s],
                   v.back());
   }
+  uint32_t hs[4];
+  CK(hipMemcpy(hs, stats, 16, hipMemcpyDeviceToHost));
+  std::printf(", \"sel_slabs_per_query\": %.1f, \"sel_survivors_per_query\": %.1f, \"sel_slow_queries\": %u, "
+              "\"sel_quarter_bound_won\": %u", (double)hs[0] / nq, (double)hs[1] / nq, hs[2], hs[3]);
   std::printf("}\n");
   return 0;
 }

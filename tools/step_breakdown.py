@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-step stage split of a bench.py run from a rocprofv3 kernel trace.
 
-    python tools/step_breakdown.py RUN_kernel_trace.csv [--anchor NAME] [--last N] [--json]
+    python tools/step_breakdown.py RUN_kernel_trace.csv [--anchor NAME] [--last N] [--with NAME] [--json]
 
 A step is the span from one launch of the anchor kernel (default: the query
 preprocess, the first launch of every search) to the next one. For the last N
@@ -9,7 +9,12 @@ complete steps the tool reports, per kernel name, the mean duration and count
 per step, the idle time between consecutive kernels on the device (the gaps),
 and the step span; so "outside the main pass" = span - main pass is read off
 directly. Kernels of the CPU-side setup (generate,
-quantize) fall outside the steps and are ignored.
+quantize) fall outside the steps and are ignored. --with NAME keeps only the
+steps that launch a kernel whose short name contains NAME, --without NAME
+drops those that do (bench.py's run
+holds the main line's steps, then the secondary line's and the bf16_pass
+line's: `--with true>` picks the int8 pass's, `mfma<768,0,2304,2,false,false>`
+the bf16 pass's).
 """
 from __future__ import annotations
 
@@ -45,6 +50,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--anchor", default="query_prep")
     ap.add_argument("--last", type=int, default=40)
+    ap.add_argument("--with", dest="with_", default=None)
+    ap.add_argument("--without", default=None)
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args()
     rows = load(a.trace)
@@ -52,7 +59,14 @@ def main():
     if len(starts) < 3:
         sys.exit(f"fewer than 3 anchors ({a.anchor}) in the trace")
     # steps: [starts[j], starts[j+1]); keep the last N complete ones
-    spans = list(zip(starts[:-1], starts[1:]))[-a.last:]
+    spans = list(zip(starts[:-1], starts[1:]))
+    if a.with_:
+        spans = [(i0, i1) for i0, i1 in spans if any(a.with_ in r[2] for r in rows[i0:i1])]
+    if a.without:
+        spans = [(i0, i1) for i0, i1 in spans if not any(a.without in r[2] for r in rows[i0:i1])]
+    spans = spans[-a.last:]
+    if not spans:
+        sys.exit("no complete step matches")
     per = defaultdict(lambda: [0.0, 0])
     gaps, span_ns = 0.0, 0.0
     for i0, i1 in spans:
