@@ -2223,56 +2223,69 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   // appends its 8 dots (int32 bits) -- the select bounds and rescores them.
   // Padding and filtered-out rows (the pre-mask) are INT_MIN in the slab:
   // never a maximum, never a survivor.
-  auto q8_epi = [&](f32x4_t (&ac)[2][G], uint32_t trow0, bool full) {
+  // (r05) split in two halves, so the deferred form below can place them in
+  // different MFMA steps: q8_epi_mx masks query group g's dots of the tile
+  // (padding / filtered rows -> INT_MIN, in ac) and returns their maximum;
+  // q8_epi_app appends them when that reaches the group's threshold.
+  auto q8_epi_am = [&](uint32_t trow0) -> uint32_t {
     uint32_t am = 0xFFu;
     if (a.allow) {
       const uint32_t tw = (uint32_t)(a.allow[trow0 >> 6] >> (trow0 & 32)) >> (4 * kq);
       am = (tw & 0xFu) | ((tw >> 12) & 0xF0u);
     }
+    return am;
+  };
+  // (may_filter false: the caller knows a.allow is null -- the split form)
+  auto q8_epi_mx = [&](f32x4_t (&ac)[2][G], int g, uint32_t trow0, bool full, uint32_t am,
+                       bool may_filter = true) -> int {
+    // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
+    // one ext_vector element (it reads element 0; tools/q8_check.hip found it)
+    const i32x4_t a0 = __builtin_bit_cast(i32x4_t, ac[0][g]);
+    const i32x4_t a1 = __builtin_bit_cast(i32x4_t, ac[1][g]);
+    int v[8];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      // whole-vector bit casts: this hipcc miscompiles __builtin_bit_cast of
-      // one ext_vector element (it reads element 0; tools/q8_check.hip found it)
-      const i32x4_t a0 = __builtin_bit_cast(i32x4_t, ac[0][g]);
-      const i32x4_t a1 = __builtin_bit_cast(i32x4_t, ac[1][g]);
-      int v[8];
+    for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
+    if (!full || (may_filter && a.allow)) {  // uniform: unfiltered full tiles skip it
+      // the row base and mask bits are taken opaque inside the branch: the
+      // compiler otherwise hoists their 16 adds/ands into every unfiltered
+      // full tile (r05 ISA: 17 of the epilogue's 38 VALU per tile)
+      uint32_t rb = trow0 + 4 * kq, amv = am;
+      asm volatile("" : "+v"(rb), "+v"(amv));
 #pragma unroll
-      for (int b = 0; b < 4; ++b) v[b] = a0[b], v[4 + b] = a1[b];
-      if (!full || a.allow) {  // uniform: unfiltered full tiles skip it
-        // the row base and mask bits are taken opaque inside the branch: the
-        // compiler otherwise hoists their 16 adds/ands into every unfiltered
-        // full tile (r05 ISA: 17 of the epilogue's 38 VALU per tile)
-        uint32_t rb = trow0 + 4 * kq, amv = am;
-        asm volatile("" : "+v"(rb), "+v"(amv));
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (rb + 16 * (b >> 2) + (b & 3) >= wr1 || !((amv >> b) & 1u)) v[b] = INT_MIN;
-        ac[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
-        ac[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
-      }
-      const int mx = imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
-      // VAR 16777216 (timing ablation only, wrong answers): never append
-      if ((VAR & 16777216) != 0) {
-        asm volatile("" ::"v"(mx >= th_i[g]));
-        continue;
-      }
-      if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
-        const uint32_t sub = a.cand_cap >> 2;
-        const uint32_t cg = cnt_r[g];
-        // r05: a full quarter keeps counting (a count past its capacity
-        // marks it lossy: select_q8 recomputes its rows from the int8
-        // copy) and its largest dot stays exact; no hand-back
-        if (cg < sub) {
-          const size_t slot = (size_t)slot0[g] + cg;
-          f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
-          sp[0] = ac[0][g];
-          sp[1] = ac[1][g];
-          a.cand_tile[slot] = a.row_base + trow0;
-        }
-        cnt_r[g] = cg + 1;
-        qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
-      }
+      for (int b = 0; b < 8; ++b)
+        if (rb + 16 * (b >> 2) + (b & 3) >= wr1 || !((amv >> b) & 1u)) v[b] = INT_MIN;
+      ac[0][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[0], v[1], v[2], v[3]});
+      ac[1][g] = __builtin_bit_cast(f32x4_t, i32x4_t{v[4], v[5], v[6], v[7]});
     }
+    return imax3(imax3(v[0], v[1], v[2]), imax3(v[3], v[4], v[5]), imax3(v[6], v[7], INT_MIN));
+  };
+  auto q8_epi_app = [&](f32x4_t (&ac)[2][G], int g, uint32_t trow0, int mx) {
+    // VAR 16777216 (timing ablation only, wrong answers): never append
+    if ((VAR & 16777216) != 0) {
+      asm volatile("" ::"v"(mx >= th_i[g]));
+      return;
+    }
+    if (mx >= th_i[g]) {  // th_i > INT_MIN: padding never passes; invalid queries: INT_MAX
+      const uint32_t sub = a.cand_cap >> 2;
+      const uint32_t cg = cnt_r[g];
+      // r05: a full quarter keeps counting (a count past its capacity
+      // marks it lossy: select_q8 recomputes its rows from the int8
+      // copy) and its largest dot stays exact; no hand-back
+      if (cg < sub) {
+        const size_t slot = (size_t)slot0[g] + cg;
+        f32x4_t* sp = (f32x4_t*)a.cand + 2 * slot;
+        sp[0] = ac[0][g];
+        sp[1] = ac[1][g];
+        a.cand_tile[slot] = a.row_base + trow0;
+      }
+      cnt_r[g] = cg + 1;
+      qmx_r[g] = mx > qmx_r[g] ? mx : qmx_r[g];
+    }
+  };
+  auto q8_epi = [&](f32x4_t (&ac)[2][G], uint32_t trow0, bool full) {
+    const uint32_t am = q8_epi_am(trow0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) q8_epi_app(ac, g, trow0, q8_epi_mx(ac, g, trow0, full, am));
   };
   // VAR 67108864 (r05, int8 pass): the epilogue of tile t runs after the first
   // step's MFMAs of tile t + 1, on the other of two accumulator sets, so its
@@ -2282,6 +2295,25 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
   f32x4_t accq[kEpiPipe ? 2 : 1][2][G];
   uint32_t prow0 = 0;
   bool pfull = true, have_prev = false;
+  // VAR 65536 (r05, with 67108864): the deferred epilogue split over the next
+  // tile's steps -- group g's maximum after step 1 + g, the appends after
+  // step G + 1 -- so its compares sit in the MFMA steps' issue gaps instead
+  // of one block. Only full tiles are deferred (a partial last tile runs its
+  // own at once); the first tile's "previous" set starts as INT_MIN dots,
+  // which never pass, so no step tests whether a previous tile exists.
+  constexpr bool kEpiSplit = kEpiPipe && (VAR & 65536) != 0;
+  // (the launcher runs this form only without a filter: a.allow is null)
+  int mxp[G];
+  if constexpr (kEpiSplit) {
+#pragma unroll
+    for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        accq[1][hr][g] = __builtin_bit_cast(f32x4_t, i32x4_t{INT_MIN, INT_MIN, INT_MIN, INT_MIN});
+        mxp[g] = INT_MIN;
+      }
+    prow0 = wr0;
+  }
   // VAR 32768 (r05, ablation): a tile's first PD A-fragment reads are issued
   // at the end of the previous tile, before its epilogue (the next tile's
   // first chunk was published by the barrier at the head of this tile's last
@@ -2418,7 +2450,16 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
             }
           }
           if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
-          if constexpr (kEpiPipe) {
+          if constexpr (kEpiSplit) {
+            if (u == 0) {  // compile-time: u, s unrolled
+              if (s >= 1 && s <= G)
+                mxp[s - 1] = q8_epi_mx(accq[1 - SET], s - 1, prow0, true, 0xFFu, false);
+              if (s == G + 1) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) q8_epi_app(accq[1 - SET], g, prow0, mxp[g]);
+              }
+            }
+          } else if constexpr (kEpiPipe) {
             if (u == 0 && s == 0 && have_prev) {
               q8_epi(accq[1 - SET], prow0, pfull);
               __builtin_amdgcn_sched_barrier(0);
@@ -2478,7 +2519,12 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
       }
     }
     if constexpr (I8 && MODE == 0) {
-      if constexpr (kEpiPipe) {  // run after the next tile's first step (or at the end)
+      if constexpr (kEpiSplit) {  // full tiles: in the next tile's steps (or at the end)
+        if (full)
+          prow0 = trow0;
+        else
+          q8_epi(acc, trow0, false);
+      } else if constexpr (kEpiPipe) {  // run after the next tile's first step (or at the end)
         prow0 = trow0, pfull = full, have_prev = true;
       } else {
         q8_epi(acc, trow0, full);
@@ -2633,7 +2679,14 @@ __global__ __launch_bounds__(64 * mf_waves(G), mf_waves(G) == 4 ? 1 : 8 / mf_wav
     } else {
       for (uint32_t t = 0; t < ntiles; ++t) tile_p(t, MfFull<false>{}, stag_tag);
     }
-    if constexpr (kEpiPipe) {  // the last tile's epilogue
+    if constexpr (kEpiSplit) {  // the last tile's, when it is a deferred full one
+      if (ntiles == nfull && nfull > 0) {
+        if ((nfull - 1) & 1u)
+          q8_epi(accq[1], prow0, true);
+        else
+          q8_epi(accq[0], prow0, true);
+      }
+    } else if constexpr (kEpiPipe) {  // the last tile's epilogue
       if (have_prev) {
         if ((ntiles - 1) & 1u)
           q8_epi(accq[1], prow0, pfull);

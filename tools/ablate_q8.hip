@@ -13,9 +13,10 @@
 //   pair     VAR 33554432: one barrier per pair of tiles (vs_kernels.hip)
 //   epipipe  VAR 67108864: each tile's epilogue deferred into the next tile
 //   spread   VAR 16384: a chunk's DMA pieces spread over its steps
-//   stream-spread  the stream skeleton with them spread
 //   prea     VAR 32768: a tile's first A-fragment reads before the previous
-//            tile's epilogue (prea+spread both; mfma-prea: the MFMA skeleton)
+//            tile's epilogue
+//   split    VAR 67108864 + 65536: the deferred epilogue split over the next
+//            tile's steps 1 .. G + 1
 // (r05 records of the dropped arms -- pd2/pd3: A fragments 2 / 3 steps
 // ahead, stag: waves 4-7 half a chunk ahead, pair+epi -- all slower than
 // prod: profiles/r05_ablate_q8*.json)
@@ -129,10 +130,8 @@ int main(int argc, char** argv) {
       {"pair", run<768, 0, 2304 + 33554432, true>, {}},
       {"epipipe", run<768, 0, 2304 + 67108864, true>, {}},
       {"spread", run<768, 0, 2304 + 16384, true>, {}},
-      {"stream-spread", run<384, 2, 2304 + 16384, false>, {}},
       {"prea", run<768, 0, 2304 + 32768, true>, {}},
-      {"prea+spread", run<768, 0, 2304 + 32768 + 16384, true>, {}},
-      {"mfma-prea", run<384, 4, 2304 + 32768, false>, {}},
+      {"split", run<768, 0, 2304 + 67108864 + 65536, true>, {}},
   };
   // an arm's name as the 4th argument: that arm alone (PMC passes), R x B launches
   if (argc > 4) {
@@ -237,9 +236,9 @@ int main(int argc, char** argv) {
   };
   std::vector<uint32_t> ref, got;
   if (snap(run<768, 0, 2304, true>, ref)) return 1;
-  const char* vnames[4] = {"pair", "epipipe", "spread", "prea+spread"};
+  const char* vnames[4] = {"pair", "epipipe", "spread", "split"};
   float (*vfns[4])(const Ctx&) = {run<768, 0, 2304 + 33554432, true>, run<768, 0, 2304 + 67108864, true>,
-                                  run<768, 0, 2304 + 16384, true>, run<768, 0, 2304 + 32768 + 16384, true>};
+                                  run<768, 0, 2304 + 16384, true>, run<768, 0, 2304 + 67108864 + 65536, true>};
   for (int v = 0; v < 4; ++v) {
     if (snap(vfns[v], got)) return 1;
     size_t diff = 0;
