@@ -272,7 +272,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             const float* bound, const void* X8, const void* Q8,
                             const uint64_t* allow, uint32_t n_rows, hipStream_t st,
                             uint32_t* stats = nullptr,  // (tools) += slabs read, survivors, slow paths
-                            uint64_t* clk = nullptr);   // (tools) [nq][8] stage wall clocks
+                            uint64_t* clk = nullptr);   // (tools) [nq][16] stage wall clocks
 // Store side (vs_q8.hip; X: bf16 rows, or fp32 rows when f32): glob[0] = max
 // |x| over n values (atomic max; zero it first); glob[3] = S = glob[0] / 127
 // (1 when 0).

@@ -3452,9 +3452,11 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t hist[256], hws[4], hpick, habove;  // kth_floor's radix state
   // (tools/share_pipe.hip) per-workgroup wall clock at the stage boundaries:
   // 0 start, 1 bound, 2 survivors, 3 rescore, 4 end; two rounds: 5 first
-  // floor, 6 first round, 7 second floor
+  // floor, 6 first round, 7 second floor; inside the survivor stage (thread
+  // 0's view): 8 lossy test, 9 owners written, 10 first round's loads
+  // issued, 11 its rows tested ([nq][16])
   auto tick = [&](int i) {
-    if (clk && threadIdx.x == 0) clk[(size_t)blockIdx.x * 8 + i] = wall_clock64();
+    if (clk && threadIdx.x == 0) clk[(size_t)blockIdx.x * 16 + i] = wall_clock64();
   };
   tick(0);
   const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -3557,6 +3559,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   if (c1 && (float)x1 * sqS + mg < Tcut) c1 = 0, lossy1 = false;
   // a lossy quarter that can reach Tcut: its rows are recomputed (slow path)
   const bool slow = __syncthreads_or(lossy0 || lossy1) != 0;
+  tick(8);
   if (lossy0) c0 = 0;
   if (lossy1) c1 = 0;
   uint32_t incl = c0 + c1;
@@ -3583,6 +3586,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   for (uint32_t j = 0; j < c1; ++j)
     if (ex + c0 + j < 2 * kSelChunk) owner[ex + c0 + j] = (uint16_t)(l0 + 1);
   __syncthreads();
+  tick(9);
   const uint32_t T = total;
   auto slab_at = [&](uint32_t l, uint32_t j) -> size_t {
     return ((size_t)(l >> 2) * kMfmaQueries + q) * cap + (l & 3) * sub + j;
@@ -3615,6 +3619,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
       v[u][1] = __builtin_bit_cast(i32x4_t, slabs[2 * e + 1]);
       tl[u] = ok[u] ? tiles[e] : row_base;
     }
+    if (base == 0) tick(10);
 #pragma unroll
     for (int u = 0; u < kQ8Held; ++u) {
       const uint32_t lt = (tl[u] - row_base) >> 5;
@@ -3638,6 +3643,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
         }
       }
     }
+    if (base == 0) tick(11);
   }
   __syncthreads();
   tick(2);

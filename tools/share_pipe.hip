@@ -84,8 +84,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bound, PS * 4));
   uint64_t *out, *clk;
   CK(hipMalloc(&out, (size_t)nq * k * 8));
-  CK(hipMalloc(&clk, (size_t)nq * 8 * 8));
-  CK(hipMemset(clk, 0, (size_t)nq * 8 * 8));
+  CK(hipMalloc(&clk, (size_t)nq * 16 * 8));
+  CK(hipMemset(clk, 0, (size_t)nq * 16 * 8));
 
   uint32_t L = 0;
   auto prep = [&]() { CK(vsk::launch_query_prep(qf, nq, dim, false, true, nullptr, qb, st)); };
@@ -160,15 +160,16 @@ int main(int argc, char** argv) {
   CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim, q8par,
                            glob, meta, bound, X8, q8q, nullptr, n, st, stats, clk));
   CK(hipStreamSynchronize(st));
-  std::vector<uint64_t> h((size_t)nq * 8);
+  std::vector<uint64_t> h((size_t)nq * 16);
   CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
   uint64_t t0 = ~0ull;
-  for (uint32_t q = 0; q < nq; ++q) t0 = std::min(t0, h[(size_t)q * 8]);
-  const char* names[8] = {"start", "bound", "survivors", "rescore", "end", "p1", "round1", "p2"};
-  for (int s = 0; s < 8; ++s) {
+  for (uint32_t q = 0; q < nq; ++q) t0 = std::min(t0, h[(size_t)q * 16]);
+  const char* names[12] = {"start", "bound",  "survivors", "rescore", "end",    "p1",
+                           "round1", "p2", "s_lossy",  "s_owner", "s_issue", "s_tested"};
+  for (int s = 0; s < 12; ++s) {
     std::vector<double> v;
     for (uint32_t q = 0; q < nq; ++q)
-      if (h[(size_t)q * 8 + s]) v.push_back((h[(size_t)q * 8 + s] - t0) * 0.01);
+      if (h[(size_t)q * 16 + s]) v.push_back((h[(size_t)q * 16 + s] - t0) * 0.01);
     std::sort(v.begin(), v.end());
     if (!v.empty())
       std::printf(", \"sel_%s_us_med\": %.2f, \"sel_%s_us_max\": %.2f", names[s], v[v.size() / 2], names[s],
