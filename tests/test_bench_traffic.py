@@ -37,8 +37,13 @@ def test_traffic_only_for_the_measured_rows():
     e = _entry(bench, "c3_i8")
     assert e["rows"] == 10_000_000
     assert bench.pmc_traffic("c3_i8", 10_000_000) == e["hbm_bytes_per_launch"]
-    for rows in (5_000_000, 2_500_000, 1_250_000, 9_999_999):
+    for rows in (5_000_000, 2_500_000, 9_999_999):
         assert bench.pmc_traffic("c3_i8", rows) is None
+    # a share measured at its own size has its own entry (key c3_i8@1250000)
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    s = d.get("c3_i8@1250000")
+    want = s["hbm_bytes_per_launch"] if s and s.get("rows") == 1_250_000 else None
+    assert bench.pmc_traffic("c3_i8", 1_250_000) == want
     assert bench.pmc_traffic("no_such_config", 10_000_000) is None
 
 
