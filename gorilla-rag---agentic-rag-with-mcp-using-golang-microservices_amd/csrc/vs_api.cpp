@@ -133,7 +133,7 @@ struct vs_engine {
   std::vector<uint64_t> dev_bytes;
   std::vector<uint32_t> dev_colls;
   // one process per GPU (vs_comm_init): the ranks' communicator and the
-  // all-gather output of vs_gather_merge_keys (guarded by dev[0]->work_mu)
+  // all-gather output of vs_gather_merge_keys (guarded by gm_mu, below)
   ncclComm_t pcomm = nullptr;
   uint32_t pranks = 0, prank = 0;
   DevBuf pgather;
@@ -141,7 +141,9 @@ struct vs_engine {
   // pgather (and, for k <= kMaxK, a scratch-free merge), so it orders itself
   // after the previous exchange (gm_ev on gm_stream) instead of joining the
   // primary context's search stream -- an exchange on a side stream then
-  // overlaps the next batch's search
+  // overlaps the next batch's search. Every exchange, the
+  // large-k one too, holds gm_mu and follows gm_ev, so no two exchanges
+  // share pgather at once whatever streams they run on.
   std::mutex gm_mu;
   hipStream_t gm_stream = nullptr;
   hipEvent_t gm_ev = nullptr;
@@ -1336,21 +1338,6 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
   DevEngine* d0 = eng->dev[0];
   hipStream_t cs = (hipStream_t)stream;
   const size_t lbytes = (size_t)nq * k_in * 8;
-  if (k > vsk::kMaxK || k_in > vsk::kMaxK) {
-    // the large-k merge uses the primary context's scratch: its stream order
-    std::lock_guard<std::mutex> g(d0->work_mu);
-    VS_HIP(vsd::set_dev(d0), "hipSetDevice");
-    VS_HIP(vsd::use_stream(d0, cs), "stream order");
-    if (eng->pgather.bytes < lbytes * eng->pranks) {
-      VS_HIP(hipStreamSynchronize(cs), "sync");
-      VS_HIP(eng->pgather.ensure(lbytes * eng->pranks), "alloc gathered keys");
-    }
-    const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
-                                         eng->pcomm, cs);
-    if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-    return vsd::merge_any(d0, eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in,
-                          nq, k_in, k, d_out_keys);
-  }
   std::lock_guard<std::mutex> g(eng->gm_mu);
   VS_HIP(vsd::set_dev(d0), "hipSetDevice");
   if (!eng->gm_ev) VS_HIP(hipEventCreateWithFlags(&eng->gm_ev, hipEventDisableTiming), "event");
@@ -1360,17 +1347,32 @@ int vs_gather_merge_keys(vs_engine* eng, const uint64_t* d_local, uint32_t nq, u
     VS_HIP(hipStreamWaitEvent(cs, eng->gm_ev, 0), "stream order");
   eng->gm_stream = cs;
   if (eng->pgather.bytes < lbytes * eng->pranks) {
+    // (cs waits for the previous exchange, so this also drains that one)
     VS_HIP(hipStreamSynchronize(cs), "sync");
     VS_HIP(eng->pgather.ensure(lbytes * eng->pranks), "alloc gathered keys");
   }
   const ncclResult_t r = ncclAllGather(d_local, eng->pgather.p, (size_t)nq * k_in, ncclUint64,
                                        eng->pcomm, cs);
-  if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-  VS_HIP(vsk::launch_merge(eng->pgather.as<uint64_t>(), eng->pranks, (uint64_t)nq * k_in, k_in, nq,
-                           k_in, k, d_out_keys, cs),
-         "merge");
+  int rc = VS_OK;
+  if (r != ncclSuccess) {
+    rc = nccl_fail(r, "ncclAllGather");
+  } else if (k > vsk::kMaxK || k_in > vsk::kMaxK) {
+    // the large-k merge uses the primary context's scratch: its stream order
+    // too (lock order: gm_mu, then work_mu; nothing takes them the other way)
+    std::lock_guard<std::mutex> w(d0->work_mu);
+    const hipError_t e = vsd::use_stream(d0, cs);
+    rc = e != hipSuccess ? ::vsd::fail_hip(e, "stream order")
+                         : vsd::merge_any(d0, eng->pgather.as<uint64_t>(), eng->pranks,
+                                          (uint64_t)nq * k_in, k_in, nq, k_in, k, d_out_keys);
+  } else {
+    const hipError_t e = vsk::launch_merge(eng->pgather.as<uint64_t>(), eng->pranks,
+                                           (uint64_t)nq * k_in, k_in, nq, k_in, k, d_out_keys, cs);
+    if (e != hipSuccess) rc = ::vsd::fail_hip(e, "merge");
+  }
+  // recorded whatever happened above: the next exchange waits for every
+  // operation this one enqueued on pgather
   VS_HIP(hipEventRecord(eng->gm_ev, cs), "stream order");
-  return VS_OK;
+  return rc;
 }
 
 int vs_decode_keys(vs_engine* eng, const uint64_t* d_keys, uint32_t nq, uint32_t k,

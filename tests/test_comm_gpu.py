@@ -74,6 +74,24 @@ with torch.cuda.stream(st):
     s, r, c = eng.decode_keys(merged.data_ptr(), nq, k, st.cuda_stream)
 st.synchronize()
 out["gather_is_truncation"] = bool(torch.equal(g, lists[1, :, :k]))
+# (r05) exchanges on two streams, small-k and large-k (> kMaxK, the merge on
+# the primary context's scratch) interleaved: every exchange orders itself
+# after the previous one on the shared gather buffer, whatever its stream
+kbig, kout = 1100, 1050
+st2 = torch.cuda.Stream()
+with torch.cuda.stream(st):
+    big = torch.zeros((nq, kbig), dtype=torch.int64, device="cuda")
+    eng.search_keys("s1", dq.data_ptr(), nq, dim, kbig, big.data_ptr(), st.cuda_stream)
+st.synchronize()
+gb = [torch.zeros((nq, kout), dtype=torch.int64, device="cuda") for _ in range(4)]
+gs = [torch.zeros((nq, k), dtype=torch.int64, device="cuda") for _ in range(4)]
+for i in range(4):
+    sx = st if i % 2 == 0 else st2
+    eng.gather_merge_keys(big.data_ptr(), nq, kbig, kout, gb[i].data_ptr(), sx.cuda_stream)
+    eng.gather_merge_keys(lists[0].data_ptr(), nq, kin, k, gs[i].data_ptr(), sx.cuda_stream)
+torch.cuda.synchronize()
+out["two_stream_big"] = all(bool(torch.equal(x, big[:, :kout])) for x in gb)
+out["two_stream_small"] = all(bool(torch.equal(x, lists[0, :, :k])) for x in gs)
 Qp = orc.preprocess(orc.generate(orc.SEED_QUERY, 0, nq, dim), False, True)
 s64, rr, cc = orc.search_generated(orc.SEED_CORPUS, 0, n, Qp, k, True)
 resc = orc.rescore_generated(orc.SEED_CORPUS, Qp, r, c, True)
@@ -90,4 +108,5 @@ def test_comm_one_rank():
     assert r["no_init"] == -1 and r["bad_rank"] == -1 and r["multi"] == -1
     assert r["twice"] == -6  # VS_ERR_EXISTS
     assert r["gather_is_truncation"]
+    assert r["two_stream_big"] and r["two_stream_small"]
     assert r["bad"] == []
