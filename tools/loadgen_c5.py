@@ -12,6 +12,7 @@ service's listener (vsvc_http_start on 127.0.0.1), each client on its own
 keep-alive connection. One JSON line per run.
 """
 import argparse
+import resource
 import json
 import os
 import sys
@@ -20,6 +21,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+
+
+def _cpu_quota():
+    """CPUs the cgroup grants (cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except Exception:
+        return None
 
 def main():
     ap = argparse.ArgumentParser()
@@ -73,8 +83,10 @@ def main():
             addr = "127.0.0.1:%d" % lis.port if transport == "http" else None
             svc.loadgen(names, args.dim, clients=clients, seconds=0.5, http=addr)  # warm-up
             before = svc.stats()
+            ru0, w0 = resource.getrusage(resource.RUSAGE_SELF), time.time()
             rep = svc.loadgen(names, args.dim, clients=clients, seconds=args.seconds,
                               seed=clients, http=addr)
+            ru1, w1 = resource.getrusage(resource.RUSAGE_SELF), time.time()
             st = svc.stats()
             calls = st["engine_calls"] - before["engine_calls"]
             nreq = st["requests"] - before["requests"]
@@ -87,7 +99,12 @@ def main():
                     "lat_ms": {k: round(v, 3) for k, v in rep["lat_ms"].items()},
                     "engine_calls": calls,
                     "mean_batch": round(nreq / calls, 2) if calls else None,
-                    "largest_call": st["largest_call"]}
+                    "largest_call": st["largest_call"],
+                    # (r05) host CPU the process used over the run (clients,
+                    # listener, batcher, engine host side), in CPUs busy
+                    "host_cpus_busy": round((ru1.ru_utime - ru0.ru_utime + ru1.ru_stime - ru0.ru_stime)
+                                            / max(w1 - w0, 1e-9), 2),
+                    "cpu_quota": _cpu_quota()}
             print(json.dumps(line), flush=True)
         if lis is not None:
             lis.stop()
