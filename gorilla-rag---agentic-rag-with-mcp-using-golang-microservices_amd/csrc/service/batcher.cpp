@@ -25,9 +25,13 @@ struct Batcher::Req {
   uint32_t* count;
   int rc = VS_OK;
   std::string err;
-  bool done = false;
+  bool done = false;  // (under *mu)
   int lane = -1;  // the collection's device (vs_collection_placement)
-  std::condition_variable* cv = nullptr;  // the waiter's
+  // the waiter's own mutex and condition (r05: a finished call wakes its
+  // requests through these, not through mu_, so the ~75 handler threads of
+  // a C5 batch do not queue on the batcher's lock to return)
+  std::mutex* mu = nullptr;
+  std::condition_variable* cv = nullptr;
 };
 
 Batcher::Batcher(vs_engine* eng, Options opt) : eng_(eng), opt_(opt) {
@@ -59,8 +63,10 @@ std::chrono::steady_clock::time_point deadline_in(int64_t us) {
 int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint32_t k,
                     float* scores, uint64_t* rows, uint32_t* count, std::string* err,
                     uint64_t filter_id) {
+  std::mutex done_mu;
   std::condition_variable done_cv;
   Req r{&coll, q, dim, k, filter_id, scores, rows, count};
+  r.mu = &done_mu;
   r.cv = &done_cv;
   std::unique_lock<std::mutex> lk(mu_);
   if (stop_) {
@@ -86,7 +92,9 @@ int Batcher::search(const std::string& coll, const float* q, uint32_t dim, uint3
   } else {
     queue_.push_back(&r);
     cv_.notify_all();
-    done_cv.wait(lk, [&] { return r.done; });
+    lk.unlock();
+    std::unique_lock<std::mutex> dl(done_mu);
+    done_cv.wait(dl, [&] { return r.done; });  // rc / err / results written before done
   }
   if (r.rc != VS_OK && err) *err = r.err;
   return r.rc;
@@ -200,10 +208,15 @@ void Batcher::run() {
     execute(batch);
     lk.lock();
     end_call(coll, lane, t0, end);
+    lk.unlock();
+    // (a request's waiter may return -- and its Req go out of scope -- as
+    // soon as its mutex is released: nothing here touches r after that)
     for (Req* r : batch) {
+      std::lock_guard<std::mutex> g(*r->mu);
       r->done = true;
       r->cv->notify_one();
     }
+    lk.lock();
     cv_.notify_all();  // a worker waiting to form its batch late
   }
 }
