@@ -74,6 +74,10 @@ class ShardedSearch:
                 self._ev = torch.cuda.Event()
             self._ev.record()  # the local keys, on the search's stream
             self.exchange_stream.wait_event(self._ev)
+            # the exchange reads `local` on its own stream: keep the caching
+            # allocator from handing its memory to the search stream before
+            # that read is done (a ring-less caller drops `local` right away)
+            local.record_stream(self.exchange_stream)
             with torch.cuda.stream(self.exchange_stream):
                 return self.gather_merge(local, k)
         if not dist.is_available() or not dist.is_initialized():
