@@ -17,12 +17,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <string>
 #include <vector>
 
+#include "vs_common.h"
 #include "vs_kernels.h"
 
 #define CK(x)                                                                           \
@@ -121,7 +123,32 @@ int main(int argc, char** argv) {
     const char* name;
     std::function<void()> f;
   };
+  // (r05) a speculative bound's best case: every query's bound set just under
+  // its exact k-th score (from the full batch above), then the int8 pass and
+  // the select alone -- no query prep, sample or bound launch. The select's
+  // k-th must reach the bound (checked below): the exactness test a
+  // speculative bound would rely on.
+  std::vector<uint64_t> hk((size_t)nq * k);
+  CK(hipMemcpy(hk.data(), out, hk.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<float> hb(nq), hb0(nq);
+  CK(hipMemcpy(hb0.data(), bound, nq * 4, hipMemcpyDeviceToHost));
+  for (uint32_t q = 0; q < nq; ++q) {
+    const float sk = vs::key_score(hk[(size_t)q * k + k - 1]);
+    hb[q] = sk - 1e-4f * std::max(1.f, std::fabs(sk));
+  }
+  float* sbound;
+  CK(hipMalloc(&sbound, nq * 4));
+  CK(hipMemcpy(sbound, hb.data(), nq * 4, hipMemcpyHostToDevice));
+  auto pass_s = [&]() {
+    CK(vsk::launch_mfma_cand_q8(X8, dim, n, 0, q8q, nq, k, sbound, q8par, glob, slabs, slab_tile, cap8,
+                                cnt, qmax, maxl, &L, gate, st, nullptr));
+  };
+  auto select_s = [&]() {
+    CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim,
+                             q8par, glob, meta, sbound, X8, q8q, nullptr, n, st, nullptr, nullptr));
+  };
   std::vector<Arm> arms = {
+      {"spec", [&] { pass_s(), select_s(); }},
       {"full", [&] { prep(), sample(), boundq8(), pass(), select(nullptr); }},
       {"r04gate", [&] { prep(), sample(), boundq8(), pass(), select(nullptr), gated(); }},
       {"noselect", [&] { prep(), sample(), boundq8(), pass(); }},
@@ -175,6 +202,19 @@ int main(int argc, char** argv) {
       std::printf(", \"sel_%s_us_med\": %.2f, \"sel_%s_us_max\": %.2f", names[s], v[v.size() / 2], names[s],
                   v.back());
   }
+  // the speculative arm's answers: equal to the full pipeline's, and every
+  // query's k-th at or above its bound
+  pass_s(), select_s();
+  CK(hipStreamSynchronize(st));
+  std::vector<uint64_t> hk2((size_t)nq * k);
+  CK(hipMemcpy(hk2.data(), out, hk2.size() * 8, hipMemcpyDeviceToHost));
+  uint32_t spec_diff = 0, spec_below = 0;
+  for (size_t i = 0; i < hk.size(); ++i) spec_diff += hk[i] != hk2[i];
+  for (uint32_t q = 0; q < nq; ++q) spec_below += vs::key_score(hk2[(size_t)q * k + k - 1]) < hb[q];
+  double gap = 0;
+  for (uint32_t q = 0; q < nq; ++q) gap += hb[q] - hb0[q];
+  std::printf(", \"spec_keys_differ\": %u, \"spec_kth_below_bound\": %u, \"spec_bound_gain_mean\": %.5f",
+              spec_diff, spec_below, gap / nq);
   uint32_t hs[4];
   CK(hipMemcpy(hs, stats, 16, hipMemcpyDeviceToHost));
   std::printf(", \"sel_slabs_per_query\": %.1f, \"sel_survivors_per_query\": %.1f, \"sel_slow_queries\": %u, "
