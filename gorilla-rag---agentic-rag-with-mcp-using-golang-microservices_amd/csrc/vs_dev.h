@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <bitset>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -76,8 +77,13 @@ struct Collection {
   // in step with `data` by every store-side call (q8_after_write)
   void* q8 = nullptr;         // (q8_cap + kPadRows) x dim int8
   float* q8_meta = nullptr;   // {dt, nt} per 32-row tile
-  float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}
+  float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}, then (r05) the
+                              // speculative-bound ratios by k (kQ8SpecK floats)
   uint64_t q8_cap = 0;        // rows the int8 buffers hold
+  // (r05) bumped by every store-side write (the ratios are reset with it):
+  // unique in the process, so a context's record of the ratios it learned
+  // is valid only for the generation it learned them in
+  uint64_t q8_gen = 0;
   uint64_t q8_scaled_at = 0;  // rows when S was last chosen (rescaled at 2x)
   size_t elem() const { return dtype == VS_DTYPE_BF16 ? 2 : 4; }
   size_t row_bytes() const { return elem() * dim; }
@@ -273,6 +279,14 @@ struct DevEngine {
   // completion counter (zeroed at allocation; each launch leaves it zero)
   DevBuf small_part;
   DevBuf q8g;  // one query on the int8 copy: workgroup lists, wave bounds, candidates
+  // (r05) per collection (Collection::gen): the int8 copy generation and the
+  // k whose speculative-bound ratio this context has recorded on its stream
+  // (a later batch of this context may then use it: stream order)
+  struct SpecSeen {
+    uint64_t q8_gen = 0;
+    std::bitset<130> k;
+  };
+  std::unordered_map<uint64_t, SpecSeen> spec_seen;
   std::vector<uint64_t> h_keys;
   std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing

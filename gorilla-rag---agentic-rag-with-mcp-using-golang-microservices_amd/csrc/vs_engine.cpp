@@ -133,6 +133,10 @@ hipError_t ev_end(DevEngine* eng, std::vector<EventPair>& v) {
 // Rows allocated past the capacity: the MFMA scan streams whole 32-row tiles
 // and reads (then masks) up to 31 rows beyond the last one.
 constexpr uint64_t kPadRows = 32;
+// (r05) q8_glob: {absmax, dmax, nmax, S} then the speculative-bound ratio of
+// each k in [0, kMfmaMaxK] (DESIGN.md §5 "Speculative bound")
+constexpr uint32_t kQ8SpecK = vsk::kMfmaMaxK + 1;
+constexpr size_t kQ8GlobBytes = 16 + (size_t)kQ8SpecK * 4;
 // Filtered single-query searches gather the allowed rows when at most
 // 1 / kGatherDensityDen of the collection is allowed: below
 // that density the scattered 1.5-3 KB row reads stay near the streaming rate,
@@ -243,6 +247,15 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
   return rc;
 }
 
+// (r05) The speculative-bound ratios (q8_glob + 4, index k) back to unset
+// (0x7F bytes: 3.4e38, read as "no ratio"), and a new generation, so no
+// context uses a ratio learned on the rows before this write.
+hipError_t q8_spec_reset(DevEngine* eng, Collection& c) {
+  static std::atomic<uint64_t> next_gen{1};
+  c.q8_gen = next_gen.fetch_add(1);
+  return hipMemsetAsync(c.q8_glob + 4, 0x7F, (size_t)kQ8SpecK * 4, eng->stream);
+}
+
 int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
                         const uint32_t* d_tiles, uint32_t nt) {
   if (!q8_wanted(eng, c)) return VS_OK;
@@ -256,7 +269,7 @@ int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
       const uint64_t tiles = (c.cap + kPadRows) / 32 + 1;
       hipError_t e = hipMalloc(&c.q8, (c.cap + kPadRows) * dim);
       if (e == hipSuccess) e = hipMalloc((void**)&c.q8_meta, tiles * 8);
-      if (e == hipSuccess) e = hipMalloc((void**)&c.q8_glob, 16);
+      if (e == hipSuccess) e = hipMalloc((void**)&c.q8_glob, kQ8GlobBytes);
       if (e != hipSuccess) {
         (void)hipGetLastError();
         c.q8_free();
@@ -266,6 +279,7 @@ int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
       VS_HIP(hipMemsetAsync(c.q8, 0, (c.cap + kPadRows) * dim, eng->stream), "zero int8 copy");
     }
     VS_HIP(hipMemsetAsync(c.q8_glob, 0, 16, eng->stream), "zero int8 bounds");
+    VS_HIP(q8_spec_reset(eng, c), "reset speculative-bound ratios");
     VS_HIP(vsk::launch_q8_absmax(c.data, c.dtype == VS_DTYPE_F32, (uint64_t)rows * dim, c.q8_glob,
                                  eng->stream),
            "int8 scale");
@@ -277,6 +291,7 @@ int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
     c.q8_scaled_at = c.rows;
     return VS_OK;
   }
+  VS_HIP(q8_spec_reset(eng, c), "reset speculative-bound ratios");
   if (d_tiles) {
     VS_HIP(vsk::launch_q8_quantize(c.data, c.dtype == VS_DTYPE_F32, rows, dim, d_tiles, 0, nt,
                                    (int8_t*)c.q8, c.q8_meta, c.q8_glob, eng->stream),
@@ -557,6 +572,27 @@ bool select_qmax() {
 
 // VS_Q8_SAMPLE=<factor>: overrides the int8 path's sample-tile factor (read
 // once; ablation only; 0 = the k-dependent default in search_mfma)
+// VS_Q8_SPEC (read once; default 1): batched int8 searches of bf16
+// collections run on a speculative bound once the context has learned the
+// collection's ratio for a k' >= k (r05); 0 = the sample path always
+bool q8_spec_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_SPEC");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+// VS_Q8_SPEC_FORCE_FAIL=1 (tests only, read once): speculative batches run on
+// a ratio of 12.08 (0x41 bytes), far above any unit-vector score, so every
+// one fails its check and the gated sample path must answer it
+bool q8_spec_force_fail() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_SPEC_FORCE_FAIL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 double q8_sample_scale() {
   static const double v = [] {
     const char* e = std::getenv("VS_Q8_SAMPLE");
@@ -674,20 +710,66 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     int8_t* q8q = eng->q8_q.as<int8_t>();
     float* q8par = eng->q8_par.as<float>();
     uint32_t* gate = (uint32_t*)(q8par + 4 * PS);
+    // (r05) Speculative bound: unfiltered bf16 batches whose k (or a larger
+    // k') has a ratio this context recorded, in this generation of the copy,
+    // start from bound = ratio x |q| instead of a sample pass. The select's
+    // answer is exact iff every query's k-th exact score reaches its bound -
+    // sigma nmax (q8_verify_record); otherwise the sample path re-runs the
+    // whole batch, every launch gated on the verdict word (*gate). Every
+    // unfiltered batch records 0.97 x its verified k-th scores per |q|.
+    const bool spec_rec = q8_spec_enabled() && !f32 && !allow && k < kQ8SpecK;
+    int spec_k = -1;
+    DevEngine::SpecSeen* seen = nullptr;
+    if (spec_rec) {
+      seen = &eng->spec_seen[c.gen];
+      if (seen->q8_gen != c.q8_gen) seen->q8_gen = c.q8_gen, seen->k.reset();
+      for (uint32_t kk = k; kk < kQ8SpecK && spec_k < 0; ++kk)
+        if (seen->k[kk]) spec_k = (int)kk;
+    }
+    float* ratio = c.q8_glob + 4;
     for (uint32_t q0 = 0; q0 < nq; q0 += P8) {
       const uint32_t nv = std::min(P8, nq - q0);
       uint64_t* out = d_keys + (size_t)q0 * k;
       uint32_t L = 0;
+      const uint32_t* run_if = nullptr;  // the sample path below: gated after a speculative try
+      if (spec_k >= 0) {
+        const float* r_use = ratio + spec_k;
+        if (q8_spec_force_fail()) {  // (tests) the word after *gate, 0x41414141 = 12.08f
+          VS_HIP(hipMemsetAsync(gate + 1, 0x41, 4, eng->stream), "forced ratio");
+          r_use = (const float*)(gate + 1);
+        }
+        VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream,
+                                    r_use, bound),
+               "int8 queries + speculative bound");
+        VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+        VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
+                                        c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
+                                        eng->stream, allow),
+               "int8 scan");
+        VS_HIP(ev_end(eng, eng->scan_ev), "event");
+        VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+        VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
+                                     qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
+                                     q8q, allow, n_rows, eng->stream),
+               "int8 select");
+        VS_HIP(ev_end(eng, eng->merge_ev), "event");
+        VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, true, gate,
+                                            ratio + k, eng->stream),
+               "speculative bound check");
+        run_if = gate;
+      }
       // 1. sample pass(es) -> per-query lower bounds on the k-th score; the
       // first bound launch also makes the batch's int8 queries and zeroes *gate
+      // (not behind a speculative try: *gate is then its verdict)
       for (uint32_t s0 = 0; s0 < nv; s0 += P) {
         const uint32_t ns = std::min(P, nv - s0);
         VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k, st,
-                                       tmax, maxl, &L, eng->stream, allow),
+                                       tmax, maxl, &L, eng->stream, allow, run_if),
                "mfma sample scan");
-        if (s0 == 0 && !q8_prep_apart()) {
+        if (s0 == 0 && (!q8_prep_apart() || run_if)) {
           VS_HIP(vsk::launch_sample_bound_q8(tmax, L * st, ns, k, bound, qptr(q0), f32, nv, dim,
-                                             c.q8_glob, q8q, q8par, gate, eng->stream),
+                                             c.q8_glob, q8q, q8par, run_if ? nullptr : gate,
+                                             eng->stream, run_if),
                  "sample bound + int8 queries");
         } else {
           if (s0 == 0)
@@ -701,19 +783,24 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       // 2. int8 pass -> bounded candidates -> rescored top k (r05: the select
       // recomputes a quarter the pass overflowed and streams a survivor spill
       // itself; no gated bf16 launches behind it)
-      VS_HIP(ev_begin(eng, eng->scan_ev), "event");
+      if (!run_if) VS_HIP(ev_begin(eng, eng->scan_ev), "event");
       VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                       c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
-                                      eng->stream, allow),
+                                      eng->stream, allow, run_if),
              "int8 scan");
-      VS_HIP(ev_end(eng, eng->scan_ev), "event");
-      VS_HIP(ev_begin(eng, eng->merge_ev), "event");
+      if (!run_if) VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      if (!run_if) VS_HIP(ev_begin(eng, eng->merge_ev), "event");
       VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
                                    qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
-                                   q8q, allow, n_rows, eng->stream),
+                                   q8q, allow, n_rows, eng->stream, nullptr, nullptr, run_if),
              "int8 select");
-      VS_HIP(ev_end(eng, eng->merge_ev), "event");
+      if (!run_if) VS_HIP(ev_end(eng, eng->merge_ev), "event");
+      if (spec_rec)  // the sample path's answer is exact: record its ratios
+        VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, false, nullptr,
+                                            ratio + k, eng->stream, run_if),
+               "speculative bound record");
     }
+    if (spec_rec) seen->k[k] = true;
     return VS_OK;
   }
   for (uint32_t p = 0; p < npass; ++p) {

@@ -207,7 +207,8 @@ uint32_t mfma_queries(uint32_t dim, bool f32);  // queries per launch at this di
 hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const void* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, float* tmax, uint32_t max_lists,
-                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr);
+                              uint32_t* nlists, hipStream_t st, const uint64_t* allow = nullptr,
+                              const uint32_t* run_if = nullptr);
 // bound[q] = the k-th largest of tmax[q][0, m) (radix select; -inf if m < k).
 hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
                                float* bound, hipStream_t st);
@@ -258,7 +259,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
                                uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
                                uint32_t* nlists, uint32_t* gate, hipStream_t st,
-                               const uint64_t* allow = nullptr);
+                               const uint64_t* allow = nullptr, const uint32_t* run_if = nullptr);
 // cand_max (same shape as cand_cnt): each quarter's largest appended dot
 // (int32; INT_MIN when empty), so the select reads only the quarters that
 // can hold a top-k row.
@@ -272,7 +273,8 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             const float* bound, const void* X8, const void* Q8,
                             const uint64_t* allow, uint32_t n_rows, hipStream_t st,
                             uint32_t* stats = nullptr,  // (tools) += slabs read, survivors, slow paths
-                            uint64_t* clk = nullptr);   // (tools) [nq][16] stage wall clocks
+                            uint64_t* clk = nullptr,    // (tools) [nq][16] stage wall clocks
+                            const uint32_t* run_if = nullptr);  // stand down unless *run_if
 // Store side (vs_q8.hip; X: bf16 rows, or fp32 rows when f32): glob[0] = max
 // |x| over n values (atomic max; zero it first); glob[3] = S = glob[0] / 127
 // (1 when 0).
@@ -287,14 +289,25 @@ hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t
 // Queries (bf16, or fp32 when f32; nq x dim) -> int8 rows Q8 and q8par[q] =
 // {sq * S, |sq q8|, |q - sq q8|, sigma}, norms rounded up.
 // Also zeroes *gate (the batch's overflow word) ahead of the int8 pass.
+// (r05) With ratio / bound: also bound[q] = *ratio x |q| (-inf while *ratio is
+// unset, >= 1e38): the speculative bound of DESIGN.md §5.
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
-                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st);
+                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st,
+                           const float* ratio = nullptr, float* bound = nullptr);
+// (r05) After a batch's select: check (a speculative batch) raises *fail when
+// a query's k-th exact score is under its bound - sigma nmax; verified queries
+// lower *ratio to 0.97 x their k-th score per unit |q|. run_if: stand down
+// unless *run_if.
+hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
+                                   const float* bound, const float* q8par, const float* glob,
+                                   bool check, uint32_t* fail, float* ratio, hipStream_t st,
+                                   const uint32_t* run_if = nullptr);
 // launch_sample_bound (nq_bound queries) and launch_q8_query (nq queries) as
 // one launch: the int8 path's per-batch prep, one dispatch fewer (r04).
 hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,
                                   float* bound, const void* q, bool f32, uint32_t nq,
                                   uint32_t dim, const float* glob, int8_t* q8, float* q8par,
-                                  uint32_t* gate, hipStream_t st);
+                                  uint32_t* gate, hipStream_t st, const uint32_t* run_if = nullptr);
 // Radix passes of the sample bound (VS_BOUND_PASSES, read once; default 2).
 int sample_bound_passes();
 // Sample tiles per workgroup, and the main pass's candidate capacity per

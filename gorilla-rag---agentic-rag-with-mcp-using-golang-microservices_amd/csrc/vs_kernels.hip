@@ -2829,14 +2829,15 @@ static bool mfma_args_ok(uint32_t dim, bool f32, uint32_t n_rows, uint32_t nq_va
 hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                               uint32_t row_base, const void* Q, uint32_t nq_valid,
                               uint32_t k, uint32_t max_tiles, float* tmax, uint32_t max_lists,
-                              uint32_t* nlists, hipStream_t st, const uint64_t* allow) {
+                              uint32_t* nlists, hipStream_t st, const uint64_t* allow,
+                              const uint32_t* run_if) {
   if (!mfma_args_ok(dim, f32, n_rows, nq_valid, k) || max_tiles == 0) return hipErrorInvalidValue;
   MfArgs a{};
   mfma_grid(n_rows, nlists, &a.rows_per_wg);
   if (*nlists > max_lists) return hipErrorInvalidValue;
   a.X = X, a.Q = Q, a.tmax = tmax;
   a.n_rows = n_rows, a.row_base = row_base, a.max_tiles = max_tiles, a.nq_valid = nq_valid;
-  a.k = k, a.allow = allow;
+  a.k = k, a.allow = allow, a.run_if = run_if;
   return mfma_launch_mode<3>(dim, f32, *nlists, a, st);
 }
 
@@ -2897,7 +2898,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
                                float* slabs, uint32_t* slab_tile, uint32_t cand_cap,
                                uint32_t* cand_cnt, uint32_t* cand_max, uint32_t max_lists,
                                uint32_t* nlists, uint32_t* gate, hipStream_t st,
-                               const uint64_t* allow) {
+                               const uint64_t* allow, const uint32_t* run_if) {
   if (!q8_supported(dim, false) || !mfma_args_ok(dim, false, n_rows, nq_valid, k) || cand_cap < 4 ||
       cand_cap % 4 || cand_cap > kMfmaMaxCandCap || !q8par || !q8glob || !gate || !cand_max)
     return hipErrorInvalidValue;
@@ -2908,7 +2909,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
   a.cand_tile = slab_tile, a.cand_cnt = cand_cnt, a.cand_max = cand_max;
   a.n_rows = n_rows, a.row_base = row_base;
   a.nq_valid = nq_valid, a.k = k, a.cand_cap = cand_cap;
-  a.q8par = q8par, a.q8glob = q8glob, a.gate = gate, a.allow = allow;
+  a.q8par = q8par, a.q8glob = q8glob, a.gate = gate, a.allow = allow, a.run_if = run_if;
   if (dim == 1024) {
     hipLaunchKernelGGL((mfma_topk_kernel<1024, 0, 256, 1, false, true>), dim3(*nlists), dim3(512), 0,
                        st, a);
@@ -3441,7 +3442,8 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
     const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from, uint32_t opts,
-    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk) {
+    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk, const uint32_t* __restrict__ run_if) {
+  if (run_if && *run_if == 0u) return;  // (r05) the fallback behind a verified speculative batch
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -3926,7 +3928,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, const void* X8, const void* Q8,
                             const uint64_t* allow, uint32_t n_rows, hipStream_t st, uint32_t* stats,
-                            uint64_t* clk) {
+                            uint64_t* clk, const uint32_t* run_if) {
   if (!select_args_ok(nwg, cap, nq, k) || !cand_max || !X8 || !Q8) return hipErrorInvalidValue;
   uint32_t gwg = 0, rpw = 0;
   mfma_grid(n_rows, &gwg, &rpw);
@@ -3959,7 +3961,8 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
                      cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
-                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, opts, stats, clk);
+                     (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, opts, stats, clk,
+                     run_if);
   return hipGetLastError();
 }
 

@@ -143,12 +143,17 @@ __global__ __launch_bounds__(256) void q8_quantize_kernel(
 
 // One wave per query (bf16 queries of a bf16 collection, or the fp32
 // preprocessed queries of an fp32 one).
+// (r05) With `ratio` (a collection's learned k-th score per unit |q|, DESIGN.md
+// §5 "Speculative bound"), also bound[i] = ratio x |q|, or -inf while the
+// ratio is unset (>= 1e38: the table's 0x7F-byte fill).
 template <bool F32>
 __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restrict__ qb,
                                                uint32_t nq, uint32_t dim,
                                                const float* __restrict__ glob,
                                                int8_t* __restrict__ q8, float* __restrict__ q8par,
-                                               uint32_t* __restrict__ gate) {
+                                               uint32_t* __restrict__ gate,
+                                               const float* __restrict__ ratio = nullptr,
+                                               float* __restrict__ bound = nullptr) {
   if (gate && blk == 0 && threadIdx.x == 0) *gate = 0u;
   const uint32_t i = blk * 4 + (threadIdx.x >> 6);
   if (i >= nq) return;
@@ -189,6 +194,10 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
     p[1] = norm_up(aa);
     p[2] = norm_up(cc);
     p[3] = sigma;
+    if (bound) {
+      const float r = *ratio;
+      bound[i] = r < 1e38f ? r * (float)sqrt(nn) : -INFINITY;
+    }
   }
 }
 
@@ -197,8 +206,38 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ 
                                                        uint32_t dim, const float* __restrict__ glob,
                                                        int8_t* __restrict__ q8,
                                                        float* __restrict__ q8par,
-                                                       uint32_t* __restrict__ gate) {
-  q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate);
+                                                       uint32_t* __restrict__ gate,
+                                                       const float* __restrict__ ratio,
+                                                       float* __restrict__ bound) {
+  q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate, ratio, bound);
+}
+
+// (r05) After a batch's select: per query, its k-th key's exact score s
+// against the bound b it ran with. A speculative batch is exact iff s reaches
+// b - sigma nmax for every query (every row the pass left out has U below
+// that, so below s; rows the select left out are beaten by the quarter
+// bound's k rows): otherwise *fail is raised and the batch re-runs on the
+// sample path, gated on it. Verified queries with s > 0 lower the
+// collection's ratio for this k to 0.97 s / |q| (atomicMin on the float
+// bits: positive floats order as them). run_if: stand down unless *run_if
+// (the record after a fallback).
+__global__ __launch_bounds__(256) void q8_verify_record_kernel(
+    const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint32_t dim,
+    const float* __restrict__ bound, const float* __restrict__ q8par,
+    const float* __restrict__ glob, uint32_t check, uint32_t* __restrict__ fail,
+    float* __restrict__ ratio, const uint32_t* __restrict__ run_if) {
+  if (run_if && *run_if == 0u) return;
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const uint64_t key = keys[(size_t)q * k + k - 1];
+  const float s = key ? vs::key_score(key) : -INFINITY;
+  const float sig = q8par[4 * (size_t)q + 3];
+  const bool ok = !check || (key != 0 && s >= bound[q] - sig * glob[2]);
+  if (!ok) atomicAdd(fail, 1u);
+  // |q| from sigma = (4 dim + 64) 2^-24 |q| (1 + 2^-20) (vs_bound_dev.h q8_sigma)
+  const float qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
+  if (ok && key != 0 && s > 0.f && qn > 0.f)
+    atomicMin((unsigned int*)ratio, __float_as_uint(0.97f * s / qn));
 }
 
 // Workgroups [0, nq_bound): the sample bound of query blockIdx.x; the rest:
@@ -208,7 +247,8 @@ __global__ __launch_bounds__(kBoundThreads) void sample_bound_q8_kernel(
     const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound, int passes,
     uint32_t nq_bound, const void* __restrict__ qb, uint32_t nq, uint32_t dim,
     const float* __restrict__ glob, int8_t* __restrict__ q8, float* __restrict__ q8par,
-    uint32_t* __restrict__ gate) {
+    uint32_t* __restrict__ gate, const uint32_t* __restrict__ run_if) {
+  if (run_if && *run_if == 0u) return;  // (r05) the fallback behind a verified speculative batch
   if (blockIdx.x < nq_bound)
     sample_bound_block(tmax, m, k, bound, passes, blockIdx.x);
   else
@@ -252,22 +292,33 @@ hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t
 }
 
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
-                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st) {
-  if (dim % 128 || dim == 0) return hipErrorInvalidValue;
+                           int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st,
+                           const float* ratio, float* bound) {
+  if (dim % 128 || dim == 0 || (bound && !ratio)) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   if (f32)
     hipLaunchKernelGGL(q8_query_kernel<true>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
-                       glob, q8, q8par, gate);
+                       glob, q8, q8par, gate, ratio, bound);
   else
     hipLaunchKernelGGL(q8_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
-                       glob, q8, q8par, gate);
+                       glob, q8, q8par, gate, ratio, bound);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
+                                   const float* bound, const float* q8par, const float* glob,
+                                   bool check, uint32_t* fail, float* ratio, hipStream_t st,
+                                   const uint32_t* run_if) {
+  if (nq == 0 || k == 0 || !ratio || (check && !fail)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(q8_verify_record_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, k,
+                     dim, bound, q8par, glob, check ? 1u : 0u, fail, ratio, run_if);
   return hipGetLastError();
 }
 
 hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,
                                   float* bound, const void* q, bool f32, uint32_t nq,
                                   uint32_t dim, const float* glob, int8_t* q8, float* q8par,
-                                  uint32_t* gate, hipStream_t st) {
+                                  uint32_t* gate, hipStream_t st, const uint32_t* run_if) {
   static_assert(kBoundThreads == 256, "four query waves per workgroup");
   if (dim % 128 || dim == 0 || nq == 0 || nq_bound == 0 || nq_bound > kMfmaQueries || k == 0 ||
       k > kMfmaMaxK)
@@ -276,10 +327,10 @@ hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bou
   const int passes = sample_bound_passes();
   if (f32)
     hipLaunchKernelGGL(sample_bound_q8_kernel<true>, grid, dim3(kBoundThreads), 0, st, tmax, m, k,
-                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate);
+                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate, run_if);
   else
     hipLaunchKernelGGL(sample_bound_q8_kernel<false>, grid, dim3(kBoundThreads), 0, st, tmax, m, k,
-                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate);
+                       bound, passes, nq_bound, q, nq, dim, glob, q8, q8par, gate, run_if);
   return hipGetLastError();
 }
 

@@ -1,0 +1,90 @@
+"""Speculative bound on the int8 path (r05; DESIGN.md §5 "Speculative bound",
+csrc/vs_engine.cpp search_mfma, csrc/vs_q8.hip q8_verify_record_kernel).
+
+Once a search context has answered an unfiltered bf16 batch of a collection
+at some k, later batches at k' <= k start the int8 pass from bound = ratio x
+|q| (0.97 x the smallest verified k-th score per |q|) instead of a sample
+pass. The answer is exact iff every query's k-th exact score reaches its
+bound - sigma nmax; otherwise the whole batch re-runs on the sample path,
+gated on that verdict on the device. Checked in a child process with one
+search context (VS_CONTEXTS=1, so the second batch takes the speculative
+path): repeated and fresh batches, smaller k, a write in between (the ratios
+are reset), and every speculative batch forced to fail (the gated fallback
+answers it) -- keys bit-identical to the plain bf16 pass every time, and to
+the oracle. Anchor: Points.Search, rag/vector-service/main.go:249-254.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+_SPEC = r"""
+import sys, json
+sys.path.insert(0, ROOT)
+import numpy as np
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+n, dim = 200_000, 768
+a = pkg.VectorEngine(device=0)
+b = pkg.VectorEngine(device=0, prefilter=False)
+for e in (a, b):
+    e.create_collection("p", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16, n + 4096)
+    e.generate("p", n, 91)
+out = {"mismatch": [], "parity": []}
+X = orc.generate(91, 0, n, dim, bf16=True)
+
+def check(tag, Q, k):
+    s1, r1, c1 = a.search("p", Q, k)
+    s2, r2, c2 = b.search("p", Q, k)
+    same = (np.array_equal(c1, c2) and np.array_equal(r1, r2)
+            and np.array_equal(s1.view(np.uint32), s2.view(np.uint32)))
+    if not same:
+        out["mismatch"].append(tag)
+    return s1, r1, c1
+
+runs = [("first", 0, 10), ("again", 0, 10), ("again2", 0, 10), ("fresh", 256, 10),
+        ("smaller_k", 512, 5), ("larger_k", 768, 50), ("larger_k_again", 768, 50),
+        ("fresh_k50", 1024, 50)]
+for tag, q0, k in runs:
+    Q = orc.generate(orc.SEED_QUERY, q0, 256, dim)
+    check(tag, Q, k)
+# a write in between: the ratios are reset, the next batch takes the sample path
+rows = np.arange(0, 200, dtype=np.uint64) * 97
+V = orc.generate(5, 0, 200, dim)
+for e in (a, b):
+    e.upsert("p", rows, V)
+Q = orc.generate(orc.SEED_QUERY, 0, 256, dim)
+for tag in ("after_write", "after_write_again"):
+    check(tag, Q, 10)
+# the oracle on the final rows, for the last batch
+Xw = X.copy()
+Xw[rows.astype(np.int64)] = orc.preprocess(V, False, True)
+Qp = orc.preprocess(Q, False, True)
+s, r, c = a.search("p", Q, 10)
+_, s64, rr, cc = orc.search(Xw, Qp, 10)
+resc = orc.rescore(Xw, Qp, r, c)
+out["parity"] = orc.check_topk(s, r, c, s64, rr, cc, resc, 1e-5)[:5]
+a.close(); b.close()
+print(json.dumps(out))
+"""
+
+
+def _run(env):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, VS_CONTEXTS="1", **env)
+    p = subprocess.run([sys.executable, "-c", "ROOT = %r\n" % root + _SPEC], env=e, cwd=root,
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("env", [{}, {"VS_Q8_SPEC_FORCE_FAIL": "1"}, {"VS_Q8_SPEC": "0"}],
+                         ids=["speculative", "forced_fallback", "off"])
+def test_speculative_bound_keys_equal_bf16_pass(env):
+    r = _run(env)
+    assert r["mismatch"] == [], r["mismatch"]
+    assert r["parity"] == [], r["parity"]
