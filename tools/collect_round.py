@@ -38,7 +38,11 @@ def pmc_mfma(tag, bid, kname):
             continue
         d = per.setdefault(r["Dispatch_Id"], {"wall_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    rows = list(per.values())[3:]  # past the clock-settling first launches
+    rows = list(per.values())
+    # (r05) launches that stood down (the gated fallback behind a verified
+    # speculative batch: its grid exits at once) are not the pass
+    top = max((x["wall_ns"] for x in rows), default=0)
+    rows = [x for x in rows if x["wall_ns"] > 0.25 * top][3:]  # past the clock-settling first ones
     if not rows:
         return
     def avg(k):
@@ -76,10 +80,13 @@ def main():
             w.writerow([r["Kernel_Name"], r["Start_Timestamp"], r["End_Timestamp"],
                         int(r["End_Timestamp"]) - int(r["Start_Timestamp"])])
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    # (r05) without the gated launches that stood down (a few us each)
+    nstand = sum(1 for x in dur if x <= 0.25 * max(dur))
+    dur = [x for x in dur if x > 0.25 * max(dur)]
     pr = json.load(open(os.path.join(G, f"{tag}_prof_c3.json")))
     print(f"build {bid}: bench kernel_ms {b['roofline']['kernel_ms']} (frac {b['roofline']['frac']}); "
           f"under rocprof {pr['roofline']['kernel_ms']}; trace mean after 10 launches "
-          f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10}")
+          f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10} ({nstand} stood down)")
     pmc_mfma(tag, bid, kname)
     fetch = []
     for cfg in ("c3", "c3b1"):

@@ -51,6 +51,9 @@ def main():
                 name = r["Kernel_Name"].split("(")[0].replace("void vsk::", "")
         if not vals:
             raise SystemExit(f"no FETCH_SIZE rows for {SCAN[cfg]} in {path}")
+        # (r05) launches that stood down (the gated fallback behind a verified
+        # speculative batch) fetch next to nothing: not the pass
+        vals = [v for v in vals if v > 0.25 * max(vals)]
         kb = sum(vals) / len(vals)
         # rows one launch scanned: bench.py reports the entry only for a run
         # whose rows_per_gpu equals it (an N > 1 share is a different launch)
