@@ -24,11 +24,16 @@ import numpy as np
 import __graft_entry__ as ge
 from oracle import oracle as orc
 pkg = ge.load_package()
-n, dim = 200_000, 768
+import os
+n, dim = 200_000, int(os.environ.get("T_DIM", "768"))
+cosine = os.environ.get("T_COSINE") == "1"
+nq = int(os.environ.get("T_NQ", "256"))
+ks = [int(x) for x in os.environ.get("T_KS", "10,10,10,10,5,50,50,50").split(",")]
 a = pkg.VectorEngine(device=0)
 b = pkg.VectorEngine(device=0, prefilter=False)
 for e in (a, b):
-    e.create_collection("p", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16, n + 4096)
+    e.create_collection("p", dim, pkg.METRIC_COSINE if cosine else pkg.METRIC_DOT, pkg.DTYPE_BF16,
+                        n + 4096)
     e.generate("p", n, 91)
 out = {"mismatch": [], "parity": []}
 X = orc.generate(91, 0, n, dim, bf16=True)
@@ -42,26 +47,26 @@ def check(tag, Q, k):
         out["mismatch"].append(tag)
     return s1, r1, c1
 
-runs = [("first", 0, 10), ("again", 0, 10), ("again2", 0, 10), ("fresh", 256, 10),
-        ("smaller_k", 512, 5), ("larger_k", 768, 50), ("larger_k_again", 768, 50),
-        ("fresh_k50", 1024, 50)]
-for tag, q0, k in runs:
-    Q = orc.generate(orc.SEED_QUERY, q0, 256, dim)
-    check(tag, Q, k)
+# batches: repeated, fresh, smaller and larger k (the KS list, in order)
+q0s = [0, 0, 0, 1, 2, 3, 3, 4]
+for i, k in enumerate(ks):
+    Q = orc.generate(orc.SEED_QUERY, q0s[i % len(q0s)] * nq, nq, dim)
+    check("batch%d_k%d" % (i, k), Q, k)
 # a write in between: the ratios are reset, the next batch takes the sample path
 rows = np.arange(0, 200, dtype=np.uint64) * 97
 V = orc.generate(5, 0, 200, dim)
 for e in (a, b):
     e.upsert("p", rows, V)
-Q = orc.generate(orc.SEED_QUERY, 0, 256, dim)
+Q = orc.generate(orc.SEED_QUERY, 0, nq, dim)
+k0 = ks[0]
 for tag in ("after_write", "after_write_again"):
-    check(tag, Q, 10)
+    check(tag, Q, k0)
 # the oracle on the final rows, for the last batch
-Xw = X.copy()
-Xw[rows.astype(np.int64)] = orc.preprocess(V, False, True)
-Qp = orc.preprocess(Q, False, True)
-s, r, c = a.search("p", Q, 10)
-_, s64, rr, cc = orc.search(Xw, Qp, 10)
+Xw = orc.preprocess(X, cosine, True) if cosine else X.copy()
+Xw[rows.astype(np.int64)] = orc.preprocess(V, cosine, True)
+Qp = orc.preprocess(Q, cosine, True)
+s, r, c = a.search("p", Q, k0)
+_, s64, rr, cc = orc.search(Xw, Qp, k0)
 resc = orc.rescore(Xw, Qp, r, c)
 out["parity"] = orc.check_topk(s, r, c, s64, rr, cc, resc, 1e-5)[:5]
 a.close(); b.close()
@@ -86,5 +91,14 @@ def _run(env):
                          ids=["speculative", "forced_fallback", "off"])
 def test_speculative_bound_keys_equal_bf16_pass(env):
     r = _run(env)
+    assert r["mismatch"] == [], r["mismatch"]
+    assert r["parity"] == [], r["parity"]
+
+
+@pytest.mark.parametrize("env", [{}, {"VS_Q8_SPEC_FORCE_FAIL": "1"}], ids=["speculative", "forced_fallback"])
+def test_speculative_bound_1024_cosine_two_chunks(env):
+    """C5's row shape (1024-d cosine, 128 queries a launch), 300 queries a
+    call (three int8 launches), k up to 128."""
+    r = _run(dict(env, T_DIM="1024", T_COSINE="1", T_NQ="300", T_KS="128,128,7,128,40,100,128,3"))
     assert r["mismatch"] == [], r["mismatch"]
     assert r["parity"] == [], r["parity"]
