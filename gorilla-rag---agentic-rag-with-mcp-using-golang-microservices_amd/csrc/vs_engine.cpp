@@ -717,7 +717,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // sigma nmax (q8_verify_record); otherwise the sample path re-runs the
     // whole batch, every launch gated on the verdict word (*gate). Every
     // unfiltered batch records 0.97 x its verified k-th scores per |q|.
-    const bool spec_rec = q8_spec_enabled() && !f32 && !allow && k < kQ8SpecK;
+    const bool spec_rec = q8_spec_enabled() && !allow && k < kQ8SpecK;
     int spec_k = -1;
     DevEngine::SpecSeen* seen = nullptr;
     if (spec_rec) {
@@ -776,7 +776,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
             VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate,
                                         eng->stream),
                    "int8 queries");
-          VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream),
+          VS_HIP(vsk::launch_sample_bound(tmax, L * st, ns, k, bound + s0, eng->stream, run_if),
                  "sample bound");
         }
       }

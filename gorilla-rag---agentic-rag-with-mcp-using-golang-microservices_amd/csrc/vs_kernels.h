@@ -211,7 +211,7 @@ hipError_t launch_mfma_sample(const void* X, bool f32, uint32_t dim, uint32_t n_
                               const uint32_t* run_if = nullptr);
 // bound[q] = the k-th largest of tmax[q][0, m) (radix select; -inf if m < k).
 hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
-                               float* bound, hipStream_t st);
+                               float* bound, hipStream_t st, const uint32_t* run_if = nullptr);
 hipError_t launch_mfma_cand(const void* X, bool f32, uint32_t dim, uint32_t n_rows,
                             uint32_t row_base, const void* Q, uint32_t nq_valid, uint32_t k,
                             const float* init_score, float* slabs,

@@ -3315,7 +3315,8 @@ __global__ __launch_bounds__(kSelThreads) void select_slab_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBoundThreads) void sample_bound_kernel(
     const float* __restrict__ tmax, uint32_t m, uint32_t k, float* __restrict__ bound,
-    int passes) {
+    int passes, const uint32_t* __restrict__ run_if) {
+  if (run_if && *run_if == 0u) return;  // (r05) the fallback behind a verified speculative batch
   sample_bound_block(tmax, m, k, bound, passes, blockIdx.x);  // vs_bound_dev.h
 }
 
@@ -3332,10 +3333,10 @@ int sample_bound_passes() {
 }
 
 hipError_t launch_sample_bound(const float* tmax, uint32_t m, uint32_t nq, uint32_t k,
-                               float* bound, hipStream_t st) {
+                               float* bound, hipStream_t st, const uint32_t* run_if) {
   if (nq == 0 || nq > kMfmaQueries || k == 0 || k > kMfmaMaxK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_bound_kernel, dim3(nq), dim3(kBoundThreads), 0, st, tmax, m, k, bound,
-                     sample_bound_passes());
+                     sample_bound_passes(), run_if);
   return hipGetLastError();
 }
 

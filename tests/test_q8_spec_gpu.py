@@ -29,14 +29,15 @@ n, dim = 200_000, int(os.environ.get("T_DIM", "768"))
 cosine = os.environ.get("T_COSINE") == "1"
 nq = int(os.environ.get("T_NQ", "256"))
 ks = [int(x) for x in os.environ.get("T_KS", "10,10,10,10,5,50,50,50").split(",")]
+f32 = os.environ.get("T_F32") == "1"
 a = pkg.VectorEngine(device=0)
 b = pkg.VectorEngine(device=0, prefilter=False)
 for e in (a, b):
-    e.create_collection("p", dim, pkg.METRIC_COSINE if cosine else pkg.METRIC_DOT, pkg.DTYPE_BF16,
-                        n + 4096)
+    e.create_collection("p", dim, pkg.METRIC_COSINE if cosine else pkg.METRIC_DOT,
+                        pkg.DTYPE_F32 if f32 else pkg.DTYPE_BF16, n + 4096)
     e.generate("p", n, 91)
 out = {"mismatch": [], "parity": []}
-X = orc.generate(91, 0, n, dim, bf16=True)
+X = orc.generate(91, 0, n, dim, bf16=not f32)
 
 def check(tag, Q, k):
     s1, r1, c1 = a.search("p", Q, k)
@@ -62,9 +63,9 @@ k0 = ks[0]
 for tag in ("after_write", "after_write_again"):
     check(tag, Q, k0)
 # the oracle on the final rows, for the last batch
-Xw = orc.preprocess(X, cosine, True) if cosine else X.copy()
-Xw[rows.astype(np.int64)] = orc.preprocess(V, cosine, True)
-Qp = orc.preprocess(Q, cosine, True)
+Xw = orc.preprocess(X, cosine, not f32) if cosine else X.copy()
+Xw[rows.astype(np.int64)] = orc.preprocess(V, cosine, not f32)
+Qp = orc.preprocess(Q, cosine, not f32)
 s, r, c = a.search("p", Q, k0)
 _, s64, rr, cc = orc.search(Xw, Qp, k0)
 resc = orc.rescore(Xw, Qp, r, c)
@@ -100,5 +101,14 @@ def test_speculative_bound_1024_cosine_two_chunks(env):
     """C5's row shape (1024-d cosine, 128 queries a launch), 300 queries a
     call (three int8 launches), k up to 128."""
     r = _run(dict(env, T_DIM="1024", T_COSINE="1", T_NQ="300", T_KS="128,128,7,128,40,100,128,3"))
+    assert r["mismatch"] == [], r["mismatch"]
+    assert r["parity"] == [], r["parity"]
+
+
+@pytest.mark.parametrize("env", [{}, {"VS_Q8_SPEC_FORCE_FAIL": "1"}], ids=["speculative", "forced_fallback"])
+def test_speculative_bound_fp32(env):
+    """fp32 rows: two 128-query sample passes behind a speculative try (both
+    gated), survivors rescored on the f32 pass's chain."""
+    r = _run(dict(env, T_F32="1", T_KS="10,10,10,10,5,64,64,64"))
     assert r["mismatch"] == [], r["mismatch"]
     assert r["parity"] == [], r["parity"]
