@@ -515,7 +515,7 @@ def main():
                    # (r05) batches after the first start from the collection's
                    # learned k-th-score ratio, checked per query in the select,
                    # the sample path re-run on a miss
-                   "int8_speculative_bound": bool(int8 and batch > 1 and dtype == "bf16"
+                   "int8_speculative_bound": bool(int8 and batch > 1
                                                   and os.environ.get("VS_Q8_SPEC", "1") != "0"),
                    "build_id": pkg.build_id()},
         "roofline": roof,
