@@ -215,6 +215,73 @@ int main(int argc, char** argv) {
   for (uint32_t q = 0; q < nq; ++q) gap += hb[q] - hb0[q];
   std::printf(", \"spec_keys_differ\": %u, \"spec_kth_below_bound\": %u, \"spec_bound_gain_mean\": %.5f",
               spec_diff, spec_below, gap / nq);
+  // (r05) a speculative bound from another batch's statistics: r = 0.97 x the
+  // smallest k-th score per unit |q| over batch A (the one above), applied to
+  // a fresh batch B (the next nq queries of the stream) as b(q) = r |q|;
+  // B's keys through the full pipeline and through pass + select under that
+  // bound, compared, and B's queries whose k-th fell under their bound (the
+  // ones a gated fallback would redo) counted
+  {
+    auto norms = [&](std::vector<float>& nv) {
+      std::vector<float> hq((size_t)nq * dim);
+      CK(hipMemcpy(hq.data(), qf, hq.size() * 4, hipMemcpyDeviceToHost));
+      nv.assign(nq, 0.f);
+      for (uint32_t q = 0; q < nq; ++q) {
+        double a2 = 0;
+        for (uint32_t d = 0; d < dim; ++d) a2 += (double)hq[(size_t)q * dim + d] * hq[(size_t)q * dim + d];
+        nv[q] = (float)std::sqrt(a2);
+      }
+    };
+    std::vector<float> na, nb;
+    norms(na);
+    double rmin = 1e30;
+    for (uint32_t q = 0; q < nq; ++q)
+      if (na[q] > 0) rmin = std::min(rmin, (double)vs::key_score(hk[(size_t)q * k + k - 1]) / na[q]);
+    const float r = (float)(rmin > 0 ? rmin * 0.97 : 0.0);
+    CK(vsk::launch_generate(0xC0FFEE, nq, nq, dim, false, qf, 0, st, 1));
+    CK(hipStreamSynchronize(st));
+    norms(nb);
+    prep(), sample(), boundq8(), pass(), select(nullptr);
+    CK(hipStreamSynchronize(st));
+    std::vector<uint64_t> kb((size_t)nq * k), kb2((size_t)nq * k);
+    CK(hipMemcpy(kb.data(), out, kb.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<float> bb(nq);
+    for (uint32_t q = 0; q < nq; ++q) bb[q] = r * nb[q];
+    CK(hipMemcpy(sbound, bb.data(), nq * 4, hipMemcpyHostToDevice));
+    pass_s(), select_s();
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(kb2.data(), out, kb2.size() * 8, hipMemcpyDeviceToHost));
+    uint32_t diff = 0, below = 0;
+    for (size_t i = 0; i < kb.size(); ++i) diff += kb[i] != kb2[i];
+    for (uint32_t q = 0; q < nq; ++q) below += vs::key_score(kb[(size_t)q * k + k - 1]) < bb[q];
+    auto time_arm = [&](const std::function<void()>& f) {
+      for (int w = 0; w < 5; ++w) f();
+      std::vector<float> tv;
+      for (int rr = 0; rr < 3; ++rr) {
+        CK(hipEventRecord(a, st));
+        for (int j = 0; j < reps; ++j) f();
+        CK(hipEventRecord(b, st));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tv.push_back(ms * 1e3f / reps);
+      }
+      std::sort(tv.begin(), tv.end());
+      return tv[1];
+    };
+    const float tf = time_arm([&] { prep(), sample(), boundq8(), pass(), select(nullptr); });
+    const float ts = time_arm([&] { pass_s(), select_s(); });
+    std::printf(", \"fresh_ratio\": %.5f, \"fresh_full_us\": %.2f, \"fresh_spec_us\": %.2f, "
+                "\"fresh_keys_differ_where_kth_reaches_bound\": %u, \"fresh_kth_below_bound\": %u",
+                r, tf, ts, below ? 0u : diff, below);
+    if (below) {  // keys of queries whose k-th reached their bound must still agree
+      uint32_t d2 = 0;
+      for (uint32_t q = 0; q < nq; ++q)
+        if (vs::key_score(kb[(size_t)q * k + k - 1]) >= bb[q])
+          for (uint32_t j = 0; j < k; ++j) d2 += kb[(size_t)q * k + j] != kb2[(size_t)q * k + j];
+      std::printf(", \"fresh_keys_differ_verified_queries\": %u", d2);
+    }
+  }
   uint32_t hs[4];
   CK(hipMemcpy(hs, stats, 16, hipMemcpyDeviceToHost));
   std::printf(", \"sel_slabs_per_query\": %.1f, \"sel_survivors_per_query\": %.1f, \"sel_slow_queries\": %u, "
