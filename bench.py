@@ -221,16 +221,24 @@ def scan_roofline(config, rows_local, dim, dtype, batch, k, scan_ms, int8, q8_b1
 
 
 def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_fn, row0):
-    """Times `steps` searches of one batch; returns (max elapsed s over ranks,
-    scan/merge ms, every timed step's result tensor). The result tensors
-    rotate over at least `steps` buffers (shard.engine_callables ring), so
-    each step's answer is still intact after the timed region."""
+    """Times `steps` searches; returns (max elapsed s over ranks, scan/merge ms,
+    every timed step's result tensor, the query rows of each timed step).
+
+    Every step searches a FRESH batch (r06): warmup +
+    steps distinct batches of the query stream (query rows row0 + i * batch
+    ...) are generated into HBM before the timer, and step i searches batch i,
+    so nothing the engine learned from one batch (the speculative bound's
+    ratio) is ever timed on the batch it was learned from. The
+    result tensors rotate over at least `steps` buffers
+    (shard.engine_callables ring), so each step's answer is still intact
+    after the timed region."""
     import torch.distributed as dist
 
-    q = torch.empty((batch, dim), dtype=torch.float32, device="cuda")
-    eng.generate_vectors(0xC0FFEE, row0, batch, dim, q.data_ptr(), stream_fn())
-    for _ in range(warmup):
-        sharded.search(q, k)
+    nb = warmup + steps
+    q = torch.empty((nb, batch, dim), dtype=torch.float32, device="cuda")
+    eng.generate_vectors(0xC0FFEE, row0, nb * batch, dim, q.data_ptr(), stream_fn())
+    for i in range(warmup):
+        sharded.search(q[i], k)
     torch.cuda.synchronize()
     eng.timing(reset=True)
     if dist_on:
@@ -238,8 +246,8 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     outs = []
-    for _ in range(steps):
-        outs.append(sharded.search(q, k))
+    for i in range(warmup, nb):
+        outs.append(sharded.search(q[i], k))
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -250,45 +258,56 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     tm = eng.timing(reset=True)
-    return el, tm, outs
+    return el, tm, outs, (q, warmup)
 
 
-def verify_steps(pkg, outs, k, n_rows):
-    """After the timed region: every timed step's answer is identical to the
-    first one (the same batch each step), full (min(k, rows) keys per query)
-    and sorted. Raises on any violation; returns the checked count."""
-    first = outs[0].cpu().numpy()
-    for i, o in enumerate(outs[1:], 1):
-        if not np.array_equal(o.cpu().numpy(), first):
-            raise AssertionError(f"timed step {i} returned a different answer than step 0")
-    s, r, c = pkg.keys_decode(first.view(np.uint64))
-    if int(c.min()) != min(k, n_rows):
-        raise AssertionError("incomplete result lists")
-    if not np.all(np.diff(s, axis=1) <= 0):
-        raise AssertionError("unsorted results")
+def verify_steps(pkg, outs, k, n_rows, sharded=None, qs=None, recheck=(0, -1)):
+    """After the timed region: every timed step's answer is full (min(k, rows)
+    keys per query) and sorted, and (with `sharded`) the steps in `recheck`,
+    searched again on their own batch, return the same keys -- the answer
+    does not depend on what the engine learned between. Raises on any
+    violation; returns the checked count."""
+    for o in outs:
+        s, r, c = pkg.keys_decode(o.cpu().numpy().view(np.uint64))
+        if int(c.min()) != min(k, n_rows):
+            raise AssertionError("incomplete result lists")
+        if not np.all(np.diff(s, axis=1) <= 0):
+            raise AssertionError("unsorted results")
+    if sharded is not None and qs is not None:
+        q, w = qs
+        for i in recheck:
+            i = i % len(outs)
+            again = sharded.search(q[w + i], k)
+            torch.cuda.synchronize()
+            if not np.array_equal(again.cpu().numpy(), outs[i].cpu().numpy()):
+                raise AssertionError(f"timed step {i}: a second search of its batch differs")
     return len(outs)
 
 
-def oracle_parity(pkg, cfg, n_full, keys, pick=(0, 85, 170, 255)):
-    """Part of the CPU-baseline leg (rank 0, N = 1): `pick` queries of the
-    timed batch checked against the streaming fp64 oracle over the whole
-    generated corpus (the north_star rule, oracle.check_topk). Test
-    infrastructure only: called after the timed region, never timed."""
+def oracle_parity(pkg, cfg, n_full, outs, batch, row0, picks):
+    """Part of the CPU-baseline leg (rank 0, N = 1): queries of several timed
+    batches (`picks`: (step, query) pairs) checked against the streaming fp64
+    oracle over the whole generated corpus (the north_star rule,
+    oracle.check_topk). Test infrastructure only: called after the timed
+    region, never timed."""
     from oracle import oracle
 
-    rows, dim, dtype, metric, batch, k, _ = cfg
+    rows, dim, dtype, metric, _, k, _ = cfg
     bf16 = dtype == "bf16"
-    idx = [i for i in pick if i < keys.shape[0]]
-    Q = oracle.generate(oracle.SEED_QUERY, 0, keys.shape[0], dim)[idx]
+    picks = [(st % len(outs), qi) for st, qi in picks if qi < batch]
+    gids = [row0 + st * batch + qi for st, qi in picks]
+    Q = np.concatenate([oracle.generate(oracle.SEED_QUERY, g, 1, dim) for g in gids])
     Qp = oracle.preprocess(Q, metric == "cosine", bf16)
-    s, r, c = pkg.keys_decode(keys[idx])
+    keys = np.stack([outs[st].cpu().numpy().view(np.uint64)[qi] for st, qi in picks])
+    s, r, c = pkg.keys_decode(keys)
     t0 = time.perf_counter()
     s64, rr, cc = oracle.search_generated(oracle.SEED_CORPUS, 0, n_full, Qp, k, bf16)
     resc = oracle.rescore_generated(oracle.SEED_CORPUS, Qp, r, c, bf16)
     bad = oracle.check_topk(s, r, c, s64, rr, cc, resc, score_rtol=1e-5)
-    return {"queries_checked": len(idx), "query_ids": idx, "violations": len(bad),
-            "first_violations": bad[:3], "rule": "north_star: ids exact except exact-score "
-            "near-ties < 1e-5 rel; scores within 1e-5 rel of the fp64 score",
+    return {"queries_checked": len(picks), "steps_and_queries": [list(p) for p in picks],
+            "query_stream_rows": gids, "violations": len(bad), "first_violations": bad[:3],
+            "rule": "north_star: ids exact except exact-score near-ties < 1e-5 rel; scores within "
+                    "1e-5 rel of the fp64 score",
             "oracle": "oracle.search_generated (fp64, full corpus regenerated)",
             "oracle_s": round(time.perf_counter() - t0, 2)}
 
@@ -480,14 +499,22 @@ def main():
                 log("[bench] torch.distributed exchange instead of the engine communicator")
                 collective = "torch"
 
-    el, tm, outs = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup, dist_on,
-                             stream_fn, 0)
+    int8_pre = batch > 1 and eng.prefilter_bytes(coll) > 0
+    spec0 = eng.spec_stats(coll) if int8_pre else None
+    el, tm, outs, qs = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup,
+                                 dist_on, stream_fn, 0)
+    # the speculative bound's counters over the timed steps (read after the
+    # timer: the call waits for the device)
+    spec = None
+    if int8_pre:
+        s1 = eng.spec_stats(coll)
+        spec = {key: s1[key] - spec0[key] for key in s1}
     out = outs[-1]
-    steps_verified = verify_steps(pkg, outs, k, n_full)
+    steps_verified = verify_steps(pkg, outs, k, n_full, sharded, qs)
     elem = 2 if dtype == "bf16" else 4
     # batched bf16 searches of a collection with an int8 copy run the int8
     # prefilter pass (the engine's default; VS_FLAG_NO_PREFILTER turns it off)
-    int8 = batch > 1 and eng.prefilter_bytes(coll) > 0
+    int8 = int8_pre
     q8_b1 = batch == 1 and q8_gemv_used(eng.prefilter_bytes(coll), dim, k)
     qpp = queries_per_pass(dim, dtype)
     roof = scan_roofline(args.config, hi - lo, dim, dtype, batch, k, tm["scan_ms"], int8, q8_b1)
@@ -520,6 +547,12 @@ def main():
                    "build_id": pkg.build_id()},
         "roofline": roof,
         "steps_verified": steps_verified,
+        # (r06) each timed step searched its own fresh batch; speculative
+        # batches of the timed steps whose check failed (the sample path then
+        # re-answered them), and those a cool-down sent to the sample path
+        "fresh_batches": True,
+        "spec_fallbacks": spec["fallbacks"] if spec else None,
+        "spec_stats": spec,
     }
 
     # secondary: the single-query GEMV line on the same resident corpus
@@ -528,14 +561,15 @@ def main():
         # costs a quarter second, and its sampled kernel average (every 4th
         # launch) then rests on 25+ launches instead of 13
         steps1 = max(100, args.steps)
-        el1, tm1, outs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 10, dist_on,
-                                    stream_fn, 1000)
+        el1, tm1, outs1, qs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 10, dist_on,
+                                         stream_fn, 1000)
         r1 = scan_roofline(args.config + "b1", hi - lo, dim, dtype, 1, k, tm1["scan_ms"], False,
                            q8_gemv_used(eng.prefilter_bytes(coll), dim, k))
         result["secondary"] = {"workload": "same corpus, single query (GEMV path)",
                                "value": round(steps1 / el1, 2), "unit": "queries/s",
                                "ms_per_step": round(el1 / steps1 * 1e3, 4), "roofline": r1,
-                               "steps_verified": verify_steps(pkg, outs1, k, n_full)}
+                               "steps_verified": verify_steps(pkg, outs1, k, n_full, sharded,
+                                                              qs1)}
 
     # secondary (one GPU): the same batch on the bf16 / f32 pass alone -- a
     # second engine without the int8 copy over the same generated rows
@@ -549,11 +583,13 @@ def main():
             e2.generate(coll, hi - lo, 0x5EED)
             ls2, mg2 = shard.engine_callables(e2, coll, dim, stream_fn, reuse=True, ring=ring)
             sh2 = shard.ShardedSearch(ls2, mg2)
-            el2, tm2, outs2 = run_phase(e2, sh2, coll, dim, batch, k, args.steps, args.warmup,
-                                        False, stream_fn, 0)
-            # the int8 path rescores on the bf16 pass's MFMA chain: same keys
-            same = float((outs2[-1].cpu().numpy().view(np.uint64) ==
-                          out.cpu().numpy().view(np.uint64)).mean())
+            el2, tm2, outs2, _ = run_phase(e2, sh2, coll, dim, batch, k, args.steps, args.warmup,
+                                           False, stream_fn, 0)
+            # the int8 path rescores on the bf16 pass's MFMA chain: same keys,
+            # every timed step (the same fresh batches in the same order)
+            same = float(np.mean([(a.cpu().numpy().view(np.uint64) ==
+                                   b.cpu().numpy().view(np.uint64)).mean()
+                                  for a, b in zip(outs2, outs)]))
             result[f"{dtype}_pass"] = {
                 "workload": f"the same batch on the {dtype} MFMA pass (VS_FLAG_NO_PREFILTER)",
                 "value": round(batch * args.steps / el2, 2), "unit": "queries/s",
@@ -571,7 +607,10 @@ def main():
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
         # the same leg checks the timed batch against the oracle (outside the timer)
         try:
-            result["parity"] = oracle_parity(pkg, cfg, n_full, out.cpu().numpy().view(np.uint64))
+            K = len(outs)
+            result["parity"] = oracle_parity(pkg, cfg, n_full, outs, batch, args.warmup * batch,
+                                             [(0, 0), (K // 3, 85), (2 * K // 3, 170),
+                                              (K - 1, 255)])
         except Exception as e:  # reported, never silent
             result["parity"] = {"queries_checked": 0, "error": repr(e)}
     elif rank == 0:

@@ -1170,6 +1170,23 @@ int vs_collection_prefilter_bytes(vs_engine* eng, const char* name, uint64_t* by
   return VS_OK;
 }
 
+int vs_collection_spec_stats(vs_engine* eng, const char* name, uint64_t out[4]) {
+  if (!eng || !out) return fail(VS_ERR_INVALID_ARG, "engine and out are required");
+  if (!eng->sharded) return vsd::spec_stats(eng->dev[0], name, out);
+  auto sc = find_scoll(eng, name);
+  if (!sc) return not_found(name);
+  if (sc->home >= 0) return vsd::spec_stats(home_eng(eng, *sc), sc->iname[0].c_str(), out);
+  uint64_t sum[4] = {0, 0, 0, 0};
+  for (uint32_t s = 0; s < eng->shards(); ++s) {
+    uint64_t part[4];
+    const int rc = vsd::spec_stats(shard_eng(eng, s), sc->iname[s].c_str(), part);
+    if (rc != VS_OK) return rc;
+    for (int j = 0; j < 4; ++j) sum[j] += part[j];
+  }
+  std::memcpy(out, sum, sizeof(sum));
+  return VS_OK;
+}
+
 int vs_upsert(vs_engine* eng, const char* coll, uint64_t n, uint32_t dim, const uint64_t* rows,
               const float* vecs) {
   if (!eng) return fail(VS_ERR_INVALID_ARG, "engine is NULL");

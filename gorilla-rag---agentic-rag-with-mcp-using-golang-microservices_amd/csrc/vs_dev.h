@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/vsearch.h"
+#include "vs_kernels.h"
 
 namespace vsd {
 
@@ -77,8 +78,8 @@ struct Collection {
   // in step with `data` by every store-side call (q8_after_write)
   void* q8 = nullptr;         // (q8_cap + kPadRows) x dim int8
   float* q8_meta = nullptr;   // {dt, nt} per 32-row tile
-  float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}, then (r05) the
-                              // speculative-bound ratios by k (kQ8SpecK floats)
+  float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}, then the speculative
+                              // bound's counters and per-k state (vs_kernels.h)
   uint64_t q8_cap = 0;        // rows the int8 buffers hold
   // (r05) bumped by every store-side write (the ratios are reset with it):
   // unique in the process, so a context's record of the ratios it learned
@@ -280,11 +281,12 @@ struct DevEngine {
   DevBuf small_part;
   DevBuf q8g;  // one query on the int8 copy: workgroup lists, wave bounds, candidates
   // (r05) per collection (Collection::gen): the int8 copy generation and the
-  // k whose speculative-bound ratio this context has recorded on its stream
-  // (a later batch of this context may then use it: stream order)
+  // k this context has answered a batch of on its stream (a later batch of
+  // this context may then try the speculative bound; whether it runs is
+  // decided on the device, r06). At most 256 entries (search_mfma).
   struct SpecSeen {
     uint64_t q8_gen = 0;
-    std::bitset<130> k;
+    std::bitset<vsk::kQ8SpecK> k;
   };
   std::unordered_map<uint64_t, SpecSeen> spec_seen;
   std::vector<uint64_t> h_keys;
@@ -320,6 +322,7 @@ int collection_info(DevEngine* eng, const char* name, uint32_t* dim, uint64_t* r
                     int* dtype);
 int collection_drop(DevEngine* eng, const char* name);
 int prefilter_bytes(DevEngine* eng, const char* name, uint64_t* bytes);
+int spec_stats(DevEngine* eng, const char* name, uint64_t out[4]);
 int upsert(DevEngine* eng, const char* coll, uint64_t n, uint32_t dim, const uint64_t* rows,
            const float* vecs);
 // appends n generator rows whose global numbers are g0, g0 + stride, ...

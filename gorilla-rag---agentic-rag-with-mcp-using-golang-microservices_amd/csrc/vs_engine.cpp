@@ -133,10 +133,10 @@ hipError_t ev_end(DevEngine* eng, std::vector<EventPair>& v) {
 // Rows allocated past the capacity: the MFMA scan streams whole 32-row tiles
 // and reads (then masks) up to 31 rows beyond the last one.
 constexpr uint64_t kPadRows = 32;
-// (r05) q8_glob: {absmax, dmax, nmax, S} then the speculative-bound ratio of
-// each k in [0, kMfmaMaxK] (DESIGN.md §5 "Speculative bound")
-constexpr uint32_t kQ8SpecK = vsk::kMfmaMaxK + 1;
-constexpr size_t kQ8GlobBytes = 16 + (size_t)kQ8SpecK * 4;
+// q8_glob: {absmax, dmax, nmax, S}, then (r06) the speculative bound's
+// counters and per-k state (vs_kernels.h Q8SpecStat / Q8SpecK)
+using vsk::kQ8GlobBytes;
+using vsk::kQ8SpecK;
 // Filtered single-query searches gather the allowed rows when at most
 // 1 / kGatherDensityDen of the collection is allowed: below
 // that density the scattered 1.5-3 KB row reads stay near the streaming rate,
@@ -247,13 +247,14 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
   return rc;
 }
 
-// (r05) The speculative-bound ratios (q8_glob + 4, index k) back to unset
-// (0x7F bytes: 3.4e38, read as "no ratio"), and a new generation, so no
-// context uses a ratio learned on the rows before this write.
+// The speculative bound's per-k state back to unset (zero: no ratio, no
+// cool-down; its counters stay), and a new generation, so no context uses a
+// ratio learned on the rows before this write (r05).
 hipError_t q8_spec_reset(DevEngine* eng, Collection& c) {
   static std::atomic<uint64_t> next_gen{1};
   c.q8_gen = next_gen.fetch_add(1);
-  return hipMemsetAsync(c.q8_glob + 4, 0x7F, (size_t)kQ8SpecK * 4, eng->stream);
+  return hipMemsetAsync(vsk::q8_spec_k(c.q8_glob), 0, (size_t)kQ8SpecK * sizeof(vsk::Q8SpecK),
+                        eng->stream);
 }
 
 int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
@@ -277,6 +278,8 @@ int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
       }
       c.q8_cap = c.cap;
       VS_HIP(hipMemsetAsync(c.q8, 0, (c.cap + kPadRows) * dim, eng->stream), "zero int8 copy");
+      VS_HIP(hipMemsetAsync(vsk::q8_spec_stat(c.q8_glob), 0, sizeof(vsk::Q8SpecStat), eng->stream),
+             "zero speculative-bound counters");
     }
     VS_HIP(hipMemsetAsync(c.q8_glob, 0, 16, eng->stream), "zero int8 bounds");
     VS_HIP(q8_spec_reset(eng, c), "reset speculative-bound ratios");
@@ -710,57 +713,67 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     int8_t* q8q = eng->q8_q.as<int8_t>();
     float* q8par = eng->q8_par.as<float>();
     uint32_t* gate = (uint32_t*)(q8par + 4 * PS);
-    // (r05) Speculative bound: unfiltered bf16 batches whose k (or a larger
-    // k') has a ratio this context recorded, in this generation of the copy,
-    // start from bound = ratio x |q| instead of a sample pass. The select's
-    // answer is exact iff every query's k-th exact score reaches its bound -
-    // sigma nmax (q8_verify_record); otherwise the sample path re-runs the
-    // whole batch, every launch gated on the verdict word (*gate). Every
-    // unfiltered batch records 0.97 x its verified k-th scores per |q|.
-    const bool spec_rec = q8_spec_enabled() && !allow && k < kQ8SpecK;
+    // Speculative bound (r05): unfiltered batches whose k (or a
+    // larger k') this context has seen answered in this generation of the
+    // copy start from bound = ratio x |q| instead of a sample pass. The
+    // select's answer is exact iff every query's k-th exact score reaches its
+    // bound - sigma nmax (q8_verify_record); otherwise the sample path re-runs
+    // the whole batch, every launch gated on the verdict word. The ratio's
+    // device state decides on the device whether the try runs at all (r06:
+    // unset ratio or a cool-down after failed checks -> go = 0, the
+    // speculative launches stand down and the sample path answers).
+    const bool spec_rec =
+        q8_spec_enabled() && !(eng->flags & VS_FLAG_NO_SPECULATIVE) && !allow && k < kQ8SpecK;
     int spec_k = -1;
     DevEngine::SpecSeen* seen = nullptr;
     if (spec_rec) {
+      // a hint only (the device state decides), so bounded: dropped
+      // collections' entries go with the rest when it grows past 256
+      if (eng->spec_seen.size() > 256 && !eng->spec_seen.count(c.gen)) eng->spec_seen.clear();
       seen = &eng->spec_seen[c.gen];
       if (seen->q8_gen != c.q8_gen) seen->q8_gen = c.q8_gen, seen->k.reset();
       for (uint32_t kk = k; kk < kQ8SpecK && spec_k < 0; ++kk)
         if (seen->k[kk]) spec_k = (int)kk;
     }
-    float* ratio = c.q8_glob + 4;
+    vsk::Q8SpecK* sk = vsk::q8_spec_k(c.q8_glob);
+    vsk::Q8SpecStat* sstat = vsk::q8_spec_stat(c.q8_glob);
+    const uint32_t* verdict = gate + vsk::kGateVerdict;
+    const uint32_t* go = gate + vsk::kGateGo;
     for (uint32_t q0 = 0; q0 < nq; q0 += P8) {
       const uint32_t nv = std::min(P8, nq - q0);
       uint64_t* out = d_keys + (size_t)q0 * k;
       uint32_t L = 0;
       const uint32_t* run_if = nullptr;  // the sample path below: gated after a speculative try
       if (spec_k >= 0) {
-        const float* r_use = ratio + spec_k;
-        if (q8_spec_force_fail()) {  // (tests) the word after *gate, 0x41414141 = 12.08f
-          VS_HIP(hipMemsetAsync(gate + 1, 0x41, 4, eng->stream), "forced ratio");
-          r_use = (const float*)(gate + 1);
+        const float* r_use = &sk[spec_k].ratio;
+        const bool force = q8_spec_force_fail();
+        if (force) {  // (tests) 0x41414141 = 12.08f, far above any unit-vector score
+          VS_HIP(hipMemsetAsync(gate + vsk::kGateForced, 0x41, 4, eng->stream), "forced ratio");
+          r_use = (const float*)(gate + vsk::kGateForced);
         }
         VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream,
-                                    r_use, bound),
+                                    r_use, bound, &sk[k], sstat, force),
                "int8 queries + speculative bound");
         VS_HIP(ev_begin(eng, eng->scan_ev), "event");
         VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                         c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
-                                        eng->stream, allow),
+                                        eng->stream, allow, go),
                "int8 scan");
         VS_HIP(ev_end(eng, eng->scan_ev), "event");
         VS_HIP(ev_begin(eng, eng->merge_ev), "event");
         VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
                                      qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
-                                     q8q, allow, n_rows, eng->stream),
+                                     q8q, allow, n_rows, eng->stream, nullptr, nullptr, go),
                "int8 select");
         VS_HIP(ev_end(eng, eng->merge_ev), "event");
         VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, true, gate,
-                                            ratio + k, eng->stream),
+                                            &sk[k], sstat, eng->stream, go),
                "speculative bound check");
-        run_if = gate;
+        run_if = verdict;
       }
       // 1. sample pass(es) -> per-query lower bounds on the k-th score; the
-      // first bound launch also makes the batch's int8 queries and zeroes *gate
-      // (not behind a speculative try: *gate is then its verdict)
+      // first bound launch also makes the batch's int8 queries and zeroes the
+      // verdict word (not behind a speculative try: the word is then its verdict)
       for (uint32_t s0 = 0; s0 < nv; s0 += P) {
         const uint32_t ns = std::min(P, nv - s0);
         VS_HIP(vsk::launch_mfma_sample(X, f32, dim, n_rows, row_base, qptr(q0 + s0), ns, k, st,
@@ -795,9 +808,9 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                    q8q, allow, n_rows, eng->stream, nullptr, nullptr, run_if),
              "int8 select");
       if (!run_if) VS_HIP(ev_end(eng, eng->merge_ev), "event");
-      if (spec_rec)  // the sample path's answer is exact: record its ratios
+      if (spec_rec)  // the sample path's answer is exact: it replaces the ratio
         VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, false, nullptr,
-                                            ratio + k, eng->stream, run_if),
+                                            &sk[k], sstat, eng->stream, run_if),
                "speculative bound record");
     }
     if (spec_rec) seen->k[k] = true;
@@ -1213,6 +1226,25 @@ int prefilter_bytes(DevEngine* eng, const char* name, uint64_t* bytes) {
                                             " not found");
   std::shared_lock<std::shared_mutex> rl(c->mu);
   *bytes = c->q8 ? (c->q8_cap + kPadRows) * c->dim : 0;
+  return VS_OK;
+}
+
+// (r06) The speculative bound's counters of a collection (vs_kernels.h
+// Q8SpecStat), after every search enqueued so far on this device finished.
+int spec_stats(DevEngine* eng, const char* name, uint64_t out[4]) {
+  if (!eng || !out) return fail(VS_ERR_INVALID_ARG, "engine and out are required");
+  auto c = find_coll(eng, name);
+  if (!c) return fail(VS_ERR_NOT_FOUND, std::string("collection ") + (name ? name : "") +
+                                            " not found");
+  std::shared_lock<std::shared_mutex> rl(c->mu);
+  std::memset(out, 0, 4 * sizeof(uint64_t));
+  if (!c->q8_glob) return VS_OK;
+  VS_HIP(set_dev(eng), "set device");
+  VS_HIP(hipDeviceSynchronize(), "sync");
+  vsk::Q8SpecStat h{};
+  VS_HIP(hipMemcpy(&h, vsk::q8_spec_stat(c->q8_glob), sizeof(h), hipMemcpyDeviceToHost),
+         "read speculative-bound counters");
+  out[0] = h.tries, out[1] = h.fails, out[2] = h.skipped;
   return VS_OK;
 }
 

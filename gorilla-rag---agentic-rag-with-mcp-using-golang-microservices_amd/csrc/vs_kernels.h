@@ -286,22 +286,63 @@ hipError_t launch_q8_set_scale(float* glob, hipStream_t st);
 hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t dim,
                               const uint32_t* tiles, uint32_t t0, uint32_t ntiles, int8_t* X8,
                               float* meta, float* glob, hipStream_t st);
+// Speculative bound, device state after a collection's int8
+// bounds {absmax, dmax, nmax, S} in the same allocation (q8_glob):
+//   Q8SpecStat at byte 16: cumulative counters, zeroed when the copy is made;
+//   Q8SpecK[kQ8SpecK] at byte 48: per k, zeroed by every store-side write.
+// ratio: the k-th exact score per unit |q| a speculative batch of this k (or
+// a smaller one) starts from, 0 = unset. It is REPLACED by every batch that
+// verifies or is answered on the sample path: 0.97 x a low quantile (the
+// 1 + n/64-th smallest) of that batch's ratios, so up to n/64 outlier queries
+// (a k-th far under the others') never lower it. cool: batches left that run
+// on the sample path; backoff: the cool-down the next failed check sets
+// (1, 2, 4 ... 64 over consecutive failures; 0 again after a verified batch).
+struct Q8SpecStat {
+  unsigned long long tries;    // speculative batches run (ratio set, no cool-down)
+  unsigned long long fails;    // of those, failed their check: the sample path re-answered
+  unsigned long long skipped;  // sent to the sample path (ratio unset or a cool-down)
+  unsigned long long spare;
+};
+struct Q8SpecK {
+  float ratio;
+  uint32_t cool, backoff, pad;
+};
+constexpr uint32_t kQ8SpecK = kMfmaMaxK + 1;
+constexpr size_t kQ8SpecStatOff = 16, kQ8SpecKOff = 48;
+constexpr size_t kQ8GlobBytes = kQ8SpecKOff + (size_t)kQ8SpecK * sizeof(Q8SpecK);
+constexpr uint32_t kQ8SpecMaxBackoff = 64;
+inline Q8SpecStat* q8_spec_stat(float* glob) {
+  return (Q8SpecStat*)((char*)glob + kQ8SpecStatOff);
+}
+inline Q8SpecK* q8_spec_k(float* glob) { return (Q8SpecK*)((char*)glob + kQ8SpecKOff); }
+// The batch's control words (after q8par's kMfmaQueries x 4 floats): [0] the
+// verdict (the sample path runs unless 0), [1] a forced ratio (tests), [2] go
+// (the speculative launches run unless 0).
+constexpr uint32_t kGateVerdict = 0, kGateForced = 1, kGateGo = 2;
+
 // Queries (bf16, or fp32 when f32; nq x dim) -> int8 rows Q8 and q8par[q] =
 // {sq * S, |sq q8|, |q - sq q8|, sigma}, norms rounded up.
-// Also zeroes *gate (the batch's overflow word) ahead of the int8 pass.
-// (r05) With ratio / bound: also bound[q] = *ratio x |q| (-inf while *ratio is
-// unset, >= 1e38): the speculative bound of DESIGN.md §5.
+// Also zeroes gate[kGateVerdict] ahead of the int8 pass.
+// Speculative form (spec_k non-null): also bound[q] = *ratio x |q|, and the
+// batch's go / verdict words: go = 1, verdict = 0 when *ratio is set and (unless
+// force) spec_k has no cool-down pending; else go = 0, verdict = 1 (the
+// sample path answers) and one cool-down batch is counted off.
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st,
-                           const float* ratio = nullptr, float* bound = nullptr);
-// (r05) After a batch's select: check (a speculative batch) raises *fail when
-// a query's k-th exact score is under its bound - sigma nmax; verified queries
-// lower *ratio to 0.97 x their k-th score per unit |q|. run_if: stand down
-// unless *run_if.
+                           const float* ratio = nullptr, float* bound = nullptr,
+                           Q8SpecK* spec_k = nullptr, Q8SpecStat* stat = nullptr,
+                           bool force = false);
+// After a batch's select (one workgroup; nq <= kMfmaQueries). check (a
+// speculative batch): a query whose k-th exact score is under its bound -
+// sigma nmax fails it; any failure sets gate[kGateVerdict] (the sample path
+// re-answers the batch), counts it and sets spec_k's cool-down / back-off; a
+// verified batch clears the back-off. A verified batch, or any batch with
+// check off (the sample path's answer), replaces spec_k->ratio (see
+// Q8SpecK). run_if: stand down unless *run_if.
 hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
                                    const float* bound, const float* q8par, const float* glob,
-                                   bool check, uint32_t* fail, float* ratio, hipStream_t st,
-                                   const uint32_t* run_if = nullptr);
+                                   bool check, uint32_t* gate, Q8SpecK* spec_k, Q8SpecStat* stat,
+                                   hipStream_t st, const uint32_t* run_if = nullptr);
 // launch_sample_bound (nq_bound queries) and launch_q8_query (nq queries) as
 // one launch: the int8 path's per-batch prep, one dispatch fewer (r04).
 hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,

@@ -141,11 +141,36 @@ __global__ __launch_bounds__(256) void q8_quantize_kernel(
   }
 }
 
+// A ratio a speculative batch may start from: set (> 0) and finite.
+__device__ __forceinline__ bool ratio_set(float r) { return r > 0.f && r < 1e38f; }
+
+// (r06) The speculative try's go / verdict words (vs_kernels.h Q8SpecK): one
+// thread, before any launch of the batch reads them.
+__device__ __forceinline__ void spec_decide(const float* __restrict__ ratio, Q8SpecK* __restrict__ sk,
+                                            Q8SpecStat* __restrict__ stat, uint32_t* __restrict__ gate,
+                                            bool force) {
+  bool go = ratio_set(*ratio);
+  if (go && !force) {
+    // a pending cool-down: count one batch off it (never below 0, whatever
+    // other contexts do meanwhile) and take the sample path
+    uint32_t c = __hip_atomic_load(&sk->cool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (c != 0u) {
+      const uint32_t o = atomicCAS(&sk->cool, c, c - 1u);
+      if (o == c) break;
+      c = o;
+    }
+    go = c == 0u;
+  }
+  gate[kGateVerdict] = go ? 0u : 1u;
+  gate[kGateGo] = go ? 1u : 0u;
+  atomicAdd(go ? &stat->tries : &stat->skipped, 1ull);
+}
+
 // One wave per query (bf16 queries of a bf16 collection, or the fp32
 // preprocessed queries of an fp32 one).
 // (r05) With `ratio` (a collection's learned k-th score per unit |q|, DESIGN.md
-// §5 "Speculative bound"), also bound[i] = ratio x |q|, or -inf while the
-// ratio is unset (>= 1e38: the table's 0x7F-byte fill).
+// §5 "Speculative bound"), also bound[i] = ratio x |q| (-inf while the ratio
+// is unset: the batch then stands down, spec_decide).
 template <bool F32>
 __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restrict__ qb,
                                                uint32_t nq, uint32_t dim,
@@ -153,8 +178,16 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
                                                int8_t* __restrict__ q8, float* __restrict__ q8par,
                                                uint32_t* __restrict__ gate,
                                                const float* __restrict__ ratio = nullptr,
-                                               float* __restrict__ bound = nullptr) {
-  if (gate && blk == 0 && threadIdx.x == 0) *gate = 0u;
+                                               float* __restrict__ bound = nullptr,
+                                               Q8SpecK* __restrict__ sk = nullptr,
+                                               Q8SpecStat* __restrict__ stat = nullptr,
+                                               bool force = false) {
+  if (gate && blk == 0 && threadIdx.x == 0) {
+    if (sk)
+      spec_decide(ratio, sk, stat, gate, force);
+    else
+      gate[kGateVerdict] = 0u;
+  }
   const uint32_t i = blk * 4 + (threadIdx.x >> 6);
   if (i >= nq) return;
   const int lane = threadIdx.x & 63;
@@ -196,7 +229,7 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
     p[3] = sigma;
     if (bound) {
       const float r = *ratio;
-      bound[i] = r < 1e38f ? r * (float)sqrt(nn) : -INFINITY;
+      bound[i] = ratio_set(r) ? r * (float)sqrt(nn) : -INFINITY;
     }
   }
 }
@@ -208,36 +241,77 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ 
                                                        float* __restrict__ q8par,
                                                        uint32_t* __restrict__ gate,
                                                        const float* __restrict__ ratio,
-                                                       float* __restrict__ bound) {
-  q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate, ratio, bound);
+                                                       float* __restrict__ bound,
+                                                       Q8SpecK* __restrict__ sk,
+                                                       Q8SpecStat* __restrict__ stat, uint32_t force) {
+  q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate, ratio, bound, sk, stat,
+                      force != 0u);
 }
 
-// (r05) After a batch's select: per query, its k-th key's exact score s
-// against the bound b it ran with. A speculative batch is exact iff s reaches
-// b - sigma nmax for every query (every row the pass left out has U below
-// that, so below s; rows the select left out are beaten by the quarter
-// bound's k rows): otherwise *fail is raised and the batch re-runs on the
-// sample path, gated on it. Verified queries with s > 0 lower the
-// collection's ratio for this k to 0.97 s / |q| (atomicMin on the float
-// bits: positive floats order as them). run_if: stand down unless *run_if
-// (the record after a fallback).
-__global__ __launch_bounds__(256) void q8_verify_record_kernel(
+// After a batch's select (one workgroup, thread q = query q): its k-th key's
+// exact score s against the bound b it ran with. A speculative batch is exact
+// iff s reaches b - sigma nmax for every query (every row the pass left out
+// has U below that, so below s; rows the select left out are beaten by the
+// quarter bound's k rows): otherwise the verdict word is raised and the batch
+// re-runs on the sample path, gated on it (r05).
+// (r06) What the batch teaches the next one: r05 lowered
+// one running minimum with every verified query, so a single off-topic query
+// pinned the bound of every later batch near zero until the next write. Now a
+// verified (or sample-path) batch REPLACES the ratio with 0.97 x the
+// (1 + n/64)-th smallest of its queries' s / |q| (s > 0): up to n/64 outliers
+// a batch are ignored, and whatever a batch teaches lasts one batch. A failed
+// check counts itself and starts a cool-down (back-off doubling to 64 batches
+// over consecutive failures), so traffic whose every batch holds an outlier
+// settles on the sample path instead of paying for two passes a batch.
+// run_if: stand down unless *run_if.
+__global__ __launch_bounds__(kMfmaQueries) void q8_verify_record_kernel(
     const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint32_t dim,
     const float* __restrict__ bound, const float* __restrict__ q8par,
-    const float* __restrict__ glob, uint32_t check, uint32_t* __restrict__ fail,
-    float* __restrict__ ratio, const uint32_t* __restrict__ run_if) {
+    const float* __restrict__ glob, uint32_t check, uint32_t* __restrict__ gate,
+    Q8SpecK* __restrict__ sk, Q8SpecStat* __restrict__ stat, const uint32_t* __restrict__ run_if) {
   if (run_if && *run_if == 0u) return;
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  const uint64_t key = keys[(size_t)q * k + k - 1];
-  const float s = key ? vs::key_score(key) : -INFINITY;
-  const float sig = q8par[4 * (size_t)q + 3];
-  const bool ok = !check || (key != 0 && s >= bound[q] - sig * glob[2]);
-  if (!ok) atomicAdd(fail, 1u);
-  // |q| from sigma = (4 dim + 64) 2^-24 |q| (1 + 2^-20) (vs_bound_dev.h q8_sigma)
-  const float qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
-  if (ok && key != 0 && s > 0.f && qn > 0.f)
-    atomicMin((unsigned int*)ratio, __float_as_uint(0.97f * s / qn));
+  __shared__ float rq[kMfmaQueries];
+  __shared__ float pick;
+  const uint32_t q = threadIdx.x;
+  bool ok = true;
+  float r = INFINITY;  // this query's ratio; +inf: none (no k-th, s <= 0, zero query)
+  if (q < nq) {
+    const uint64_t key = keys[(size_t)q * k + k - 1];
+    const float s = key ? vs::key_score(key) : -INFINITY;
+    const float sig = q8par[4 * (size_t)q + 3];
+    ok = !check || (key != 0 && s >= bound[q] - sig * glob[2]);
+    // |q| from sigma = (4 dim + 64) 2^-24 |q| (1 + 2^-20) (vs_bound_dev.h q8_sigma)
+    const float qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
+    if (key != 0 && s > 0.f && qn > 0.f) r = s / qn;
+  }
+  rq[q] = r;
+  if (q == 0) pick = INFINITY;
+  const int nbad = __syncthreads_count(!ok);
+  const int nvalid = __syncthreads_count(r < INFINITY);
+  // the m-th smallest ratio (ties by query index), m = 1 + nvalid / 64
+  if (r < INFINITY) {
+    const int m = 1 + nvalid / 64;
+    int rank = 0;
+    for (uint32_t j = 0; j < kMfmaQueries; ++j) {
+      const float o = rq[j];
+      rank += (o < r) || (o == r && j < q);
+    }
+    if (rank == m - 1) pick = r;
+  }
+  __syncthreads();
+  if (q != 0) return;
+  if (check) {
+    if (nbad) {
+      gate[kGateVerdict] = 1u;
+      atomicAdd(&stat->fails, 1ull);
+      const uint32_t b = sk->backoff;
+      sk->cool = b;
+      sk->backoff = b ? (2 * b < kQ8SpecMaxBackoff ? 2 * b : kQ8SpecMaxBackoff) : 1u;
+      return;  // the sample path's record replaces the ratio
+    }
+    sk->backoff = 0u;
+  }
+  if (pick < INFINITY) sk->ratio = 0.97f * pick;
 }
 
 // Workgroups [0, nq_bound): the sample bound of query blockIdx.x; the rest:
@@ -293,25 +367,28 @@ hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t
 
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st,
-                           const float* ratio, float* bound) {
-  if (dim % 128 || dim == 0 || (bound && !ratio)) return hipErrorInvalidValue;
+                           const float* ratio, float* bound, Q8SpecK* spec_k, Q8SpecStat* stat,
+                           bool force) {
+  if (dim % 128 || dim == 0 || (bound && !ratio) || (spec_k && (!ratio || !stat || !gate)))
+    return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   if (f32)
     hipLaunchKernelGGL(q8_query_kernel<true>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
-                       glob, q8, q8par, gate, ratio, bound);
+                       glob, q8, q8par, gate, ratio, bound, spec_k, stat, force ? 1u : 0u);
   else
     hipLaunchKernelGGL(q8_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
-                       glob, q8, q8par, gate, ratio, bound);
+                       glob, q8, q8par, gate, ratio, bound, spec_k, stat, force ? 1u : 0u);
   return hipGetLastError();
 }
 
 hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
                                    const float* bound, const float* q8par, const float* glob,
-                                   bool check, uint32_t* fail, float* ratio, hipStream_t st,
-                                   const uint32_t* run_if) {
-  if (nq == 0 || k == 0 || !ratio || (check && !fail)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(q8_verify_record_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, k,
-                     dim, bound, q8par, glob, check ? 1u : 0u, fail, ratio, run_if);
+                                   bool check, uint32_t* gate, Q8SpecK* spec_k, Q8SpecStat* stat,
+                                   hipStream_t st, const uint32_t* run_if) {
+  if (nq == 0 || nq > kMfmaQueries || k == 0 || !spec_k || !stat || (check && !gate))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(q8_verify_record_kernel, dim3(1), dim3(kMfmaQueries), 0, st, keys, nq, k, dim,
+                     bound, q8par, glob, check ? 1u : 0u, gate, spec_k, stat, run_if);
   return hipGetLastError();
 }
 

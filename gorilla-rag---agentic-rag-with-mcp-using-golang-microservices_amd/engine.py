@@ -39,6 +39,7 @@ FLAG_TIMING_SAMPLE = 4
 FLAG_PLACE_COLLECTIONS = 8
 FLAG_ENGINE_PER_SHARD = 16
 FLAG_NO_PREFILTER = 32
+FLAG_NO_SPECULATIVE = 64
 
 # Every function include/vsearch.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -51,7 +52,7 @@ EXPORTS = (
     "vs_filter_create", "vs_filter_drop", "vs_search_filter_id", "vs_open_multi",
     "vs_engine_layout", "vs_comm_unique_id", "vs_comm_init", "vs_gather_merge_keys",
     "vs_copy_last_error", "vs_build_id", "vs_collection_placement", "vs_runtime_check",
-    "vs_collection_prefilter_bytes",
+    "vs_collection_prefilter_bytes", "vs_collection_spec_stats",
 )
 COMM_ID_BYTES = 128
 
@@ -124,6 +125,7 @@ def load_library(path: str = LIB_PATH):
         "vs_engine_layout": ([vp, vp, vp], i32),
         "vs_collection_placement": ([vp, cp, vp], i32),
         "vs_collection_prefilter_bytes": ([vp, cp, vp], i32),
+        "vs_collection_spec_stats": ([vp, cp, vp], i32),
         "vs_close": ([vp], None),
         "vs_device_count": ([], i32),
         "vs_collection_create": ([vp, cp, u32, i32, i32, u64, u64], i32),
@@ -214,19 +216,22 @@ class VectorEngine:
     (VS_FLAG_PLACE_COLLECTIONS); ``engine_per_shard`` then gives every entry
     of ``shards`` its own device engine even where ordinals repeat
     (VS_FLAG_ENGINE_PER_SHARD). ``prefilter=False`` keeps no int8 copies
-    (VS_FLAG_NO_PREFILTER: batched bf16 searches run the bf16 pass)."""
+    (VS_FLAG_NO_PREFILTER: batched bf16 searches run the bf16 pass);
+    ``speculative=False`` runs every int8 batch on its sample pass
+    (VS_FLAG_NO_SPECULATIVE, DESIGN.md §5 "Speculative bound")."""
 
     def __init__(self, device: int = -1, timing: bool = False, timing_merge: bool = False,
                  timing_sample: bool = False, shards: Optional[Sequence[int]] = None,
                  place_collections: bool = False, engine_per_shard: bool = False,
-                 prefilter: bool = True):
+                 prefilter: bool = True, speculative: bool = True):
         L = load_library()
         flags = ((FLAG_TIMING if timing else 0) |
                  (FLAG_TIMING_MERGE if timing and timing_merge else 0) |
                  (FLAG_TIMING_SAMPLE if timing and timing_sample else 0) |
                  (FLAG_PLACE_COLLECTIONS if place_collections else 0) |
                  (FLAG_ENGINE_PER_SHARD if engine_per_shard else 0) |
-                 (0 if prefilter else FLAG_NO_PREFILTER))
+                 (0 if prefilter else FLAG_NO_PREFILTER) |
+                 (0 if speculative else FLAG_NO_SPECULATIVE))
         h = ctypes.c_void_p()
         if shards is None:
             cfg = _Config(device, flags)
@@ -257,6 +262,16 @@ class VectorEngine:
         b = ctypes.c_uint64()
         _check(self._L.vs_collection_prefilter_bytes(self._h, name.encode(), ctypes.byref(b)))
         return int(b.value)
+
+    def spec_stats(self, name: str) -> dict:
+        """Counters of the collection's speculative bound (vs_collection_spec_stats,
+        DESIGN.md §5): batches tried, of those failed (the sample path
+        re-answered: the bench's `spec_fallbacks`), and batches a cool-down or
+        an unset ratio sent to the sample path. Waits for the device."""
+        a = (ctypes.c_uint64 * 4)()
+        _check(self._L.vs_collection_spec_stats(self._h, name.encode(), a))
+        return {"tries": int(a[0]), "fallbacks": int(a[1]), "skipped": int(a[2])}
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.vs_close(self._h)

@@ -113,6 +113,10 @@ typedef struct vs_config {
  * an int8 MFMA pass whose candidates are rescored exactly from the bf16 rows:
  * the same keys as the bf16 pass ("int8 prefilter"). */
 #define VS_FLAG_NO_PREFILTER 32u
+/* (r06) No speculative bound for this engine's batched int8
+ * searches: every batch runs the sample pass for its bound. Same keys either
+ * way; the environment's VS_Q8_SPEC=0 does this for every engine. */
+#define VS_FLAG_NO_SPECULATIVE 64u
 
 /* ---- engine lifetime ---------------------------------------------------- */
 
@@ -176,6 +180,15 @@ int vs_collection_drop(vs_engine* eng, const char* name);
 /* HBM bytes of the collection's int8 prefilter copy (summed over shards; 0 =
  * none: its batched searches run the bf16 pass). See VS_FLAG_NO_PREFILTER. */
 int vs_collection_prefilter_bytes(vs_engine* eng, const char* name, uint64_t* bytes);
+
+/* (r06, diagnostics; no reference counterpart) Counters of the speculative
+ * bound of the collection's batched int8 searches, summed over
+ * shards, after every search enqueued so far on its devices has finished:
+ * out[0] speculative batches run, out[1] of those that failed their check (the
+ * sample path re-answered them: `spec_fallbacks`), out[2] batches a cool-down
+ * or an unset ratio sent to the sample path, out[3] 0. All zero without an
+ * int8 copy. Counted since the copy was (re)built. */
+int vs_collection_spec_stats(vs_engine* eng, const char* name, uint64_t out[4]);
 
 /* ---- store side ----------------------------------------------------------- */
 

@@ -1,0 +1,149 @@
+"""The speculative bound under off-topic queries (r06).
+
+r05's ratio was one running minimum over every verified query, so a single
+query whose k-th score is far under the rest (an off-topic question against
+clustered embeddings: the traffic retrieval-service sends one query at a
+time, rag/retrieval-service/main.go:219-276) pinned the bound of every later
+batch near zero until the next write: the answers stayed exact, the int8 pass
+then admitted whole clusters. Now a batch REPLACES the ratio with a low
+quantile of its own queries' ratios (csrc/vs_q8.hip q8_verify_record_kernel)
+and a failed check backs off to the sample path.
+
+A clustered corpus (64 Gaussian clusters, unit rows, bf16, inner product) is
+searched in one process by two engines over the same rows: speculation on
+(the default) and off (VS_FLAG_NO_SPECULATIVE, the sample path every batch).
+The sequence: on-topic batches (the ratio is learned), ONE batch mixing
+on-topic queries with a few near-orthogonal ones, then more fresh on-topic
+batches, then a run of batches that all carry outliers. Checked: keys
+bit-identical between the engines on every batch, the oracle on the outliers
+and on on-topic queries after them, and -- the point -- no on-topic batch
+after the outlier runs more than 2% slower with speculation on than off
+(device events around each batch, engines interleaved batch by batch).
+Anchor: Points.Search, rag/vector-service/main.go:249-254.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+_CLIFF = r"""
+import sys, os, json
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import __graft_entry__ as ge
+from oracle import oracle as orc
+pkg = ge.load_package()
+n, dim, C, B, k = int(os.environ.get("T_ROWS", "2000000")), 768, 64, 256, 10
+g = torch.Generator(device="cuda").manual_seed(2026)
+cent = torch.randn((C, dim), device="cuda", generator=g)
+cent /= cent.norm(dim=1, keepdim=True)
+def clustered(m, noise=1.0):
+    lab = torch.randint(0, C, (m,), device="cuda", generator=g)
+    v = cent[lab] + noise * torch.randn((m, dim), device="cuda", generator=g) / dim ** 0.5
+    return v / v.norm(dim=1, keepdim=True)
+X = torch.cat([clustered(200_000) for _ in range(n // 200_000)]).cpu().numpy()
+# near-orthogonal to every cluster centre: the centres' span projected out
+Qc, _ = torch.linalg.qr(cent.T)
+def outliers(m):
+    v = torch.randn((m, dim), device="cuda", generator=g)
+    v = v - (v @ Qc) @ Qc.T
+    return v / v.norm(dim=1, keepdim=True)
+on = pkg.VectorEngine(device=0)
+off = pkg.VectorEngine(device=0, speculative=False)
+for e in (on, off):
+    e.create_collection("c", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16, n)
+    for r0 in range(0, n, 500_000):
+        e.upsert("c", np.arange(r0, min(n, r0 + 500_000), dtype=np.uint64), X[r0:r0 + 500_000])
+assert on.prefilter_bytes("c") > 0
+stream = torch.cuda.current_stream()
+keys = {e: torch.empty((B, k), dtype=torch.int64, device="cuda") for e in (on, off)}
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+def run(e, q):
+    ev[0].record(stream)
+    e.search_keys("c", q.data_ptr(), B, dim, k, keys[e].data_ptr(), stream.cuda_stream)
+    ev[1].record(stream)
+    ev[1].synchronize()
+    return ev[0].elapsed_time(ev[1]), keys[e].cpu().numpy().view(np.uint64).copy()
+out = {"batches": [], "mismatch": [], "parity": [], "stats": {}}
+kept = []  # (phase, queries, keys) for the oracle
+def batch(phase, q):
+    i = len(out["batches"])
+    order = (on, off) if i % 2 == 0 else (off, on)
+    t = {}
+    ks = {}
+    for e in order:
+        t[e], ks[e] = run(e, q)
+    if not np.array_equal(ks[on], ks[off]):
+        out["mismatch"].append(i)
+    out["batches"].append({"phase": phase, "on_ms": t[on], "off_ms": t[off]})
+    return ks[on]
+# warm both engines and the learned ratio on on-topic batches
+for _ in range(6):
+    batch("warm", clustered(B))
+# one batch with a few off-topic queries among on-topic ones
+nout = int(os.environ.get("T_OUTLIERS", "3"))
+q = torch.cat([clustered(B - nout), outliers(nout)])
+kq = batch("outlier", q)
+kept.append(("outlier", q[B - nout - 2:].cpu().numpy(), kq[B - nout - 2:]))
+# fresh on-topic batches after it
+for i in range(10):
+    q = clustered(B)
+    kq = batch("after", q)
+    if i in (0, 5):
+        kept.append(("after", q[:3].cpu().numpy(), kq[:3]))
+# every batch carrying outliers (back-off regime)
+for i in range(int(os.environ.get("T_MIXED", "16"))):
+    q = torch.cat([clustered(B - nout), outliers(nout)])
+    batch("mixed", q)
+out["stats"] = {"on": on.spec_stats("c"), "off": off.spec_stats("c")}
+# the oracle on the kept queries (rows as stored: bf16)
+Xb = orc.preprocess(X, False, True)
+for phase, Q, kk in kept:
+    Q = orc.preprocess(Q, False, True)
+    s, r, c = pkg.keys_decode(kk)
+    _, s64, rr, cc = orc.search(Xb, Q, k)
+    resc = orc.rescore(Xb, Q, r, c)
+    bad = orc.check_topk(s, r, c, s64, rr, cc, resc, 1e-5)
+    if bad:
+        out["parity"].append([phase, bad[:3]])
+on.close(); off.close()
+print(json.dumps(out))
+"""
+
+
+def _run(env):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, **env)
+    p = subprocess.run([sys.executable, "-c", "ROOT = %r\n" % root + _CLIFF], env=e, cwd=root,
+                       capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_outlier_queries_do_not_poison_later_batches():
+    r = _run({})
+    rec = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(rec):
+        with open(os.path.join(rec, "spec_cliff.json"), "w") as f:
+            json.dump(r, f)
+    assert r["mismatch"] == [], r["mismatch"]
+    assert r["parity"] == [], r["parity"]
+    b = r["batches"]
+    after = [x for x in b if x["phase"] == "after"]
+    ratios = [x["on_ms"] / x["off_ms"] for x in after]
+    # no on-topic batch after the outlier pays for it (r05's running minimum
+    # made every one of them several times slower)
+    assert max(ratios) <= 1.02, ratios
+    st = r["stats"]["on"]
+    # the outlier batch (and the first mixed ones) failed their check; the
+    # back-off then sent most mixed batches to the sample path
+    assert st["fallbacks"] >= 1 and st["skipped"] >= 1, st
+    assert r["stats"]["off"]["tries"] == 0, r["stats"]
+    mixed = [x for x in b if x["phase"] == "mixed"]
+    tail = mixed[len(mixed) // 2:]
+    assert sum(x["on_ms"] for x in tail) <= 1.25 * sum(x["off_ms"] for x in tail), tail
