@@ -80,6 +80,13 @@ struct Collection {
   float* q8_meta = nullptr;   // {dt, nt} per 32-row tile
   float* q8_glob = nullptr;   // {absmax, dmax, nmax, S}, then the speculative
                               // bound's counters and per-k state (vs_kernels.h)
+  // (r06) the speculative bound's advice to the host, coherent mapped pinned
+  // memory the device writes (vs_kernels.h Q8SpecK): [k] 1 = the bound is
+  // loose for k (enqueue the sample path alone), [kQ8SpecK + k] batches of k
+  // left in a cool-down after a failed check (counted off by the host)
+  uint32_t* q8_advice = nullptr;
+  uint32_t* q8_advice_dev = nullptr;
+  std::atomic<uint64_t> spec_host_skips{0};  // batches the advice kept off a try
   uint64_t q8_cap = 0;        // rows the int8 buffers hold
   // (r05) bumped by every store-side write (the ratios are reset with it):
   // unique in the process, so a context's record of the ratios it learned
@@ -92,7 +99,9 @@ struct Collection {
     if (q8) (void)hipFree(q8);
     if (q8_meta) (void)hipFree(q8_meta);
     if (q8_glob) (void)hipFree(q8_glob);
+    if (q8_advice) (void)hipHostFree(q8_advice);
     q8 = nullptr, q8_meta = nullptr, q8_glob = nullptr, q8_cap = 0, q8_scaled_at = 0;
+    q8_advice = q8_advice_dev = nullptr;
   }
   ~Collection() {
     if (data) (void)hipFree(data);
@@ -287,6 +296,7 @@ struct DevEngine {
   struct SpecSeen {
     uint64_t q8_gen = 0;
     std::bitset<vsk::kQ8SpecK> k;
+    uint8_t loose_tick[vsk::kQ8SpecK] = {};  // batches while the advice said loose
   };
   std::unordered_map<uint64_t, SpecSeen> spec_seen;
   std::vector<uint64_t> h_keys;

@@ -145,6 +145,9 @@ constexpr uint64_t kGatherDensityDen = 8;
 // Per-query launch overhead of a gathered scan (scan + merge launches,
 // ~10 us) in bytes of HBM streaming, for the batch decision in search_core.
 constexpr uint64_t kGatherCallBytes = 64ull << 20;
+// While a k's speculative bound is judged loose, one batch in kLooseRecord
+// records (and re-judges) it; the others run the sample path alone.
+constexpr uint8_t kLooseRecord = 8;
 // Collection bytes from which a batched host search is "heavy" (heavy_search).
 constexpr uint64_t kHeavyBytes = 256ull << 20;
 // Smallest batch of an fp32 collection that takes the MFMA pass.
@@ -253,6 +256,7 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
 hipError_t q8_spec_reset(DevEngine* eng, Collection& c) {
   static std::atomic<uint64_t> next_gen{1};
   c.q8_gen = next_gen.fetch_add(1);
+  for (uint32_t k = 0; k < 2 * kQ8SpecK; ++k) __atomic_store_n(&c.q8_advice[k], 0u, __ATOMIC_RELAXED);
   return hipMemsetAsync(vsk::q8_spec_k(c.q8_glob), 0, (size_t)kQ8SpecK * sizeof(vsk::Q8SpecK),
                         eng->stream);
 }
@@ -271,6 +275,10 @@ int q8_after_write_impl(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
       hipError_t e = hipMalloc(&c.q8, (c.cap + kPadRows) * dim);
       if (e == hipSuccess) e = hipMalloc((void**)&c.q8_meta, tiles * 8);
       if (e == hipSuccess) e = hipMalloc((void**)&c.q8_glob, kQ8GlobBytes);
+      if (e == hipSuccess)
+        e = hipHostMalloc((void**)&c.q8_advice, 2 * kQ8SpecK * 4,
+                          hipHostMallocCoherent | hipHostMallocMapped);
+      if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c.q8_advice_dev, c.q8_advice, 0);
       if (e != hipSuccess) {
         (void)hipGetLastError();
         c.q8_free();
@@ -725,6 +733,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     const bool spec_rec =
         q8_spec_enabled() && !(eng->flags & VS_FLAG_NO_SPECULATIVE) && !allow && k < kQ8SpecK;
     int spec_k = -1;
+    bool record = spec_rec;  // the sample path's answer teaches the ratio
     DevEngine::SpecSeen* seen = nullptr;
     if (spec_rec) {
       // a hint only (the device state decides), so bounded: dropped
@@ -734,6 +743,25 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
       if (seen->q8_gen != c.q8_gen) seen->q8_gen = c.q8_gen, seen->k.reset();
       for (uint32_t kk = k; kk < kQ8SpecK && spec_k < 0; ++kk)
         if (seen->k[kk]) spec_k = (int)kk;
+      // The device's advice (vs_kernels.h Q8SpecK). Loose: the last
+      // sample-path record found the bound loose for this k, so enqueue the
+      // sample path alone and its record only every kLooseRecord-th batch
+      // (which re-judges it). A cool-down after a failed check: the sample
+      // path and its record, one batch counted off.
+      if (spec_k >= 0 && !q8_spec_force_fail()) {
+        uint32_t* cool = &c.q8_advice[kQ8SpecK + k];
+        uint32_t n = __atomic_load_n(cool, __ATOMIC_RELAXED);
+        while (n && !__atomic_compare_exchange_n(cool, &n, n - 1, false, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED)) {
+        }
+        if (__atomic_load_n(&c.q8_advice[k], __ATOMIC_RELAXED) != 0u) {
+          spec_k = -1;
+          record = seen->loose_tick[k]++ % kLooseRecord == 0;
+        } else if (n) {
+          spec_k = -1;
+        }
+        if (spec_k < 0) c.spec_host_skips.fetch_add(1, std::memory_order_relaxed);
+      }
     }
     vsk::Q8SpecK* sk = vsk::q8_spec_k(c.q8_glob);
     vsk::Q8SpecStat* sstat = vsk::q8_spec_stat(c.q8_glob);
@@ -767,7 +795,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                "int8 select");
         VS_HIP(ev_end(eng, eng->merge_ev), "event");
         VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, true, gate,
-                                            &sk[k], sstat, eng->stream, go),
+                                            &sk[k], sstat, c.q8_advice_dev + k, eng->stream, go),
                "speculative bound check");
         run_if = verdict;
       }
@@ -808,9 +836,10 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                    q8q, allow, n_rows, eng->stream, nullptr, nullptr, run_if),
              "int8 select");
       if (!run_if) VS_HIP(ev_end(eng, eng->merge_ev), "event");
-      if (spec_rec)  // the sample path's answer is exact: it replaces the ratio
+      if (record)  // the sample path's answer is exact: it replaces the ratio
         VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, false, nullptr,
-                                            &sk[k], sstat, eng->stream, run_if),
+                                            &sk[k], sstat, c.q8_advice_dev + k, eng->stream,
+                                            run_if),
                "speculative bound record");
     }
     if (spec_rec) seen->k[k] = true;
@@ -1244,7 +1273,8 @@ int spec_stats(DevEngine* eng, const char* name, uint64_t out[4]) {
   vsk::Q8SpecStat h{};
   VS_HIP(hipMemcpy(&h, vsk::q8_spec_stat(c->q8_glob), sizeof(h), hipMemcpyDeviceToHost),
          "read speculative-bound counters");
-  out[0] = h.tries, out[1] = h.fails, out[2] = h.skipped;
+  out[0] = h.tries, out[1] = h.fails;
+  out[2] = h.skipped + c->spec_host_skips.load(std::memory_order_relaxed);
   return VS_OK;
 }
 

@@ -294,23 +294,32 @@ hipError_t launch_q8_quantize(const void* X, bool f32, uint32_t n_rows, uint32_t
 // a smaller one) starts from, 0 = unset. It is REPLACED by every batch that
 // verifies or is answered on the sample path: 0.97 x a low quantile (the
 // 1 + n/64-th smallest) of that batch's ratios, so up to n/64 outlier queries
-// (a k-th far under the others') never lower it. cool: batches left that run
-// on the sample path; backoff: the cool-down the next failed check sets
-// (1, 2, 4 ... 64 over consecutive failures; 0 again after a verified batch).
+// (a k-th far under the others') never lower it (r06). backoff: the cool-down
+// the next failed check sets (0, 1, 2, 4 ... 64 batches on the sample path
+// over consecutive failures; 0 again after a verified batch), handed to the
+// host through its advice words (launch_q8_verify_record).
+// loose: set by a sample-path batch when ratio x |q| falls under more than a
+// quarter of its queries' sample bounds -- a single ratio cannot follow the
+// queries' own k-th scores (clustered rows), so speculating would admit more
+// rows than the sample pass does; no speculative batch runs while it is set.
+// since: speculative batches since the last sample-path one; every
+// kQ8SpecProbe-th runs the sample path instead, which re-judges `loose`.
 struct Q8SpecStat {
-  unsigned long long tries;    // speculative batches run (ratio set, no cool-down)
+  unsigned long long tries;    // speculative batches run
   unsigned long long fails;    // of those, failed their check: the sample path re-answered
-  unsigned long long skipped;  // sent to the sample path (ratio unset or a cool-down)
+  unsigned long long skipped;  // sent to the sample path by the device (ratio unset,
+                               // loose or a probe; host-side skips: Collection)
   unsigned long long spare;
 };
 struct Q8SpecK {
   float ratio;
-  uint32_t cool, backoff, pad;
+  uint32_t backoff, loose, since, pad[4];
 };
 constexpr uint32_t kQ8SpecK = kMfmaMaxK + 1;
 constexpr size_t kQ8SpecStatOff = 16, kQ8SpecKOff = 48;
 constexpr size_t kQ8GlobBytes = kQ8SpecKOff + (size_t)kQ8SpecK * sizeof(Q8SpecK);
 constexpr uint32_t kQ8SpecMaxBackoff = 64;
+constexpr uint32_t kQ8SpecProbe = 16;
 inline Q8SpecStat* q8_spec_stat(float* glob) {
   return (Q8SpecStat*)((char*)glob + kQ8SpecStatOff);
 }
@@ -324,9 +333,9 @@ constexpr uint32_t kGateVerdict = 0, kGateForced = 1, kGateGo = 2;
 // {sq * S, |sq q8|, |q - sq q8|, sigma}, norms rounded up.
 // Also zeroes gate[kGateVerdict] ahead of the int8 pass.
 // Speculative form (spec_k non-null): also bound[q] = *ratio x |q|, and the
-// batch's go / verdict words: go = 1, verdict = 0 when *ratio is set and (unless
-// force) spec_k has no cool-down pending; else go = 0, verdict = 1 (the
-// sample path answers) and one cool-down batch is counted off.
+// batch's go / verdict words: go = 1, verdict = 0 when *ratio is set and
+// (unless force) spec_k is neither loose nor due a probe; else go = 0,
+// verdict = 1 (the sample path answers).
 hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, const float* glob,
                            int8_t* q8, float* q8par, uint32_t* gate, hipStream_t st,
                            const float* ratio = nullptr, float* bound = nullptr,
@@ -335,14 +344,19 @@ hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, c
 // After a batch's select (one workgroup; nq <= kMfmaQueries). check (a
 // speculative batch): a query whose k-th exact score is under its bound -
 // sigma nmax fails it; any failure sets gate[kGateVerdict] (the sample path
-// re-answers the batch), counts it and sets spec_k's cool-down / back-off; a
+// re-answers the batch), counts it and starts a cool-down (spec_k->backoff); a
 // verified batch clears the back-off. A verified batch, or any batch with
-// check off (the sample path's answer), replaces spec_k->ratio (see
-// Q8SpecK). run_if: stand down unless *run_if.
+// check off (the sample path's answer: `bound` then holds its sample bounds,
+// which also re-judge spec_k->loose), replaces spec_k->ratio (see Q8SpecK).
+// advice (nullable; coherent mapped host memory, this k's word of the
+// collection's 2 x kQ8SpecK): the record stores loose (1: the host enqueues
+// the sample path alone), a failed check stores the cool-down's length at
+// advice[kQ8SpecK] (the host counts it off). run_if: stand down unless *run_if.
 hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
                                    const float* bound, const float* q8par, const float* glob,
                                    bool check, uint32_t* gate, Q8SpecK* spec_k, Q8SpecStat* stat,
-                                   hipStream_t st, const uint32_t* run_if = nullptr);
+                                   uint32_t* advice, hipStream_t st,
+                                   const uint32_t* run_if = nullptr);
 // launch_sample_bound (nq_bound queries) and launch_q8_query (nq queries) as
 // one launch: the int8 path's per-batch prep, one dispatch fewer (r04).
 hipError_t launch_sample_bound_q8(const float* tmax, uint32_t m, uint32_t nq_bound, uint32_t k,

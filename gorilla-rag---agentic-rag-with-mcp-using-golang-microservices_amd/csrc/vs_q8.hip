@@ -151,15 +151,11 @@ __device__ __forceinline__ void spec_decide(const float* __restrict__ ratio, Q8S
                                             bool force) {
   bool go = ratio_set(*ratio);
   if (go && !force) {
-    // a pending cool-down: count one batch off it (never below 0, whatever
-    // other contexts do meanwhile) and take the sample path
-    uint32_t c = __hip_atomic_load(&sk->cool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (c != 0u) {
-      const uint32_t o = atomicCAS(&sk->cool, c, c - 1u);
-      if (o == c) break;
-      c = o;
-    }
-    go = c == 0u;
+    // (the host reads the same verdict from its advice words and normally
+    // enqueues no try at all while loose)
+    go = __hip_atomic_load(&sk->loose, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    // every kQ8SpecProbe-th try runs the sample path, which re-judges `loose`
+    if (go) go = (atomicAdd(&sk->since, 1u) + 1u) % kQ8SpecProbe != 0u;
   }
   gate[kGateVerdict] = go ? 0u : 1u;
   gate[kGateGo] = go ? 1u : 0u;
@@ -268,20 +264,23 @@ __global__ __launch_bounds__(kMfmaQueries) void q8_verify_record_kernel(
     const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint32_t dim,
     const float* __restrict__ bound, const float* __restrict__ q8par,
     const float* __restrict__ glob, uint32_t check, uint32_t* __restrict__ gate,
-    Q8SpecK* __restrict__ sk, Q8SpecStat* __restrict__ stat, const uint32_t* __restrict__ run_if) {
+    Q8SpecK* __restrict__ sk, Q8SpecStat* __restrict__ stat, uint32_t* advice,
+    const uint32_t* __restrict__ run_if) {
   if (run_if && *run_if == 0u) return;
   __shared__ float rq[kMfmaQueries];
   __shared__ float pick;
   const uint32_t q = threadIdx.x;
   bool ok = true;
   float r = INFINITY;  // this query's ratio; +inf: none (no k-th, s <= 0, zero query)
+  float qn = 0.f, b = -INFINITY;
   if (q < nq) {
     const uint64_t key = keys[(size_t)q * k + k - 1];
     const float s = key ? vs::key_score(key) : -INFINITY;
     const float sig = q8par[4 * (size_t)q + 3];
-    ok = !check || (key != 0 && s >= bound[q] - sig * glob[2]);
+    b = bound[q];
+    ok = !check || (key != 0 && s >= b - sig * glob[2]);
     // |q| from sigma = (4 dim + 64) 2^-24 |q| (1 + 2^-20) (vs_bound_dev.h q8_sigma)
-    const float qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
+    qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
     if (key != 0 && s > 0.f && qn > 0.f) r = s / qn;
   }
   rq[q] = r;
@@ -299,19 +298,32 @@ __global__ __launch_bounds__(kMfmaQueries) void q8_verify_record_kernel(
     if (rank == m - 1) pick = r;
   }
   __syncthreads();
+  const float R = 0.97f * pick;  // the ratio this batch teaches (+inf: none)
+  // (sample path) queries whose sample bound the speculative bound R |q|
+  // would fall under: each would admit more rows than its sample pass does
+  const int nloose = __syncthreads_count(!check && r < INFINITY && R * qn < b);
   if (q != 0) return;
   if (check) {
     if (nbad) {
       gate[kGateVerdict] = 1u;
       atomicAdd(&stat->fails, 1ull);
-      const uint32_t b = sk->backoff;
-      sk->cool = b;
-      sk->backoff = b ? (2 * b < kQ8SpecMaxBackoff ? 2 * b : kQ8SpecMaxBackoff) : 1u;
+      // the cool-down: the host runs the next `bo` batches of this k on the
+      // sample path alone, counting them off its advice word
+      const uint32_t bo = sk->backoff;
+      sk->backoff = bo ? (2 * bo < kQ8SpecMaxBackoff ? 2 * bo : kQ8SpecMaxBackoff) : 1u;
+      if (advice && bo)
+        __hip_atomic_store(advice + kQ8SpecK, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;  // the sample path's record replaces the ratio
     }
     sk->backoff = 0u;
   }
-  if (pick < INFINITY) sk->ratio = 0.97f * pick;
+  if (pick < INFINITY) sk->ratio = R;
+  if (!check) {
+    const uint32_t loose = pick < INFINITY && 4 * nloose > nvalid ? 1u : 0u;
+    sk->loose = loose;
+    sk->since = 0u;
+    if (advice) __hip_atomic_store(advice, loose, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Workgroups [0, nq_bound): the sample bound of query blockIdx.x; the rest:
@@ -384,11 +396,11 @@ hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, c
 hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k, uint32_t dim,
                                    const float* bound, const float* q8par, const float* glob,
                                    bool check, uint32_t* gate, Q8SpecK* spec_k, Q8SpecStat* stat,
-                                   hipStream_t st, const uint32_t* run_if) {
+                                   uint32_t* advice, hipStream_t st, const uint32_t* run_if) {
   if (nq == 0 || nq > kMfmaQueries || k == 0 || !spec_k || !stat || (check && !gate))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(q8_verify_record_kernel, dim3(1), dim3(kMfmaQueries), 0, st, keys, nq, k, dim,
-                     bound, q8par, glob, check ? 1u : 0u, gate, spec_k, stat, run_if);
+                     bound, q8par, glob, check ? 1u : 0u, gate, spec_k, stat, advice, run_if);
   return hipGetLastError();
 }
 

@@ -9,9 +9,12 @@ then admitted whole clusters. Now a batch REPLACES the ratio with a low
 quantile of its own queries' ratios (csrc/vs_q8.hip q8_verify_record_kernel)
 and a failed check backs off to the sample path.
 
-A clustered corpus (64 Gaussian clusters, unit rows, bf16, inner product) is
-searched in one process by two engines over the same rows: speculation on
-(the default) and off (VS_FLAG_NO_SPECULATIVE, the sample path every batch).
+Two corpora (4M unit rows, bf16, inner product): 64 Gaussian clusters, where
+one ratio cannot follow the queries' own k-th scores and speculation must
+switch itself off (Q8SpecK.loose), and isotropic rows with planted topics of
+near-duplicates, where it pays and must keep paying. Each is searched in one
+process by two engines over the same rows: speculation on (the default) and
+off (VS_FLAG_NO_SPECULATIVE, the sample path every batch).
 The sequence: on-topic batches (the ratio is learned), ONE batch mixing
 on-topic queries with a few near-orthogonal ones, then more fresh on-topic
 batches, then a run of batches that all carry outliers. Checked: keys
@@ -38,21 +41,46 @@ import torch
 import __graft_entry__ as ge
 from oracle import oracle as orc
 pkg = ge.load_package()
-n, dim, C, B, k = int(os.environ.get("T_ROWS", "2000000")), 768, 64, 256, 10
+n, dim, C, B, k = int(os.environ.get("T_ROWS", "4000000")), 768, 64, 256, 10
 g = torch.Generator(device="cuda").manual_seed(2026)
 cent = torch.randn((C, dim), device="cuda", generator=g)
 cent /= cent.norm(dim=1, keepdim=True)
-def clustered(m, noise=1.0):
-    lab = torch.randint(0, C, (m,), device="cuda", generator=g)
-    v = cent[lab] + noise * torch.randn((m, dim), device="cuda", generator=g) / dim ** 0.5
+KIND = os.environ.get("T_KIND", "clusters")
+def unit(v):
     return v / v.norm(dim=1, keepdim=True)
-X = torch.cat([clustered(200_000) for _ in range(n // 200_000)]).cpu().numpy()
-# near-orthogonal to every cluster centre: the centres' span projected out
-Qc, _ = torch.linalg.qr(cent.T)
-def outliers(m):
-    v = torch.randn((m, dim), device="cuda", generator=g)
-    v = v - (v @ Qc) @ Qc.T
-    return v / v.norm(dim=1, keepdim=True)
+if KIND == "clusters":
+    # 64 Gaussian clusters: every row and on-topic query is a centre plus noise
+    # of the same norm, so a query's own cluster crowds the scores just under
+    # its k-th, and that k-th moves with the query (its noise along the centre)
+    def clustered(m, noise=1.0):
+        lab = torch.randint(0, C, (m,), device="cuda", generator=g)
+        return unit(cent[lab] + noise * torch.randn((m, dim), device="cuda", generator=g) / dim ** 0.5)
+    X = torch.cat([clustered(200_000) for _ in range(n // 200_000)]).cpu().numpy()
+    # near-orthogonal to every cluster centre: the centres' span projected out
+    Qc, _ = torch.linalg.qr(cent.T)
+    def outliers(m):
+        v = torch.randn((m, dim), device="cuda", generator=g)
+        return unit(v - (v @ Qc) @ Qc.T)
+else:
+    # "planted": isotropic random rows plus 4096 topics of 32 near-duplicate
+    # rows each (RAG chunks close to a question); an on-topic query sits on a
+    # topic (k-th score ~0.9), an outlier is a random direction (~0.16)
+    T, per = 4096, 32
+    top = unit(torch.randn((T, dim), device="cuda", generator=g))
+    def near(t, m):
+        return unit(top[t] + 0.35 * torch.randn((m, dim), device="cuda", generator=g) / dim ** 0.5)
+    Xt = torch.empty((n, dim), device="cuda")
+    for r0 in range(0, n, 200_000):
+        r1 = min(n, r0 + 200_000)
+        Xt[r0:r1] = unit(torch.randn((r1 - r0, dim), device="cuda", generator=g))
+    slots = torch.randperm(n, device="cuda", generator=g)[:T * per]
+    Xt[slots] = near(torch.arange(T, device="cuda").repeat_interleave(per), T * per)
+    X = Xt.cpu().numpy()
+    del Xt
+    def clustered(m):
+        return near(torch.randint(0, T, (m,), device="cuda", generator=g), m)
+    def outliers(m):
+        return unit(torch.randn((m, dim), device="cuda", generator=g))
 on = pkg.VectorEngine(device=0)
 off = pkg.VectorEngine(device=0, speculative=False)
 for e in (on, off):
@@ -125,25 +153,33 @@ def _run(env):
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-def test_outlier_queries_do_not_poison_later_batches():
-    r = _run({})
+@pytest.mark.parametrize("kind", ["clusters", "planted"])
+def test_outlier_queries_do_not_poison_later_batches(kind):
+    r = _run({"T_KIND": kind})
     rec = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
     if os.path.isdir(rec):
-        with open(os.path.join(rec, "spec_cliff.json"), "w") as f:
+        with open(os.path.join(rec, f"spec_cliff_{kind}.json"), "w") as f:
             json.dump(r, f)
     assert r["mismatch"] == [], r["mismatch"]
     assert r["parity"] == [], r["parity"]
     b = r["batches"]
     after = [x for x in b if x["phase"] == "after"]
-    ratios = [x["on_ms"] / x["off_ms"] for x in after]
+    # the engines alternate which runs a batch first, and the second run of a
+    # batch is ~2% slower on the same work (clock), so times are compared
+    # over consecutive pairs of batches (one of each order)
+    ratios = [(after[i]["on_ms"] + after[i + 1]["on_ms"]) /
+              (after[i]["off_ms"] + after[i + 1]["off_ms"]) for i in range(len(after) - 1)]
     # no on-topic batch after the outlier pays for it (r05's running minimum
     # made every one of them several times slower)
     assert max(ratios) <= 1.02, ratios
     st = r["stats"]["on"]
-    # the outlier batch (and the first mixed ones) failed their check; the
-    # back-off then sent most mixed batches to the sample path
-    assert st["fallbacks"] >= 1 and st["skipped"] >= 1, st
     assert r["stats"]["off"]["tries"] == 0, r["stats"]
     mixed = [x for x in b if x["phase"] == "mixed"]
     tail = mixed[len(mixed) // 2:]
     assert sum(x["on_ms"] for x in tail) <= 1.25 * sum(x["off_ms"] for x in tail), tail
+    if kind == "planted":
+        # a corpus where speculating pays: it kept paying after the outlier
+        # (the outlier failed its batch's check; the ratio it would have
+        # dragged down was never learned), and every-batch outliers backed off
+        assert sorted(ratios)[len(ratios) // 2] <= 0.95, ratios
+        assert st["fallbacks"] >= 1 and st["skipped"] >= 1, st
