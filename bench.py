@@ -495,6 +495,7 @@ def main():
                 # RCCL and merge workgroups hold CUs the next sample pass needs
                 if os.environ.get("VS_EXCHANGE_OVERLAP", "0") == "1":
                     sharded.exchange_stream = torch.cuda.Stream()
+                    sharded.exchange_ring = ring
             else:
                 log("[bench] torch.distributed exchange instead of the engine communicator")
                 collective = "torch"

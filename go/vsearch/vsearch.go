@@ -39,6 +39,9 @@ static int vsg_collection_placement(vs_engine* h, const char* n, int32_t* d, vsg
 static int vsg_collection_prefilter_bytes(vs_engine* h, const char* n, uint64_t* b, vsg_err* e) {
 	return vsg_fin(vs_collection_prefilter_bytes(h, n, b), e);
 }
+static int vsg_collection_spec_stats(vs_engine* h, const char* n, uint64_t* o, vsg_err* e) {
+	return vsg_fin(vs_collection_spec_stats(h, n, o), e);
+}
 static int vsg_collection_info(vs_engine* h, const char* n, uint32_t* d, uint64_t* r, vsg_err* e) {
 	return vsg_fin(vs_collection_info(h, n, d, r, NULL, NULL), e);
 }
@@ -209,6 +212,19 @@ func (e *Engine) PrefilterBytes(name string) (uint64, error) {
 	var ce C.vsg_err
 	err := check(C.vsg_collection_prefilter_bytes(e.h, cs, &b, &ce), &ce)
 	return uint64(b), err
+}
+
+// SpecStats reports the collection's speculative-bound counters
+// (vs_collection_spec_stats): batches tried, of those re-answered on the
+// sample path after a failed check (fallbacks), and batches kept on the
+// sample path (skipped). Diagnostics; the reference has no counterpart.
+func (e *Engine) SpecStats(name string) (tries, fallbacks, skipped uint64, err error) {
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	var o [4]C.uint64_t
+	var ce C.vsg_err
+	err = check(C.vsg_collection_spec_stats(e.h, cs, &o[0], &ce), &ce)
+	return uint64(o[0]), uint64(o[1]), uint64(o[2]), err
 }
 
 // OpenShards opens one engine over row shards: shard s on HIP device

@@ -172,7 +172,8 @@ hipError_t launch_gemv_q8(int part, const void* X, bool bf16, const int8_t* X8, 
                           const float* q_raw, bool cosine, const uint64_t* allow, uint32_t k,
                           void* scratch, size_t scratch_bytes, uint32_t* ctr, uint64_t* dst,
                           hipStream_t st, uint64_t* flag = nullptr, uint64_t seq = 0,
-                          uint32_t* stats = nullptr);
+                          uint32_t* stats = nullptr,
+                          uint64_t* clk = nullptr);  // (tools) [finish wg][8] stage clocks
 
 // Batched scan on MFMA with fused top-k: bf16 rows on
 // v_mfma_f32_16x16x32_bf16, or fp32 rows (f32) on v_mfma_f32_16x16x4_f32.

@@ -1654,13 +1654,15 @@ struct MfArgs {
   const uint32_t* wg_tile;  // nullable: workgroup b scans tiles [wg_tile[b], wg_tile[b+1])
   // int8 prefilter pass (I8, r04; DESIGN.md §5 "int8 prefilter"): per query
   // {sqS, a, c, sigma} (q8par, float4) and the collection's {-, dmax, nmax, S}
-  // (q8glob) turn the sample bound into an integer dot threshold; a full
-  // quarter raises *gate (the batch is then answered by the bf16 pass).
+  // (q8glob) turn the sample bound into an integer dot threshold. A full
+  // quarter keeps counting past its capacity (lossy: the select recomputes
+  // it, r05); the pass raises no word of its own.
   const float* q8par;
   const float* q8glob;
-  uint32_t* gate;
-  // nullable: the launch does nothing unless *run_if != 0 (the bf16 pass and
-  // select that stand behind the int8 pass, enqueued every batch)
+  uint32_t* gate;  // (unused since r05; the batch's control words, vs_kernels.h kGate*)
+  // nullable: the launch does nothing unless *run_if != 0 (the passes of a
+  // speculative try, gated on its go word, and the sample path behind it,
+  // gated on its verdict: vs_engine.cpp search_mfma)
   const uint32_t* run_if;
 };
 
@@ -3372,8 +3374,9 @@ hipError_t launch_select_slabs(const float* slabs, const uint32_t* slab_tile,
 // two (read from the quarters whose largest U does) are the only ones that
 // can be in the top k; they are rescored from the bf16 rows on the bf16
 // pass's own MFMA chain -- the same score bits -- and the top k of those keys
-// is the bf16 pass's answer. More survivors than the LDS buffer holds raise
-// *gate: the bf16 pass and select then answer the batch.
+// is the bf16 pass's answer. A lossy quarter that can reach the cutoff is
+// recomputed from the int8 copy, and more survivors than the LDS buffer holds
+// stream through a running top k (r05); nothing is handed to another pass.
 
 // SV (timing ablation, VS_Q8_SEL_SV): return after stage SV. F32: fp32 rows
 // and queries, survivors rescored on the f32 pass's v_mfma_f32_16x16x4_f32
@@ -4455,20 +4458,30 @@ hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
 //  1. gemv_q8_scan_kernel: every row's dot on v_dot4_i32_i8 (16 B of a row
 //     per lane, 4 rows per wave step, waves interleaved over the rows as the
 //     GEMV's), its U and L; per wave the KP = 64 KPL largest U keys (a
-//     register list, merged per workgroup by rank: gemv_emit) and the largest
-//     L key's score image.
+//     register list, merged per workgroup by rank: gemv_emit) and, per
+//     workgroup (r06; per wave before), the largest L key's score image.
 //  2. gemv_q8_finish_kernel: P = the floor of the 24-bit bucket holding the
-//     k-th largest of the waves' L images (k distinct rows reach it, so it is
-//     at most the k-th GEMV score); each workgroup list's entries whose U
-//     reaches P are rescored on the GEMV's own per-row arithmetic
+//     k-th largest of the workgroups' L images (k distinct rows reach it, so
+//     it is at most the k-th GEMV score); each workgroup list's entries whose
+//     U reaches P are rescored on the GEMV's own per-row arithmetic
 //     (gemv_row_score: the same loads, chunk_dot, order and wave_sum, hence
 //     the same bits); a list that dropped a key whose U reaches P is replaced
-//     by every row of its scan workgroup. Each finishing workgroup appends its
-//     waves' top k, and the last one (agent-scope hand-off, as
-//     gemv_one_finish) merges them.
+//     by every row of its scan workgroup. Each finishing workgroup writes its
+//     sorted top k (gemv_emit), and the last one (agent-scope hand-off, as
+//     gemv_one_finish) merges those lists (merge_query).
 // Every row of the GEMV's top k has U >= s >= k-th score >= P, so it is
 // rescored and its key is the GEMV's: the answer equals the GEMV's bit for bit.
-constexpr int kQ8gLists = 4;  // scan-workgroup lists per finishing workgroup
+#ifndef VS_Q8G_LISTS
+#define VS_Q8G_LISTS 8
+#endif
+#ifndef VS_Q8G_PASSES
+#define VS_Q8G_PASSES 2
+#endif
+constexpr int kQ8gLists = VS_Q8G_LISTS;  // scan-workgroup lists per finishing workgroup
+// the finish's P: 8-bit radix passes over the top 8 x kQ8gPasses bits of the
+// workgroup L images (the floor of that bucket), from registers
+constexpr int kQ8gPasses = VS_Q8G_PASSES;
+constexpr int kQ8gHeld = 2;  // values per thread: up to 1024 scan workgroups
 
 template <int D>
 struct Q8GemvShape {
@@ -4620,7 +4633,16 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
     for (int j = 0; j < S::J; ++j) buf[0][j] = buf[1][j];
   }
   gemv_emit<KPL>(Lst, theta, KP, lane, w, ulist);
-  if (lane == 0) lbest[gw] = (uint32_t)(lmax >> 32);
+  // (r06) the workgroup's largest L image: the finish takes the k-th largest
+  // over workgroups (each reached by a distinct row), 8x fewer values than
+  // one per wave, and as tight whenever the top k rows sit in distinct
+  // workgroups (k <= 128 of ~768)
+  __shared__ uint32_t lb;
+  if (threadIdx.x == 0) lb = 0;
+  __syncthreads();
+  if (lane == 0) atomicMax(&lb, (uint32_t)(lmax >> 32));
+  __syncthreads();
+  if (threadIdx.x == 0) lbest[blockIdx.x] = lb;
 }
 
 // The score of local row `row` exactly as the GEMV scan computes it (its
@@ -4664,7 +4686,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     const float* __restrict__ q_raw, int prep, const uint64_t* __restrict__ allow, uint32_t k,
     const uint64_t* __restrict__ ulist, const uint32_t* __restrict__ lbest, uint32_t nscan,
     uint64_t* __restrict__ cand, uint32_t* __restrict__ ctr, uint64_t* __restrict__ dst,
-    uint64_t* flag, uint64_t seq, uint32_t* __restrict__ stats) {
+    uint64_t* flag, uint64_t seq, uint32_t* __restrict__ stats, uint64_t* __restrict__ clk) {
   using SQ = Q8GemvShape<D>;
   constexpr int KP = 64 * KPL;
   __shared__ float qs[D];
@@ -4674,51 +4696,73 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
   const int lane = threadIdx.x & 63;
   const uint32_t tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  // (tools) stage wall clocks of this workgroup: clk[block][0..7]
+  auto stamp = [&](int s) {
+    if (clk && tid == 0) clk[(size_t)blockIdx.x * 8 + s] = wall_clock64();
+  };
+  stamp(0);
   if (w == 0) prep_query_wave<D>(q_raw, prep, qs, lane);
   if (tid == 0) ns_sh = 0, fb_sh = 0, nz_sh = 0;
   __syncthreads();
-  // 1. P: radix floor of the k-th largest wave L image (0 = a wave without rows)
-  const uint32_t m = nscan * kGemvWaves;
-  uint32_t prefix = 0, kk = k;
+  stamp(1);
+  // 1. P: the radix floor of the k-th largest workgroup L image (0 = a
+  // workgroup without rows; one per scan workgroup since r06), 0 when fewer
+  // than k are nonzero. (A per-wave bit-by-bit select over the 768 values,
+  // no barriers, measured slower: tools/c2_finish, profiles/r06_c2_finish_*.)
+  // The values are read from global memory once, into registers (up to
+  // kQ8gHeld per thread: every grid of gfx950's 256 CUs), not once a pass.
+  const uint32_t m = nscan;
+  uint32_t P = 0;
   {
-    uint32_t nz = 0;
-    for (uint32_t i = tid; i < m; i += kGemvThreads) nz += lbest[i] != 0u;
-    if (nz) atomicAdd(&nz_sh, nz);  // complete at the first pass's barrier
-  }
-#pragma unroll 1
-  for (int pass = 0; pass < 3; ++pass) {
-    const int shift = 24 - 8 * pass;
-    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-    if (tid < 256) hist[tid] = 0;
-    __syncthreads();
-    if (nz_sh < k) break;  // uniform: fewer than k rows scanned -> P = 0
-    for (uint32_t i = tid; i < m; i += kGemvThreads) {
-      const uint32_t u = lbest[i];
-      if (u && (u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    uint32_t c = 0, x = 0;
-    if (tid < 256) {
-      c = hist[255 - tid];  // thread t: digit 255 - t (descending)
-      x = c;
+    uint32_t lv[kQ8gHeld];
+    uint32_t prefix = 0, kk = k;
+    {
+      uint32_t nz = 0;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+      for (int j = 0; j < kQ8gHeld; ++j) {
+        const uint32_t i = tid + (uint32_t)j * kGemvThreads;
+        lv[j] = i < m ? lbest[i] : 0u;
+        nz += lv[j] != 0u;
       }
-      if (lane == 63) hws[w] = x;
+      if (nz) atomicAdd(&nz_sh, nz);  // complete at the first pass's barrier
     }
-    __syncthreads();
-    if (tid < 256) {
-      for (int j = 0; j < w; ++j) x += hws[j];
-      if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
+#pragma unroll 1
+    for (int pass = 0; pass < kQ8gPasses; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      if (nz_sh < k) break;  // uniform: fewer than k rows scanned -> P = 0
+#pragma unroll
+      for (int j = 0; j < kQ8gHeld; ++j) {
+        const uint32_t u = lv[j];
+        if (u && (u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      uint32_t c = 0, x = 0;
+      if (tid < 256) {
+        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
+        x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (lane == 63) hws[w] = x;
+      }
+      __syncthreads();
+      if (tid < 256) {
+        for (int j = 0; j < w; ++j) x += hws[j];
+        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
+      }
+      __syncthreads();
+      prefix |= (255u - hpick) << shift;
+      kk -= habove;
+      __syncthreads();
     }
-    __syncthreads();
-    prefix |= (255u - hpick) << shift;
-    kk -= habove;
-    __syncthreads();
+    P = nz_sh < k ? 0u : prefix;
   }
-  const uint32_t P = nz_sh < k ? 0u : prefix;
+  stamp(2);
   // 2. the lists' entries whose U reaches P; a list whose dropped keys may
   // reach P (its last entry does) is replaced by all of its workgroup's rows
   const uint32_t l0 = blockIdx.x * kQ8gLists;
@@ -4730,6 +4774,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     if (e != 0 && (uint32_t)(e >> 32) >= P) surv[atomicAdd(&ns_sh, 1u)] = e;
   }
   __syncthreads();
+  stamp(3);
   // 3. rescore: wave w takes survivors w, w + 8, ... (those of fallback lists
   // are rescored below with every row of their workgroup)
   const uint32_t fb = fb_sh, ns = ns_sh;
@@ -4774,29 +4819,19 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     atomicAdd(&stats[0], rescored);
     if (w == 0) atomicAdd(&stats[1], (uint32_t)__popc(fb));
   }
-  // 4. this wave's top k -> the candidate array
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int i = 0; i < KPL; ++i) cnt += (uint32_t)__popcll(__ballot(R.e[i] != 0));
-  cnt = cnt < k ? cnt : k;
-  if (cnt) {
-    uint32_t base = 0;
-    if (lane == 0) base = __hip_atomic_fetch_add(&ctr[1], cnt, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    base = (uint32_t)__shfl((int)base, 0, 64);
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const uint32_t idx = (uint32_t)(i * 64 + lane);
-      if (idx < cnt) cand[base + idx] = R.e[i];
-    }
-  }
-  // 5. hand-off: the last workgroup merges every appended key
+  // 4. the workgroup's top k -> its sorted list cand[block][k] (r06: by rank,
+  // gemv_emit, as the scan's lists; r05 appended every wave's keys through one
+  // agent-scope counter, and the last workgroup sorted the pile)
+  gemv_emit<KPL>(R, theta, k, lane, w, cand);
+  // 5. hand-off: the last workgroup merges the sorted lists (merge_query's
+  // list walk, as the GEMV's own merge)
   __shared__ uint64_t mbuf[kMergeCap];
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t mcnt;
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  stamp(4);
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -4806,22 +4841,16 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      mcnt = __hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
+  stamp(5);
   if (!last) return;
-  const uint32_t N = mcnt;
-  __syncthreads();
-  if (N == 0) {
-    for (uint32_t j = tid; j < k; j += kGemvThreads) dst[j] = 0;
-  } else {
-    merge_query(cand, N, 1, 0, 1, k, 0, dst, mbuf, red, mcnt, false);
-  }
-  if (tid == 0) {
-    __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // (merge_query's tournament instead of the list walk: 36.7 against 20.2 us
+  // for the whole finish at C2, profiles/r06_c2ab_*)
+  merge_query(cand, gridDim.x, k, 0, k, k, 0, dst, mbuf, red, mcnt, false);
+  if (tid == 0) __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(6);
   if (flag) publish_host(flag, seq);
 }
 
@@ -4842,7 +4871,7 @@ static void gemv_q8_launch(int part, const void* X, const int8_t* X8, const floa
                            const float* q_raw, int prep, const uint64_t* allow, uint32_t k,
                            uint32_t nscan, uint64_t* ulist, uint32_t* lbest, uint64_t* cand,
                            uint32_t* ctr, uint64_t* dst, uint64_t* flag, uint64_t seq,
-                           uint32_t* stats, hipStream_t st) {
+                           uint32_t* stats, uint64_t* clk, hipStream_t st) {
   if (part & 1)
     hipLaunchKernelGGL((gemv_q8_scan_kernel<D, KPL>), dim3(nscan), dim3(kGemvThreads), 0, st, X8,
                        n_rows, row_base, q_raw, prep, meta, glob, allow, ulist, lbest);
@@ -4850,18 +4879,20 @@ static void gemv_q8_launch(int part, const void* X, const int8_t* X8, const floa
     hipLaunchKernelGGL((gemv_q8_finish_kernel<D, BF16, KPL>),
                      dim3((nscan + kQ8gLists - 1) / kQ8gLists), dim3(kGemvThreads), 0, st, X,
                      n_rows, row_base, q_raw, prep, allow, k, ulist, lbest, nscan, cand, ctr, dst,
-                     flag, seq, stats);
+                     flag, seq, stats, clk);
 }
 
 hipError_t launch_gemv_q8(int part, const void* X, bool bf16, const int8_t* X8, const float* meta,
                           const float* glob, uint32_t dim, uint32_t n_rows, uint32_t row_base,
                           const float* q_raw, bool cosine, const uint64_t* allow, uint32_t k,
                           void* scratch, size_t scratch_bytes, uint32_t* ctr, uint64_t* dst,
-                          hipStream_t st, uint64_t* flag, uint64_t seq, uint32_t* stats) {
+                          hipStream_t st, uint64_t* flag, uint64_t seq, uint32_t* stats,
+                          uint64_t* clk) {
   if (!gemv_q8_ok(dim, k) || n_rows == 0 || !X || !X8 || !meta || !glob || !q_raw || !ctr ||
       !dst || scratch_bytes < gemv_q8_scratch_bytes(n_rows, k))
     return hipErrorInvalidValue;
   const uint32_t nscan = gemv_q8_lists(n_rows);
+  if (nscan > (uint32_t)(kQ8gHeld * kGemvThreads)) return hipErrorInvalidValue;  // > 341 CUs
   const uint32_t kp = k <= 64 ? 64 : 128;
   uint64_t* ulist = (uint64_t*)scratch;
   uint32_t* lbest = (uint32_t*)(ulist + (size_t)nscan * kp);
@@ -4870,7 +4901,7 @@ hipError_t launch_gemv_q8(int part, const void* X, bool bf16, const int8_t* X8, 
   const int prep = (cosine ? 1 : 0) | (bf16 ? 2 : 0);
 #define VS_Q8G(DD, BB, KK)                                                                    \
   gemv_q8_launch<DD, BB, KK>(part, X, X8, meta, glob, n_rows, row_base, q_raw, prep, allow, k,  \
-                             nscan, ulist, lbest, cand, ctr, dst, flag, seq, stats, st)
+                             nscan, ulist, lbest, cand, ctr, dst, flag, seq, stats, clk, st)
   if (dim == 768) {
     if (bf16) { if (kp == 64) VS_Q8G(768, true, 1); else VS_Q8G(768, true, 2); }
     else { if (kp == 64) VS_Q8G(768, false, 1); else VS_Q8G(768, false, 2); }

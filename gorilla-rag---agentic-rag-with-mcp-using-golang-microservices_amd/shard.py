@@ -57,13 +57,31 @@ class ShardedSearch:
     # among themselves only: vs_gather_merge_keys). The returned keys are
     # ready once that stream is (a device synchronize covers both).
     exchange_stream: Optional[object] = None
+    # (r06) with exchange_stream: the result ring R (>= 2) of the
+    # callables. Batch i's local keys sit in a pooled buffer the search stream
+    # writes again at batch i + R, while batch i's exchange may still read it
+    # on the other stream: the search stream waits on that exchange first.
+    exchange_ring: int = 0
     _gather_bufs: Optional[dict] = None  # all-gather outputs, reused per shape
     _ev: Optional[object] = None
+    _xdone: Optional[list] = None  # the last exchange_ring exchanges' done events
 
     def search(self, queries, k: int):
         import torch
         import torch.distributed as dist
 
+        overlap = (self.gather_merge is not None and self.exchange_stream is not None and
+                   (self.world_size > 1 or self.always_gather))
+        if overlap:
+            if self.exchange_ring < 2:
+                raise ValueError("exchange_stream needs exchange_ring >= 2 (the callables' result "
+                                 "ring): a reused local buffer would be overwritten while its "
+                                 "exchange still reads it")
+            if self._xdone is None:
+                self._xdone = []
+            if len(self._xdone) >= self.exchange_ring:
+                # the exchange that read the buffer this search is about to reuse
+                torch.cuda.current_stream().wait_event(self._xdone.pop(0))
         local = self.local_search(queries, k)
         if self.gather_merge is not None:
             if self.world_size == 1 and not self.always_gather:
@@ -79,7 +97,13 @@ class ShardedSearch:
             # that read is done (a ring-less caller drops `local` right away)
             local.record_stream(self.exchange_stream)
             with torch.cuda.stream(self.exchange_stream):
-                return self.gather_merge(local, k)
+                out = self.gather_merge(local, k)
+                done = torch.cuda.Event()
+                done.record()
+            self._xdone.append(done)
+            # the keys are written on exchange_stream: wait on it (or on a
+            # device synchronize) before reading them
+            return out
         if not dist.is_available() or not dist.is_initialized():
             return local
         if dist.get_world_size(self.group) == 1 and not self.always_gather:

@@ -100,3 +100,22 @@ def test_two_rank_gloo_merge_equals_unsharded(orc, form):
     s32, s64, rows, cnt = orc.search(X, Q, k)
     ref = _keys(s32, rows)
     assert np.array_equal(got[0], ref) and np.array_equal(got[1], ref)
+
+
+def test_exchange_stream_needs_a_result_ring():
+    """with an exchange stream, batch i's pooled local keys would be
+    overwritten by batch i + 1's search while batch i's exchange still reads
+    them unless the results rotate over a ring (>= 2) the search stream waits
+    through; a ring-less configuration is refused before anything runs."""
+    import __graft_entry__ as ge
+    from importlib import import_module
+    pkg = ge.load_package()
+    shard = import_module(pkg.__name__ + ".shard")
+    calls = []
+    sh = shard.ShardedSearch(local_search=lambda q, k: calls.append("local"),
+                             merge=lambda g, k: None,
+                             gather_merge=lambda l, k: calls.append("gather"),
+                             world_size=2, exchange_stream=object(), exchange_ring=1)
+    with pytest.raises(ValueError, match="exchange_ring"):
+        sh.search(np.zeros((4, 8), np.float32), 3)
+    assert calls == []

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Kill-or-keep check for a block-scaled FP6 prefilter (r06).
+
+The int8 pass is MFMA-issue-bound at the sustained clock, so
+the lever asked for is fewer matrix cycles per row: an FP6 (e2m3, OCP MX:
+one E8M0 scale per 32 elements) copy of the rows on
+v_mfma_scale_f32_16x16x128_f8f6f4 (2x the int8 rate), the query in MX-FP8
+(e4m3; the f8f6f4 MFMA takes no int8 operand), under the same exact
+Cauchy-Schwarz bracket the int8 path uses:
+  q.x = q'.x' + q'.(x - x') + (q - q').x,  |.| <= |q'| dt + |q - q'| nt
+with dt = max |x - x'| and nt = max |x| over a 32-row tile. What the
+bracket costs is the rows it cannot rule out: every row whose upper bound
+reaches the k-th lower bound is rescored (550 per query at C3 on int8).
+
+This script measures, on the bench's own generator rows (CPU, numpy), per
+query: the bracket half-width m, and the rows whose score lies within 2m
+under the k-th score (the survivors a select would rescore), for the int8
+scheme the product uses and for MX-FP6 rows x MX-FP8 queries. One JSON line.
+
+    python tools/fp6_bracket.py [ROWS=1000000] [QUERIES=64] [K=10]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def mx_quant(x, mant_bits, emax, emin_sub):
+    """OCP MX block quantisation (32-element blocks, E8M0 power-of-two scale
+    chosen so the block's absmax lands in the format's top binade), RNE onto
+    a format with `mant_bits` mantissa bits, largest exponent `emax` and
+    smallest normal exponent `emin_sub` (subnormal step 2^(emin_sub -
+    mant_bits)); returns the dequantised values."""
+    n, d = x.shape
+    b = x.reshape(n, d // 32, 32)
+    amax = np.abs(b).max(axis=2, keepdims=True)
+    amax = np.where(amax > 0, amax, 1.0)
+    scale = np.exp2(np.floor(np.log2(amax)) - emax)
+    y = b / scale
+    e = np.floor(np.log2(np.maximum(np.abs(y), 2.0 ** emin_sub)))
+    e = np.clip(e, emin_sub, emax)
+    step = np.exp2(e - mant_bits)
+    q = np.round(y / step) * step
+    top = (2 - 2.0 ** -mant_bits) * 2.0 ** emax
+    q = np.clip(q, -top, top)
+    return (q * scale).reshape(n, d)
+
+
+def tile_bounds(X, Xq):
+    """Per 32-row tile: dt = max |x - x'|, nt = max |x| (the product's meta)."""
+    dt = np.linalg.norm(X - Xq, axis=1).reshape(-1, 32).max(axis=1)
+    nt = np.linalg.norm(X, axis=1).reshape(-1, 32).max(axis=1)
+    return np.repeat(dt, 32), np.repeat(nt, 32)
+
+
+def main():
+    from oracle import oracle
+
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    nq = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    n -= n % 32
+    X = oracle.generate(oracle.SEED_CORPUS, 0, n, 768, bf16=True).astype(np.float64)
+    Q = oracle.generate(oracle.SEED_QUERY, 0, nq, 768, bf16=True).astype(np.float64)
+    S = X @ Q.T  # exact enough: fp64
+    sk = -np.sort(-S, axis=0)[k - 1]
+    out = {"tool": "fp6_bracket", "rows": n, "queries": nq, "k": k,
+           "score_sd": float(S.std()), "kth_score_mean": float(sk.mean())}
+    # int8, the product's scheme: one scale per collection, one per query
+    Sx = np.abs(X).max() / 127
+    X8 = np.clip(np.rint(X / Sx), -127, 127) * Sx
+    sq = np.abs(Q).max(axis=1, keepdims=True) / 127
+    Q8 = np.clip(np.rint(Q / sq), -127, 127) * sq
+    # MX-FP6 e2m3 rows (emax 2, 3 mantissa bits, normals from 2^0), MX-FP8
+    # e4m3 queries (emax 8, 3 mantissa bits, normals from 2^-6)
+    X6 = mx_quant(X, 3, 2, 0)
+    Q6 = mx_quant(Q, 3, 8, -6)
+    for name, Xq, Qq in (("int8", X8, Q8), ("mxfp6_rows_mxfp8_query", X6, Q6)):
+        dt, nt = tile_bounds(X, Xq)
+        a = np.linalg.norm(Qq, axis=1)
+        c = np.linalg.norm(Q - Qq, axis=1)
+        m = np.outer(dt, a) + np.outer(nt, c)  # [rows, queries]
+        # rows a bracket cannot rule out: U = s + 2m at most reaches the k-th
+        # lower bound only if s >= sk - 2m (the select's T is at most sk)
+        surv = (S + 2 * m >= sk[None, :]).sum(axis=0)
+        out[name] = {"rel_row_error": float(np.median(np.linalg.norm(X - Xq, axis=1) /
+                                                      np.linalg.norm(X, axis=1))),
+                     "rel_query_error": float(np.median(c / np.linalg.norm(Q, axis=1))),
+                     "bracket_half_width_mean": float(m.mean()),
+                     "half_width_in_score_sd": float(m.mean() / S.std()),
+                     "survivors_per_query_median": float(np.median(surv)),
+                     "survivor_fraction": float(np.median(surv) / n)}
+    r = out["mxfp6_rows_mxfp8_query"]["survivors_per_query_median"] / max(
+        1.0, out["int8"]["survivors_per_query_median"])
+    out["fp6_over_int8_survivors"] = round(r, 1)
+    out["verdict"] = ("killed: the FP6/FP8 bracket admits %.0fx the int8 survivors; the "
+                      "select's rescore (random bf16 row reads) would dwarf the 2x MFMA rate" % r
+                      if r > 4 else "keep for a device prototype")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

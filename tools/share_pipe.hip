@@ -53,7 +53,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&X8, (size_t)(n + 32) * dim));
   CK(hipMemset(X8, 0, (size_t)(n + 32) * dim));
   CK(hipMalloc(&meta, (size_t)((n + 32) / 32 + 1) * 8));
-  CK(hipMalloc(&glob, 16));
+  CK(hipMalloc(&glob, vsk::kQ8GlobBytes));
+  CK(hipMemset(glob, 0, vsk::kQ8GlobBytes));
   CK(hipMalloc(&qf, (size_t)PS * dim * 4));
   CK(hipMalloc(&qp, (size_t)PS * dim * 4));
   CK(hipMalloc(&qb, (size_t)PS * dim * 2));
@@ -147,7 +148,61 @@ int main(int argc, char** argv) {
     CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim,
                              q8par, glob, meta, sbound, X8, q8q, nullptr, n, st, nullptr, nullptr));
   };
+  // (r06) the product's speculative sequence (vs_engine.cpp search_mfma),
+  // priced launch by launch: the collection's ratio for k set from the batch
+  // above (0.97 x its smallest k-th per |q|), then query prep + int8 queries
+  // with the bound and the go / verdict words, the pass and the select gated
+  // on go, the check, and behind it the five fallback launches that stand
+  // down when the batch verified
+  vsk::Q8SpecK* sk = vsk::q8_spec_k(glob);
+  vsk::Q8SpecStat* sstat = vsk::q8_spec_stat(glob);
+  {
+    std::vector<float> hq((size_t)nq * dim);
+    CK(hipMemcpy(hq.data(), qf, hq.size() * 4, hipMemcpyDeviceToHost));
+    double rmin = 1e30;
+    for (uint32_t q = 0; q < nq; ++q) {
+      double a2 = 0;
+      for (uint32_t d = 0; d < dim; ++d) a2 += (double)hq[(size_t)q * dim + d] * hq[(size_t)q * dim + d];
+      rmin = std::min(rmin, (double)vs::key_score(hk[(size_t)q * k + k - 1]) / std::sqrt(a2));
+    }
+    const float r = (float)(0.97 * rmin);
+    CK(hipMemcpy(&sk[k].ratio, &r, 4, hipMemcpyHostToDevice));
+  }
+  const uint32_t* go = gate + vsk::kGateGo;
+  auto q8q_spec = [&]() {
+    CK(vsk::launch_q8_query(qb, false, nq, dim, glob, q8q, q8par, gate, st, &sk[k].ratio, bound,
+                            &sk[k], sstat, true));
+  };
+  auto pass_g = [&]() {
+    CK(vsk::launch_mfma_cand_q8(X8, dim, n, 0, q8q, nq, k, bound, q8par, glob, slabs, slab_tile, cap8,
+                                cnt, qmax, maxl, &L, gate, st, nullptr, go));
+  };
+  auto select_g = [&]() {
+    CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim,
+                             q8par, glob, meta, bound, X8, q8q, nullptr, n, st, nullptr, nullptr, go));
+  };
+  auto verify = [&]() {
+    CK(vsk::launch_q8_verify_record(out, nq, k, dim, bound, q8par, glob, true, gate, &sk[k], sstat,
+                                    nullptr, st, go));
+  };
+  const uint32_t* fb = gate + vsk::kGateVerdict;
+  auto fallback = [&]() {
+    CK(vsk::launch_mfma_sample(X, false, dim, n, 0, qb, nq, k, stl, tmax, maxl, &L, st, nullptr, fb));
+    CK(vsk::launch_sample_bound_q8(tmax, L * stl, nq, k, bound, qb, false, nq, dim, glob, q8q, q8par,
+                                   nullptr, st, fb));
+    CK(vsk::launch_mfma_cand_q8(X8, dim, n, 0, q8q, nq, k, bound, q8par, glob, slabs, slab_tile, cap8,
+                                cnt, qmax, maxl, &L, gate, st, nullptr, fb));
+    CK(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nq, k, out, 0, X, qb, false, dim,
+                             q8par, glob, meta, bound, X8, q8q, nullptr, n, st, nullptr, nullptr, fb));
+    CK(vsk::launch_q8_verify_record(out, nq, k, dim, bound, q8par, glob, false, nullptr, &sk[k], sstat,
+                                    nullptr, st, fb));
+  };
   std::vector<Arm> arms = {
+      {"specseq_fb", [&] { prep(), q8q_spec(), pass_g(), select_g(), verify(), fallback(); }},
+      {"specseq", [&] { prep(), q8q_spec(), pass_g(), select_g(), verify(); }},
+      {"specseq_nover", [&] { prep(), q8q_spec(), pass_g(), select_g(); }},
+      {"specseq_noprep", [&] { q8q_spec(), pass_g(), select_g(), verify(); }},
+      {"specseq_pass", [&] { q8q_spec(), pass_g(); }},
       {"spec", [&] { pass_s(), select_s(); }},
       {"full", [&] { prep(), sample(), boundq8(), pass(), select(nullptr); }},
       {"r04gate", [&] { prep(), sample(), boundq8(), pass(), select(nullptr), gated(); }},
