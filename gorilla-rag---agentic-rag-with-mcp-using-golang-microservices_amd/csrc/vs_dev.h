@@ -19,6 +19,7 @@
 
 #include "../../include/vsearch.h"
 #include "vs_kernels.h"
+#include "vs_spec_host.h"
 
 namespace vsd {
 
@@ -289,16 +290,9 @@ struct DevEngine {
   // completion counter (zeroed at allocation; each launch leaves it zero)
   DevBuf small_part;
   DevBuf q8g;  // one query on the int8 copy: workgroup lists, wave bounds, candidates
-  // (r05) per collection (Collection::gen): the int8 copy generation and the
-  // k this context has answered a batch of on its stream (a later batch of
-  // this context may then try the speculative bound; whether it runs is
-  // decided on the device, r06). At most 256 entries (search_mfma).
-  struct SpecSeen {
-    uint64_t q8_gen = 0;
-    std::bitset<vsk::kQ8SpecK> k;
-    uint8_t loose_tick[vsk::kQ8SpecK] = {};  // batches while the advice said loose
-  };
-  std::unordered_map<uint64_t, SpecSeen> spec_seen;
+  // (r05) per collection (Collection::gen): what this context has answered
+  // on its stream, for the speculative bound (vs_spec_host.h spec_plan)
+  SpecSeenMap spec_seen;
   std::vector<uint64_t> h_keys;
   std::vector<std::unique_ptr<HostSlot>> host_slots;  // search_host staging, guarded by work_mu
   // timing

@@ -145,9 +145,7 @@ constexpr uint64_t kGatherDensityDen = 8;
 // Per-query launch overhead of a gathered scan (scan + merge launches,
 // ~10 us) in bytes of HBM streaming, for the batch decision in search_core.
 constexpr uint64_t kGatherCallBytes = 64ull << 20;
-// While a k's speculative bound is judged loose, one batch in kLooseRecord
-// records (and re-judges) it; the others run the sample path alone.
-constexpr uint8_t kLooseRecord = 8;
+static_assert(kSpecK == vsk::kQ8SpecK, "vs_spec_host.h sizes the host bookkeeping by k");
 // Collection bytes from which a batched host search is "heavy" (heavy_search).
 constexpr uint64_t kHeavyBytes = 256ull << 20;
 // Smallest batch of an fp32 collection that takes the MFMA pass.
@@ -256,7 +254,7 @@ int q8_after_write(DevEngine* eng, Collection& c, uint64_t r0, uint64_t r1,
 hipError_t q8_spec_reset(DevEngine* eng, Collection& c) {
   static std::atomic<uint64_t> next_gen{1};
   c.q8_gen = next_gen.fetch_add(1);
-  for (uint32_t k = 0; k < 2 * kQ8SpecK; ++k) __atomic_store_n(&c.q8_advice[k], 0u, __ATOMIC_RELAXED);
+  spec_advice_reset(c.q8_advice);
   return hipMemsetAsync(vsk::q8_spec_k(c.q8_glob), 0, (size_t)kQ8SpecK * sizeof(vsk::Q8SpecK),
                         eng->stream);
 }
@@ -732,37 +730,13 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     // speculative launches stand down and the sample path answers).
     const bool spec_rec =
         q8_spec_enabled() && !(eng->flags & VS_FLAG_NO_SPECULATIVE) && !allow && k < kQ8SpecK;
-    int spec_k = -1;
-    bool record = spec_rec;  // the sample path's answer teaches the ratio
-    DevEngine::SpecSeen* seen = nullptr;
-    if (spec_rec) {
-      // a hint only (the device state decides), so bounded: dropped
-      // collections' entries go with the rest when it grows past 256
-      if (eng->spec_seen.size() > 256 && !eng->spec_seen.count(c.gen)) eng->spec_seen.clear();
-      seen = &eng->spec_seen[c.gen];
-      if (seen->q8_gen != c.q8_gen) seen->q8_gen = c.q8_gen, seen->k.reset();
-      for (uint32_t kk = k; kk < kQ8SpecK && spec_k < 0; ++kk)
-        if (seen->k[kk]) spec_k = (int)kk;
-      // The device's advice (vs_kernels.h Q8SpecK). Loose: the last
-      // sample-path record found the bound loose for this k, so enqueue the
-      // sample path alone and its record only every kLooseRecord-th batch
-      // (which re-judges it). A cool-down after a failed check: the sample
-      // path and its record, one batch counted off.
-      if (spec_k >= 0 && !q8_spec_force_fail()) {
-        uint32_t* cool = &c.q8_advice[kQ8SpecK + k];
-        uint32_t n = __atomic_load_n(cool, __ATOMIC_RELAXED);
-        while (n && !__atomic_compare_exchange_n(cool, &n, n - 1, false, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED)) {
-        }
-        if (__atomic_load_n(&c.q8_advice[k], __ATOMIC_RELAXED) != 0u) {
-          spec_k = -1;
-          record = seen->loose_tick[k]++ % kLooseRecord == 0;
-        } else if (n) {
-          spec_k = -1;
-        }
-        if (spec_k < 0) c.spec_host_skips.fetch_add(1, std::memory_order_relaxed);
-      }
-    }
+    SpecPlan plan;  // spec_k -1: the sample path (vs_spec_host.h)
+    plan.record = spec_rec;
+    if (spec_rec)
+      plan = spec_plan(eng->spec_seen, c.gen, c.q8_gen, k, c.q8_advice, q8_spec_force_fail(),
+                       c.spec_host_skips);
+    const int spec_k = plan.spec_k;
+    const bool record = plan.record;
     vsk::Q8SpecK* sk = vsk::q8_spec_k(c.q8_glob);
     vsk::Q8SpecStat* sstat = vsk::q8_spec_stat(c.q8_glob);
     const uint32_t* verdict = gate + vsk::kGateVerdict;
@@ -842,7 +816,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                             run_if),
                "speculative bound record");
     }
-    if (spec_rec) seen->k[k] = true;
+    if (spec_rec) spec_seen_mark(plan, k);
     return VS_OK;
   }
   for (uint32_t p = 0; p < npass; ++p) {
