@@ -320,7 +320,7 @@ constexpr uint32_t kQ8SpecK = kMfmaMaxK + 1;
 constexpr size_t kQ8SpecStatOff = 16, kQ8SpecKOff = 48;
 constexpr size_t kQ8GlobBytes = kQ8SpecKOff + (size_t)kQ8SpecK * sizeof(Q8SpecK);
 constexpr uint32_t kQ8SpecMaxBackoff = 64;
-constexpr uint32_t kQ8SpecProbe = 16;
+constexpr uint32_t kQ8SpecProbe = 64;
 inline Q8SpecStat* q8_spec_stat(float* glob) {
   return (Q8SpecStat*)((char*)glob + kQ8SpecStatOff);
 }
