@@ -220,7 +220,8 @@ def scan_roofline(config, rows_local, dim, dtype, batch, k, scan_ms, int8, q8_b1
     return roof
 
 
-def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_fn, row0):
+def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_fn, row0,
+              spec_coll=None):
     """Times `steps` searches; returns (max elapsed s over ranks, scan/merge ms,
     every timed step's result tensor, the query rows of each timed step).
 
@@ -241,6 +242,9 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         sharded.search(q[i], k)
     torch.cuda.synchronize()
     eng.timing(reset=True)
+    # the speculative bound's counters over the timed steps only (read outside
+    # the timer: the call waits for the device)
+    spec0 = eng.spec_stats(spec_coll) if spec_coll else None
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -258,6 +262,9 @@ def run_phase(eng, sharded, coll, dim, batch, k, steps, warmup, dist_on, stream_
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     tm = eng.timing(reset=True)
+    if spec_coll:
+        s1 = eng.spec_stats(spec_coll)
+        tm["spec"] = {key: s1[key] - spec0[key] for key in s1}
     return el, tm, outs, (q, warmup)
 
 
@@ -501,15 +508,9 @@ def main():
                 collective = "torch"
 
     int8_pre = batch > 1 and eng.prefilter_bytes(coll) > 0
-    spec0 = eng.spec_stats(coll) if int8_pre else None
     el, tm, outs, qs = run_phase(eng, sharded, coll, dim, batch, k, args.steps, args.warmup,
-                                 dist_on, stream_fn, 0)
-    # the speculative bound's counters over the timed steps (read after the
-    # timer: the call waits for the device)
-    spec = None
-    if int8_pre:
-        s1 = eng.spec_stats(coll)
-        spec = {key: s1[key] - spec0[key] for key in s1}
+                                 dist_on, stream_fn, 0, coll if int8_pre else None)
+    spec = tm.get("spec")
     out = outs[-1]
     steps_verified = verify_steps(pkg, outs, k, n_full, sharded, qs)
     elem = 2 if dtype == "bf16" else 4
