@@ -15,7 +15,8 @@ reaches the k-th lower bound is rescored (550 per query at C3 on int8).
 This script measures, on the bench's own generator rows (CPU, numpy), per
 query: the bracket half-width m, and the rows whose score lies within 2m
 under the k-th score (the survivors a select would rescore), for the int8
-scheme the product uses and for MX-FP6 rows x MX-FP8 queries. One JSON line.
+scheme the product uses, for MX-FP6 rows x MX-FP8 queries, and for int8 with
+one scale per 32-row tile instead of per collection. One JSON line.
 
     python tools/fp6_bracket.py [ROWS=1000000] [QUERIES=64] [K=10]
 """
@@ -79,7 +80,12 @@ def main():
     # e4m3 queries (emax 8, 3 mantissa bits, normals from 2^-6)
     X6 = mx_quant(X, 3, 2, 0)
     Q6 = mx_quant(Q, 3, 8, -6)
-    for name, Xq, Qq in (("int8", X8, Q8), ("mxfp6_rows_mxfp8_query", X6, Q6)):
+    # (r06) int8 with one scale per 32-row tile instead of per collection
+    St = np.abs(X.reshape(-1, 32 * X.shape[1])).max(axis=1) / 127
+    St = np.repeat(St, 32)[:, None]
+    X8t = np.clip(np.rint(X / St), -127, 127) * St
+    for name, Xq, Qq in (("int8", X8, Q8), ("mxfp6_rows_mxfp8_query", X6, Q6),
+                         ("int8_tile_scale", X8t, Q8)):
         dt, nt = tile_bounds(X, Xq)
         a = np.linalg.norm(Qq, axis=1)
         c = np.linalg.norm(Q - Qq, axis=1)
