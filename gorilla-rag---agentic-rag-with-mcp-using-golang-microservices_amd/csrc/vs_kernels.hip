@@ -4574,19 +4574,33 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
     rowsel[j] = c / S::CPR;
     coff[j] = c % S::CPR;
   }
-  uint4 buf[2][S::J];
-  auto load = [&](uint4* dst, uint32_t r0) {
+#ifndef VS_Q8G_DEPTH
+#define VS_Q8G_DEPTH 2
+#endif
+  // Steps in flight: DEPTH - 1 ahead of the one being summed; each step's
+  // tile {dt, nt} is loaded with its rows (r06), not after its dots. (Two or
+  // three steps ahead measured slower at C2 -- 129.4 / 131.8 against 125.0 us
+  // per scan, the registers cost occupancy: profiles/r06_c2_scan_depth_*.)
+  constexpr int DEPTH = VS_Q8G_DEPTH;
+  uint4 buf[DEPTH][S::J];
+  float2 tmb[DEPTH];
+  auto load = [&](int slot, uint32_t r0) {
 #pragma unroll
     for (int j = 0; j < S::J; ++j) {
       uint32_t row = r0 + rowsel[j];
       row = row < n_rows ? row : n_rows - 1;
       const u32x4_t v = __builtin_nontemporal_load(
           (const u32x4_t*)(X8 + (size_t)row * D + (size_t)coff[j] * 16));
-      dst[j] = uint4{v[0], v[1], v[2], v[3]};
+      buf[slot][j] = uint4{v[0], v[1], v[2], v[3]};
     }
+    tmb[slot] = ((const float2*)meta)[r0 >> 5];  // the step's rows share one tile (r0 % 4 == 0)
   };
   const uint32_t lo = gw * S::RB;
-  if (lo < n_rows) load(buf[0], lo);  // the first rows' loads go out before the query is ready
+#pragma unroll
+  for (int d = 0; d < DEPTH - 1; ++d) {
+    const uint32_t r0 = lo + (uint32_t)d * stride;
+    if (r0 < n_rows) load(d, r0);
+  }
   if (w == 0) {
     prep_query_wave<D>(q_raw, prep, qs, lane);  // the GEMV's query, bit for bit
     q8_query_wave<D>(qs, q8s, par, glob[3], lane);
@@ -4600,8 +4614,8 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
   Lst.init();
   uint64_t theta = 0, lmax = 0;
   for (uint32_t r = lo; r < n_rows; r += stride) {
-    const uint32_t rn = r + stride;
-    load(buf[1], rn < n_rows ? rn : r);
+    const uint32_t rn = r + (uint32_t)(DEPTH - 1) * stride;
+    load(DEPTH - 1, rn < n_rows ? rn : r);
     int p[S::RB];
 #pragma unroll
     for (int b = 0; b < S::RB; ++b) p[b] = 0;
@@ -4611,8 +4625,8 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
 #pragma unroll
       for (int b = 0; b < S::RB; ++b) p[b] += rowsel[j] == b ? d : 0;
     }
-    // the step's rows share one tile (r % 4 == 0): its {dt, nt}
-    const float2 tm = ((const float2*)meta)[r >> 5];
+    // the step's tile {dt, nt}
+    const float2 tm = tmb[0];
     const float mt = pa * tm.x + pc * tm.y;
 #pragma unroll
     for (int b = 0; b < S::RB; ++b) {
@@ -4630,7 +4644,11 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_scan_kernel(
       }
     }
 #pragma unroll
-    for (int j = 0; j < S::J; ++j) buf[0][j] = buf[1][j];
+    for (int d = 0; d < DEPTH - 1; ++d) {
+#pragma unroll
+      for (int j = 0; j < S::J; ++j) buf[d][j] = buf[d + 1][j];
+      tmb[d] = tmb[d + 1];
+    }
   }
   gemv_emit<KPL>(Lst, theta, KP, lane, w, ulist);
   // (r06) the workgroup's largest L image: the finish takes the k-th largest

@@ -112,3 +112,56 @@ def test_speculative_bound_fp32(env):
     r = _run(dict(env, T_F32="1", T_KS="10,10,10,10,5,64,64,64"))
     assert r["mismatch"] == [], r["mismatch"]
     assert r["parity"] == [], r["parity"]
+
+
+_NEG = r"""
+import sys, json
+sys.path.insert(0, ROOT)
+import numpy as np
+import __graft_entry__ as ge
+pkg = ge.load_package()
+n, dim, nq, k = 200_000, 768, 256, 10
+rng = np.random.default_rng(5)
+u = rng.standard_normal(dim).astype(np.float32)
+u /= np.linalg.norm(u)
+# every row points away from u (inner products all about -1), the queries
+# along u: no batch has a k-th score > 0, so none records a ratio
+X = -u[None, :] + 0.05 * rng.standard_normal((n, dim)).astype(np.float32) / dim ** 0.5
+a = pkg.VectorEngine(device=0)
+b = pkg.VectorEngine(device=0, prefilter=False)
+for e in (a, b):
+    e.create_collection("neg", dim, pkg.METRIC_DOT, pkg.DTYPE_BF16, n)
+    e.upsert("neg", np.arange(n, dtype=np.uint64), X)
+out = {"mismatch": []}
+for i in range(4):
+    Q = u[None, :] + 0.05 * rng.standard_normal((nq, dim)).astype(np.float32) / dim ** 0.5
+    s1, r1, c1 = a.search("neg", Q, k)
+    s2, r2, c2 = b.search("neg", Q, k)
+    if not (np.array_equal(r1, r2) and np.array_equal(s1.view(np.uint32), s2.view(np.uint32))):
+        out["mismatch"].append(i)
+    out["max_kth"] = float(s1[:, k - 1].max())
+out["stats"] = a.spec_stats("neg")
+a.close(); b.close()
+print(json.dumps(out))
+"""
+
+
+def test_no_positive_kth_never_speculates():
+    """a dot collection whose k-th scores are all <= 0 records no
+    ratio; the batches after its first must not run on an unset bound (r05
+    ran them with bound = -inf: every row admitted). The device sees the
+    ratio unset and stands the speculative launches down, so the sample path
+    answers: keys equal the bf16 pass's, and no speculative batch is counted."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, VS_CONTEXTS="1")
+    p = subprocess.run([sys.executable, "-c", "ROOT = %r\n" % root + _NEG], env=e, cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["mismatch"] == [], r
+    assert r["max_kth"] < 0, r
+    assert r["stats"]["tries"] == 0 and r["stats"]["skipped"] >= 3, r["stats"]
