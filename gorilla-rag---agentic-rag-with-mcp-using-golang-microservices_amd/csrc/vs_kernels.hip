@@ -4466,9 +4466,10 @@ hipError_t launch_merge(const uint64_t* lists, uint32_t L, uint64_t lstride,
 //     U reaches P are rescored on the GEMV's own per-row arithmetic
 //     (gemv_row_score: the same loads, chunk_dot, order and wave_sum, hence
 //     the same bits); a list that dropped a key whose U reaches P is replaced
-//     by every row of its scan workgroup. Each finishing workgroup writes its
-//     sorted top k (gemv_emit), and the last one (agent-scope hand-off, as
-//     gemv_one_finish) merges those lists (merge_query).
+//     by every row of its scan workgroup. Each finishing workgroup appends
+//     the keys of its waves' top k whose score reaches P (nothing under P can
+//     be in the top k) with one agent-scope add, and the last one
+//     (agent-scope hand-off, as gemv_one_finish) sorts that short array.
 // Every row of the GEMV's top k has U >= s >= k-th score >= P, so it is
 // rescored and its key is the GEMV's: the answer equals the GEMV's bit for bit.
 #ifndef VS_Q8G_LISTS
@@ -4837,12 +4838,40 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     atomicAdd(&stats[0], rescored);
     if (w == 0) atomicAdd(&stats[1], (uint32_t)__popc(fb));
   }
-  // 4. the workgroup's top k -> its sorted list cand[block][k] (r06: by rank,
-  // gemv_emit, as the scan's lists; r05 appended every wave's keys through one
-  // agent-scope counter, and the last workgroup sorted the pile)
-  gemv_emit<KPL>(R, theta, k, lane, w, cand);
-  // 5. hand-off: the last workgroup merges the sorted lists (merge_query's
-  // list walk, as the GEMV's own merge)
+  // 4. the keys that can still be in the top k -> one compact array. P is at
+  // most the k-th score (k distinct rows have L >= P), so a key whose exact
+  // score image is under P cannot be; every key at or above it was rescored
+  // (its U >= its score >= P). One agent-scope add per workgroup reserves its
+  // place (r06: r05 appended every wave's top k through that counter, ~300
+  // adds, and the last workgroup sorted the pile; before this form each
+  // workgroup wrote its merged top k and the last merged 96 lists).
+  __shared__ uint32_t wcnt[kGemvWaves], wbase;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i)
+    mine += (uint32_t)__popcll(__ballot(R.e[i] != 0 && (uint32_t)(R.e[i] >> 32) >= P));
+  if (lane == 0) wcnt[w] = mine;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tot = 0;
+    for (int j = 0; j < kGemvWaves; ++j) tot += wcnt[j];
+    wbase = tot ? __hip_atomic_fetch_add(&ctr[1], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                : 0u;
+  }
+  __syncthreads();
+  {
+    uint32_t at = wbase;
+    for (int j = 0; j < w; ++j) at += wcnt[j];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const bool keep = R.e[i] != 0 && (uint32_t)(R.e[i] >> 32) >= P;
+      const uint64_t bal = __ballot(keep);
+      const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      if (keep) cand[at + rank] = R.e[i];
+      at += (uint32_t)__popcll(bal);
+    }
+  }
+  // 5. hand-off: the last workgroup takes the top k of the array
   __shared__ uint64_t mbuf[kMergeCap];
   __shared__ uint64_t red[kMergeThreads / 64];
   __shared__ uint32_t mcnt;
@@ -4859,15 +4888,33 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      mcnt = __hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
   stamp(5);
   if (!last) return;
-  // (merge_query's tournament instead of the list walk: 36.7 against 20.2 us
-  // for the whole finish at C2, profiles/r06_c2ab_*)
-  merge_query(cand, gridDim.x, k, 0, k, k, 0, dst, mbuf, red, mcnt, false);
-  if (tid == 0) __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t N = mcnt;
+  __syncthreads();
+  if (N <= 64) {  // the usual case: a few keys past P; one wave sorts them
+    if (w == 0) {
+      const uint64_t x = wave_sort_desc((uint32_t)lane < N ? cand[lane] : 0ull, lane);
+      for (uint32_t j = (uint32_t)lane; j < k; j += 64) dst[j] = j < 64 ? x : 0ull;
+    }
+  } else if (N <= (uint32_t)kMergeCap) {  // sorted in LDS
+    int p2 = 64;
+    while ((uint32_t)p2 < N) p2 <<= 1;
+    for (uint32_t i = tid; i < (uint32_t)p2; i += kGemvThreads) mbuf[i] = i < N ? cand[i] : 0ull;
+    __syncthreads();
+    bitonic_sort_desc_n(mbuf, p2, kGemvThreads);
+    for (uint32_t j = tid; j < k; j += kGemvThreads) dst[j] = j < N ? mbuf[j] : 0ull;
+  } else {  // (P = 0: fewer than k scanned rows' bounds) every key, N lists of one
+    merge_query(cand, N, 1, 0, 1, k, 0, dst, mbuf, red, mcnt, false);
+  }
+  if (tid == 0) {
+    __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   stamp(6);
   if (flag) publish_host(flag, seq);
 }
