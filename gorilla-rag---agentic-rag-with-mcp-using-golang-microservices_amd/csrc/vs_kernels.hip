@@ -4727,7 +4727,9 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
   // 1. P: the radix floor of the k-th largest workgroup L image (0 = a
   // workgroup without rows; one per scan workgroup since r06), 0 when fewer
   // than k are nonzero. (A per-wave bit-by-bit select over the 768 values,
-  // no barriers, measured slower: tools/c2_finish, profiles/r06_c2_finish_*.)
+  // no barriers, and an exact rank count of every value against all m in LDS
+  // (36 us against 5.5) both measured slower: tools/c2_finish,
+  // profiles/r06_c2_finish_*.)
   // The values are read from global memory once, into registers (up to
   // kQ8gHeld per thread: every grid of gfx950's 256 CUs), not once a pass.
   const uint32_t m = nscan;
