@@ -463,7 +463,7 @@ def main():
 
     stream_fn = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     # every timed step keeps its own result buffer (checked after the timer)
-    ring = max(args.steps, 100)  # >= every phase's timed steps (the single-query line: 100)
+    ring = max(args.steps, 160)  # >= every phase's timed steps (the single-query line: 160)
     ls, mg = shard.engine_callables(eng, coll, dim, stream_fn, reuse=True, ring=ring)
     sharded = shard.ShardedSearch(ls, mg, always_gather=force_dist)
     # the data-path exchange: the engine's own RCCL communicator (all-gather +
@@ -559,10 +559,10 @@ def main():
 
     # secondary: the single-query GEMV line on the same resident corpus
     if not args.no_secondary and batch > 1:
-        # 100+ single-query steps after 10 of warmup: at ~2.3 ms each the line
-        # costs a quarter second, and its sampled kernel average (every 4th
-        # launch) then rests on 25+ launches instead of 13
-        steps1 = max(100, args.steps)
+        # 160+ single-query steps after 10 of warmup: at ~1.3 ms each the line
+        # costs a fifth of a second, and its sampled kernel average (every 16th
+        # launch) rests on 10+ launches
+        steps1 = max(160, args.steps)
         el1, tm1, outs1, qs1 = run_phase(eng, sharded, coll, dim, 1, k, steps1, 10, dist_on,
                                          stream_fn, 1000)
         r1 = scan_roofline(args.config + "b1", hi - lo, dim, dtype, 1, k, tm1["scan_ms"], False,

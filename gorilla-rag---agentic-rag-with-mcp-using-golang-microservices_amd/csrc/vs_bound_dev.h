@@ -33,49 +33,75 @@ __device__ __forceinline__ float q8_sigma(uint32_t dim, float q_norm_up) {
   return (float)((4.0 * dim + 64.0) * 0x1p-24 * (double)q_norm_up * (1.0 + 0x1p-20));
 }
 
+// One 8-bit radix digit (r06): the digit of a complete 256-bin histogram
+// (LDS, 16-B aligned) holding the kk-th largest value, and the count of
+// values above that digit, worked out by every wave on its own -- lane l
+// takes digits 255 - 4l .. 252 - 4l (descending), a wave prefix sum, a ballot
+// -- so the pick needs no LDS round trip and no barrier after it (the form it
+// replaced split the scan over 4 waves and shared the pick: 4 more barriers a
+// pass). false: the histogram holds fewer than kk values.
+__device__ __forceinline__ bool wave_digit_pick(const uint32_t* hist, uint32_t kk, uint32_t lane,
+                                                uint32_t& dig, uint32_t& above) {
+  const uint4 o = *(const uint4*)(hist + 252 - 4 * lane);
+  const uint32_t s4 = o.x + o.y + o.z + o.w;
+  uint32_t x = s4;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  const uint64_t bal = __ballot(x >= kk);
+  if (bal == 0) return false;
+  const int L = __builtin_ctzll(bal);
+  const uint32_t ow = __builtin_amdgcn_readlane(o.w, L), oz = __builtin_amdgcn_readlane(o.z, L),
+                 oy = __builtin_amdgcn_readlane(o.y, L);
+  uint32_t a = __builtin_amdgcn_readlane(x - s4, L), g = 255u - 4u * (uint32_t)L;
+  if (a + ow < kk) {
+    a += ow, --g;
+    if (a + oz < kk) {
+      a += oz, --g;
+      if (a + oy < kk) a += oy, --g;
+    }
+  }
+  dig = g, above = a;
+  return true;
+}
+
+constexpr int kBoundMaxPasses = 4;
+
 // One workgroup of kBoundThreads: bound[q] = the radix-select lower bound on
-// the k-th largest of the m values at tmax + q * m (`passes` 8-bit digits).
+// the k-th largest of the m values at tmax + q * m (`passes` <= 4 8-bit
+// digits). One histogram a pass, zeroed up front: one barrier a pass (r06;
+// five before).
 __device__ __forceinline__ void sample_bound_block(const float* __restrict__ tmax, uint32_t m,
                                                    uint32_t k, float* __restrict__ bound,
                                                    int passes, uint32_t q) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t wsum[kBoundThreads / 64];
-  __shared__ uint32_t pick, above;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ __attribute__((aligned(16))) uint32_t hist[kBoundMaxPasses][256];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   if (m < k) {
     if (tid == 0) bound[q] = -INFINITY;
     return;
   }
   const float* v = tmax + (size_t)q * m;
+  for (uint32_t i = tid; i < (uint32_t)(kBoundMaxPasses * 256); i += kBoundThreads)
+    (&hist[0][0])[i] = 0;
+  __syncthreads();
   uint32_t prefix = 0, kk = k;  // the kk-th largest of the values matching prefix
 #pragma unroll 1
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = 24 - 8 * pass;
     const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-    hist[tid] = 0;
-    __syncthreads();
     for (uint32_t i = tid; i < m; i += kBoundThreads) {
       const uint32_t u = ord_f32(v[i]);
-      if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+      if ((u & hmask) == prefix) atomicAdd(&hist[pass][(u >> shift) & 255u], 1u);
     }
     __syncthreads();
-    // inclusive scan over the digits in descending order (thread t: digit 255 - t)
-    const uint32_t c = hist[255 - tid];
-    uint32_t x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    for (uint32_t j = 0; j < w; ++j) x += wsum[j];
-    // exactly one digit has (count above) < kk <= (count above + its own)
-    if (x >= kk && x - c < kk) pick = tid, above = x - c;
-    __syncthreads();
-    prefix |= (uint32_t)(255 - pick) << shift;
+    // m >= k values: some digit holds the kk-th (the prefix's bucket holds kk
+    // or more by construction)
+    uint32_t dig = 0, above = 0;
+    wave_digit_pick(hist[pass], kk, lane, dig, above);
+    prefix |= dig << shift;
     kk -= above;
-    __syncthreads();  // pick / above / wsum / hist are rewritten by the next pass
   }
   // the bucket of -inf starts below ord(-inf), in the negative-NaN codes
   if (tid == 0) bound[q] = prefix <= ord_f32(-INFINITY) ? -INFINITY : unord_f32(prefix);

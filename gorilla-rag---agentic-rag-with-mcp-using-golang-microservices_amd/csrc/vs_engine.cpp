@@ -107,7 +107,7 @@ bool timing_wanted(DevEngine* eng, const std::vector<EventPair>& v) {
 hipError_t ev_begin(DevEngine* eng, std::vector<EventPair>& v) {
   if (!timing_wanted(eng, v)) return hipSuccess;
   if (&v == &eng->scan_ev && (eng->flags & VS_FLAG_TIMING_SAMPLE)) {
-    eng->scan_skip = (eng->scan_tick++ & 3) != 0;  // bracket every 4th scan only
+    eng->scan_skip = (eng->scan_tick++ & 15) != 0;  // bracket every 16th scan only
     if (eng->scan_skip) return hipSuccess;
   }
   EventPair p{};

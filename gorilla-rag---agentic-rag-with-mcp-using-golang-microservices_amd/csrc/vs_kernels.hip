@@ -3455,7 +3455,7 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   __shared__ uint32_t wtot[kSelThreads / 64];
   __shared__ uint32_t wscr[kSelThreads / 64][16];  // a wave's group of 16 rows
   __shared__ uint32_t fill, spill, rfill;
-  __shared__ uint32_t hist[256], hws[4], hpick, habove;  // kth_floor's radix state
+  __shared__ __attribute__((aligned(16))) uint32_t hist[3][256];  // kth_floor's histograms
   // (tools/share_pipe.hip) per-workgroup wall clock at the stage boundaries:
   // 0 start, 1 bound, 2 survivors, 3 rescore, 4 end; two rounds: 5 first
   // floor, 6 first round, 7 second floor; inside the survivor stage (thread
@@ -3501,39 +3501,26 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   // have a high word >= P. Three 8-bit radix passes as the sample bound
   // (vs_bound_dev.h), over LDS. (r05: every k; the register sorts and wave
   // merges it replaced cost ~4 us per use in the select's latency chain.)
+  // (r06) a histogram a pass, zeroed up front, and wave_digit_pick: 5
+  // barriers a call instead of 15. 0 (no floor) if n < kk.
   auto kth_floor = [&](const uint64_t* v, uint32_t n, uint32_t kk) -> uint32_t {
+    __syncthreads();  // the previous call's waves are done with hist
+    for (uint32_t i = tid; i < 3 * 256; i += kSelThreads) (&hist[0][0])[i] = 0;
+    __syncthreads();
     uint32_t prefix = 0;
-#pragma unroll 1
+#pragma unroll
     for (int pass = 0; pass < 3; ++pass) {
       const int shift = 24 - 8 * pass;
       const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-      if (tid < 256) hist[tid] = 0;
-      __syncthreads();
       for (uint32_t i = tid; i < n; i += kSelThreads) {
         const uint32_t u = (uint32_t)(v[i] >> 32);
-        if ((u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+        if ((u & hmask) == prefix) atomicAdd(&hist[pass][(u >> shift) & 255u], 1u);
       }
       __syncthreads();
-      uint32_t c = 0, x = 0;
-      if (tid < 256) {
-        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
-        x = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) hws[w] = x;
-      }
-      __syncthreads();
-      if (tid < 256) {
-        for (uint32_t j = 0; j < w; ++j) x += hws[j];
-        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
-      }
-      __syncthreads();
-      prefix |= (255u - hpick) << shift;
-      kk -= habove;
-      __syncthreads();  // hist / hws / hpick are rewritten by the next pass
+      uint32_t dig, above;
+      if (!wave_digit_pick(hist[pass], kk, lane, dig, above)) return 0u;  // uniform
+      prefix |= dig << shift;
+      kk -= above;
     }
     return prefix;
   };
@@ -4709,7 +4696,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
   using SQ = Q8GemvShape<D>;
   constexpr int KP = 64 * KPL;
   __shared__ float qs[D];
-  __shared__ uint32_t hist[256], hws[4], hpick, habove, nz_sh;
+  __shared__ __attribute__((aligned(16))) uint32_t hist[kQ8gPasses][256];
   __shared__ uint64_t surv[kQ8gLists * KP];
   __shared__ uint32_t ns_sh, fb_sh;
   const int lane = threadIdx.x & 63;
@@ -4720,8 +4707,27 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
     if (clk && tid == 0) clk[(size_t)blockIdx.x * 8 + s] = wall_clock64();
   };
   stamp(0);
+  // (r06) the scan's outputs this workgroup reads -- the L images for P and
+  // its lists' entries -- are loaded before the query's prep, so their
+  // latency runs under it
+  const uint32_t m = nscan;
+  uint32_t lv[kQ8gHeld];
+#pragma unroll
+  for (int j = 0; j < kQ8gHeld; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kGemvThreads;
+    lv[j] = i < m ? lbest[i] : 0u;
+  }
+  constexpr int kHeldE = (kQ8gLists * KP + kGemvThreads - 1) / kGemvThreads;
+  const uint32_t l0 = blockIdx.x * kQ8gLists;
+  uint64_t ev[kHeldE];
+#pragma unroll
+  for (int t = 0; t < kHeldE; ++t) {
+    const uint32_t i = tid + (uint32_t)t * kGemvThreads, l = l0 + i / KP;
+    ev[t] = i < (uint32_t)(kQ8gLists * KP) && l < nscan ? ulist[(size_t)l * KP + i % KP] : 0ull;
+  }
   if (w == 0) prep_query_wave<D>(q_raw, prep, qs, lane);
-  if (tid == 0) ns_sh = 0, fb_sh = 0, nz_sh = 0;
+  if (tid == 0) ns_sh = 0, fb_sh = 0;
+  for (uint32_t i = tid; i < (uint32_t)(kQ8gPasses * 256); i += kGemvThreads) (&hist[0][0])[i] = 0;
   __syncthreads();
   stamp(1);
   // 1. P: the radix floor of the k-th largest workgroup L image (0 = a
@@ -4730,67 +4736,44 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_q8_finish_kernel(
   // no barriers, and an exact rank count of every value against all m in LDS
   // (36 us against 5.5) both measured slower: tools/c2_finish,
   // profiles/r06_c2_finish_*.)
-  // The values are read from global memory once, into registers (up to
-  // kQ8gHeld per thread: every grid of gfx950's 256 CUs), not once a pass.
-  const uint32_t m = nscan;
+  // The values are held in registers (up to kQ8gHeld per thread: every grid
+  // of gfx950's 256 CUs), read from global memory once, not once a pass.
+  // (r06) One barrier a pass: every pass has its own histogram (zeroed before
+  // the prep's barrier) and every wave picks the digit itself
+  // (wave_digit_pick, vs_bound_dev.h; before: 5 barriers a pass).
   uint32_t P = 0;
   {
-    uint32_t lv[kQ8gHeld];
     uint32_t prefix = 0, kk = k;
-    {
-      uint32_t nz = 0;
+    bool some = true;
 #pragma unroll
-      for (int j = 0; j < kQ8gHeld; ++j) {
-        const uint32_t i = tid + (uint32_t)j * kGemvThreads;
-        lv[j] = i < m ? lbest[i] : 0u;
-        nz += lv[j] != 0u;
-      }
-      if (nz) atomicAdd(&nz_sh, nz);  // complete at the first pass's barrier
-    }
-#pragma unroll 1
     for (int pass = 0; pass < kQ8gPasses; ++pass) {
       const int shift = 24 - 8 * pass;
       const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-      if (tid < 256) hist[tid] = 0;
-      __syncthreads();
-      if (nz_sh < k) break;  // uniform: fewer than k rows scanned -> P = 0
 #pragma unroll
       for (int j = 0; j < kQ8gHeld; ++j) {
         const uint32_t u = lv[j];
-        if (u && (u & hmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+        if (u && (u & hmask) == prefix) atomicAdd(&hist[pass][(u >> shift) & 255u], 1u);
       }
       __syncthreads();
-      uint32_t c = 0, x = 0;
-      if (tid < 256) {
-        c = hist[255 - tid];  // thread t: digit 255 - t (descending)
-        x = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        if (lane == 63) hws[w] = x;
+      // fewer than kk values under the prefix: only when fewer than k are
+      // nonzero (pass 0); P = 0 then
+      uint32_t dig, above;
+      if (!wave_digit_pick(hist[pass], kk, (uint32_t)lane, dig, above)) {
+        some = false;
+        break;
       }
-      __syncthreads();
-      if (tid < 256) {
-        for (int j = 0; j < w; ++j) x += hws[j];
-        if (x >= kk && x - c < kk) hpick = tid, habove = x - c;
-      }
-      __syncthreads();
-      prefix |= (255u - hpick) << shift;
-      kk -= habove;
-      __syncthreads();
+      prefix |= dig << shift;
+      kk -= above;
     }
-    P = nz_sh < k ? 0u : prefix;
+    P = some ? prefix : 0u;
   }
   stamp(2);
   // 2. the lists' entries whose U reaches P; a list whose dropped keys may
   // reach P (its last entry does) is replaced by all of its workgroup's rows
-  const uint32_t l0 = blockIdx.x * kQ8gLists;
-  for (uint32_t i = tid; i < (uint32_t)(kQ8gLists * KP); i += kGemvThreads) {
-    const uint32_t l = l0 + i / KP, j = i % KP;
-    if (l >= nscan) continue;
-    const uint64_t e = ulist[(size_t)l * KP + j];
+#pragma unroll
+  for (int t = 0; t < kHeldE; ++t) {
+    const uint32_t i = tid + (uint32_t)t * kGemvThreads, l = l0 + i / KP, j = i % KP;
+    const uint64_t e = ev[t];  // 0 past the lists
     if (j == KP - 1 && e != 0 && (uint32_t)(e >> 32) >= P) atomicOr(&fb_sh, 1u << (l - l0));
     if (e != 0 && (uint32_t)(e >> 32) >= P) surv[atomicAdd(&ns_sh, 1u)] = e;
   }

@@ -84,9 +84,9 @@ typedef struct vs_config {
  * few microseconds of device idle between launches, so the benchmark times
  * scans only. */
 #define VS_FLAG_TIMING_MERGE 2u
-/* With VS_FLAG_TIMING: bracket only every 4th scan launch, starting with the
- * first after a vs_timing reset (a sampled
- * average that keeps the event gaps out of 3 of 4 steps). */
+/* With VS_FLAG_TIMING: bracket only every 16th scan launch, starting with the
+ * first after a vs_timing reset (a sampled average that keeps the event gaps
+ * out of 15 of 16 steps; every 4th cost a single-query step 1.5%). */
 #define VS_FLAG_TIMING_SAMPLE 4u
 /* vs_open_multi only: place every collection WHOLE on one of the engine's
  * devices (the one with the fewest bytes reserved by capacity hints, then
