@@ -638,8 +638,18 @@ double plain_sample_scale() {
 //     pass is ever re-run and nothing here waits on the device.
 // Small collections (fewer than 8 tiles per workgroup) take the sorted-list
 // pass (k <= 16) or the GEMV path.
+// The query preprocessing search_core leaves to search_mfma (r06): enqueued
+// first on every path, except that a speculative int8 batch fuses it into its
+// first launch (launch_q8_prep_query).
+struct QPrep {
+  const float* in;
+  bool cosine, round_qp;
+  float* qp;     // fp32 copy (or null)
+  uint16_t* qb;  // bf16 copy (or null)
+};
+
 int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t k,
-                uint64_t* d_keys, const uint64_t* allow) {
+                uint64_t* d_keys, const uint64_t* allow, const QPrep& prep) {
   const uint32_t dim = c.dim;
   const uint32_t n_rows = (uint32_t)c.rows;
   const uint32_t row_base = (uint32_t)c.row_base;
@@ -650,7 +660,17 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const uint32_t maxl = vsk::mfma_max_lists(n_rows);
   const uint32_t tpw = vsk::mfma_tiles_per_wg(n_rows);
   const bool fast = tpw >= 8;
-  if (!fast && k > vsk::kMfmaListMaxK) return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
+  auto prep_now = [&]() -> int {
+    VS_HIP(vsk::launch_query_prep(prep.in, nq, dim, prep.cosine, prep.round_qp, prep.qp, prep.qb,
+                                  eng->stream),
+           "query preprocess");
+    return VS_OK;
+  };
+  if (!fast && k > vsk::kMfmaListMaxK) {
+    const int rc = prep_now();
+    if (rc != VS_OK) return rc;
+    return search_gemv(eng, c, qp, 0, nq, k, d_keys, allow);
+  }
   // int8 prefilter (batches of a collection with an int8 copy; a pre-mask
   // rides along as in the bf16 pass)
   const bool q8 = fast && c.q8 && c.q8_cap >= c.rows && q8_enabled();
@@ -737,6 +757,13 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                        c.spec_host_skips);
     const int spec_k = plan.spec_k;
     const bool record = plan.record;
+    // (r06) one speculative launch (the whole batch in one int8 launch) makes
+    // the preprocessed queries too; every other batch preprocesses first
+    const bool fused_prep = spec_k >= 0 && nq <= P8 && dim <= vsk::kQueryPrepFusedMaxDim;
+    if (!fused_prep) {
+      const int rc = prep_now();
+      if (rc != VS_OK) return rc;
+    }
     vsk::Q8SpecK* sk = vsk::q8_spec_k(c.q8_glob);
     vsk::Q8SpecStat* sstat = vsk::q8_spec_stat(c.q8_glob);
     const uint32_t* verdict = gate + vsk::kGateVerdict;
@@ -753,9 +780,15 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
           VS_HIP(hipMemsetAsync(gate + vsk::kGateForced, 0x41, 4, eng->stream), "forced ratio");
           r_use = (const float*)(gate + vsk::kGateForced);
         }
-        VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream,
-                                    r_use, bound, &sk[k], sstat, force),
-               "int8 queries + speculative bound");
+        if (fused_prep)
+          VS_HIP(vsk::launch_q8_prep_query(prep.in, prep.cosine, prep.round_qp, prep.qp, prep.qb, f32,
+                                           nv, dim, c.q8_glob, q8q, q8par, gate, eng->stream, r_use,
+                                           bound, &sk[k], sstat, force),
+                 "query preprocess + int8 queries + speculative bound");
+        else
+          VS_HIP(vsk::launch_q8_query(qptr(q0), f32, nv, dim, c.q8_glob, q8q, q8par, gate,
+                                      eng->stream, r_use, bound, &sk[k], sstat, force),
+                 "int8 queries + speculative bound");
         VS_HIP(ev_begin(eng, eng->scan_ev), "event");
         VS_HIP(vsk::launch_mfma_cand_q8(c.q8, dim, n_rows, row_base, q8q, nv, k, bound, q8par,
                                         c.q8_glob, slabs, slab_tile, cap8, cnt, qmax, maxl, &L, gate,
@@ -818,6 +851,10 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     }
     if (spec_rec) spec_seen_mark(plan, k);
     return VS_OK;
+  }
+  {
+    const int rc = prep_now();
+    if (rc != VS_OK) return rc;
   }
   for (uint32_t p = 0; p < npass; ++p) {
     const uint32_t q0 = p * P;
@@ -1034,10 +1071,12 @@ int search_core(DevEngine* eng, Collection& c, const float* d_q, uint32_t nq, ui
   // path needs it only where small collections send k > 16 to the GEMV path
   const bool need_qp = !use_mfma || !bf16 ||
                        (k > vsk::kMfmaListMaxK && vsk::mfma_tiles_per_wg((uint32_t)c.rows) < 8);
+  if (use_mfma)  // (r06) it enqueues the preprocessing itself (QPrep)
+    return search_mfma(eng, c, qp, nq, k, d_keys, allow,
+                       QPrep{d_q, cosine, bf16, need_qp ? qp : nullptr, qb});
   VS_HIP(vsk::launch_query_prep(d_q, nq, dim, cosine, bf16, need_qp ? qp : nullptr, qb,
                                 eng->stream),
          "query preprocess");
-  if (use_mfma) return search_mfma(eng, c, qp, nq, k, d_keys, allow);
   // k past the list scans, or past the list path's break-even on a streamed
   // scan (a selective filter's gather reads only its rows: lists up to 1024)
   if (k > vsk::kMaxK || (k >= large_k_from() && !gather))

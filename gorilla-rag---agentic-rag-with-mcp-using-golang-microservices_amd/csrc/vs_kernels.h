@@ -342,6 +342,17 @@ hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, c
                            const float* ratio = nullptr, float* bound = nullptr,
                            Q8SpecK* spec_k = nullptr, Q8SpecStat* stat = nullptr,
                            bool force = false);
+constexpr uint32_t kQueryPrepFusedMaxDim = 1536;  // = 64 x vs_qprep_dev.h kQPrepMax
+// (r06) The speculative form of launch_q8_query fused with launch_query_prep
+// (dim <= kQueryPrepFusedMaxDim): the raw fp32 queries `in` -> qp / qbf exactly as
+// launch_query_prep(in, nq, dim, cosine, round_qp, qp, qbf) writes them, and
+// the int8 images, bounds and go / verdict words exactly as launch_q8_query
+// over qp (f32) or qbf -- one launch.
+hipError_t launch_q8_prep_query(const float* in, bool cosine, bool round_qp, float* qp,
+                                uint16_t* qbf, bool f32, uint32_t nq, uint32_t dim,
+                                const float* glob, int8_t* q8, float* q8par, uint32_t* gate,
+                                hipStream_t st, const float* ratio, float* bound, Q8SpecK* spec_k,
+                                Q8SpecStat* stat, bool force);
 // After a batch's select (one workgroup; nq <= kMfmaQueries). check (a
 // speculative batch): a query whose k-th exact score is under its bound -
 // sigma nmax fails it; any failure sets gate[kGateVerdict] (the sample path

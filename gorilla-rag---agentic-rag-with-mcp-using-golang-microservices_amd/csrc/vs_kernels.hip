@@ -25,6 +25,7 @@
 #include "vs_common.h"
 #include "vs_bound_dev.h"
 #include "vs_kernels.h"
+#include "vs_qprep_dev.h"
 
 namespace vsk {
 
@@ -162,14 +163,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
   }
 }
 
-// Query side (search): one wave per query, dim <= 64 * kQPrepMax. All of a
-// lane's elements are loaded at once (one memory latency instead of dim/64
-// dependent ones: 9 -> ~4 us per batch), the squared norm is summed in the
-// store side's order (lane l: elements l, l+64, ... in sequence, then the
-// same butterfly) and only for cosine, and each output is optional: qp =
-// fp32 (rounded to bf16 values when round_qp: what a bf16 scan multiplies),
-// qb = bf16 copy.
-constexpr int kQPrepMax = 24;  // dim <= 1536
+// Query side (search): one wave per query, dim <= 64 * kQPrepMax
+// (vs_qprep_dev.h query_prep_one).
 __global__ __launch_bounds__(256) void query_prep_kernel(const float* __restrict__ in, uint32_t n,
                                                          uint32_t dim, int cosine, int round_qp,
                                                          float* __restrict__ qp,
@@ -177,35 +172,7 @@ __global__ __launch_bounds__(256) void query_prep_kernel(const float* __restrict
   const int lane = threadIdx.x & 63;
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
-  const float* x = in + (size_t)i * dim;
-  float v[kQPrepMax];
-#pragma unroll
-  for (int j = 0; j < kQPrepMax; ++j) {
-    const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
-    v[j] = d < dim ? x[d] : 0.f;
-  }
-  bool keep = true;
-  double nrm = 1.0;
-  if (cosine) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = 0; j < kQPrepMax; ++j) {
-      const double t = (double)v[j];
-      s = s + t * t;  // zero padding adds exact zeros: same sum as the store side
-    }
-    s = wave_sum_f64(s);
-    keep = vs::cosine_keep(s);
-    nrm = sqrt(s);
-  }
-#pragma unroll
-  for (int j = 0; j < kQPrepMax; ++j) {
-    const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
-    if (d >= dim) break;
-    const float y = keep ? v[j] : (float)((double)v[j] / nrm);
-    const uint16_t h = vs::f32_to_bf16(y);
-    if (qp) qp[(size_t)i * dim + d] = round_qp ? vs::bf16_to_f32(h) : y;
-    if (qb) qb[(size_t)i * dim + d] = h;
-  }
+  query_prep_one(in, i, dim, cosine, round_qp, qp, qb, lane);
 }
 
 hipError_t launch_query_prep(const float* in, uint32_t n, uint32_t dim, bool cosine,

@@ -17,6 +17,7 @@
 #include "vs_bound_dev.h"
 #include "vs_common.h"
 #include "vs_kernels.h"
+#include "vs_qprep_dev.h"
 
 namespace vsk {
 namespace {
@@ -163,7 +164,8 @@ __device__ __forceinline__ void spec_decide(const float* __restrict__ ratio, Q8S
 }
 
 // One wave per query (bf16 queries of a bf16 collection, or the fp32
-// preprocessed queries of an fp32 one).
+// preprocessed queries of an fp32 one; with `src`, this wave's query read
+// from there -- its LDS copy -- instead of from qb).
 // (r05) With `ratio` (a collection's learned k-th score per unit |q|, DESIGN.md
 // §5 "Speculative bound"), also bound[i] = ratio x |q| (-inf while the ratio
 // is unset: the batch then stands down, spec_decide).
@@ -177,7 +179,7 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
                                                float* __restrict__ bound = nullptr,
                                                Q8SpecK* __restrict__ sk = nullptr,
                                                Q8SpecStat* __restrict__ stat = nullptr,
-                                               bool force = false) {
+                                               bool force = false, const void* src = nullptr) {
   if (gate && blk == 0 && threadIdx.x == 0) {
     if (sk)
       spec_decide(ratio, sk, stat, gate, force);
@@ -188,10 +190,12 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
   if (i >= nq) return;
   const int lane = threadIdx.x & 63;
   const uint64_t x = (uint64_t)i * dim;
+  const void* qv = src ? src : qb;
+  const uint64_t x_in = src ? 0 : x;
   float amax = 0.f;
   for (uint32_t d = 2 * lane; d < dim; d += 128) {
     float x0, x1;
-    load2<F32>(qb, x + d, true, x0, x1);
+    load2<F32>(qv, x_in + d, true, x0, x1);
     amax = fmaxf(amax, fmaxf(fabsf(x0), fabsf(x1)));
   }
   amax = wave_max_f(amax);
@@ -199,7 +203,7 @@ __device__ __forceinline__ void q8_query_block(uint32_t blk, const void* __restr
   double aa = 0.0, cc = 0.0, nn = 0.0;
   for (uint32_t d = 2 * lane; d < dim; d += 128) {
     float x0, x1;
-    load2<F32>(qb, x + d, true, x0, x1);
+    load2<F32>(qv, x_in + d, true, x0, x1);
     const float y0 = sq > 0.f ? fminf(fmaxf(rintf(x0 / sq), -127.f), 127.f) : 0.f;
     const float y1 = sq > 0.f ? fminf(fmaxf(rintf(x1 / sq), -127.f), 127.f) : 0.f;
     const double s0 = (double)sq * (double)y0, s1 = (double)sq * (double)y1;
@@ -242,6 +246,31 @@ __global__ __launch_bounds__(256) void q8_query_kernel(const void* __restrict__ 
                                                        Q8SpecStat* __restrict__ stat, uint32_t force) {
   q8_query_block<F32>(blockIdx.x, qb, nq, dim, glob, q8, q8par, gate, ratio, bound, sk, stat,
                       force != 0u);
+}
+
+// (r06) The speculative path's first launch: the queries' preprocessing
+// (query_prep_kernel's, vs_qprep_dev.h, bit for bit) fused with their int8
+// images and the speculative bound (q8_query_kernel's, reading each query
+// from the wave's LDS copy instead of from global memory): one launch and one
+// kernel boundary instead of two.
+static_assert(64u * kQPrepMax == kQueryPrepFusedMaxDim, "the fused launch's dim limit");
+template <bool F32>
+__global__ __launch_bounds__(256) void q8_prep_query_kernel(
+    const float* __restrict__ in, uint32_t nq, uint32_t dim, int cosine, int round_qp,
+    float* __restrict__ qp, uint16_t* __restrict__ qbf, const float* __restrict__ glob,
+    int8_t* __restrict__ q8, float* __restrict__ q8par, uint32_t* __restrict__ gate,
+    const float* __restrict__ ratio, float* __restrict__ bound, Q8SpecK* __restrict__ sk,
+    Q8SpecStat* __restrict__ stat, uint32_t force) {
+  // a wave's query as the int8 image reads it: fp32 (F32) or bf16 values
+  __shared__ __attribute__((aligned(16))) uint32_t lq[4][(F32 ? 64 : 32) * kQPrepMax];
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = threadIdx.x >> 6, i = blockIdx.x * 4 + w;
+  if (i < nq)
+    query_prep_one(in, i, dim, cosine, round_qp, qp, qbf, lane, F32 ? (float*)lq[w] : nullptr,
+                   F32 ? nullptr : (uint16_t*)lq[w]);
+  __syncthreads();
+  q8_query_block<F32>(blockIdx.x, F32 ? (const void*)qp : (const void*)qbf, nq, dim, glob, q8, q8par,
+                      gate, ratio, bound, sk, stat, force != 0u, lq[w]);
 }
 
 // After a batch's select (one workgroup, thread q = query q): its k-th key's
@@ -390,6 +419,26 @@ hipError_t launch_q8_query(const void* q, bool f32, uint32_t nq, uint32_t dim, c
   else
     hipLaunchKernelGGL(q8_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, q, nq, dim,
                        glob, q8, q8par, gate, ratio, bound, spec_k, stat, force ? 1u : 0u);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_prep_query(const float* in, bool cosine, bool round_qp, float* qp,
+                                uint16_t* qbf, bool f32, uint32_t nq, uint32_t dim,
+                                const float* glob, int8_t* q8, float* q8par, uint32_t* gate,
+                                hipStream_t st, const float* ratio, float* bound, Q8SpecK* spec_k,
+                                Q8SpecStat* stat, bool force) {
+  if (dim % 128 || dim == 0 || dim > 64u * kQPrepMax || !ratio || !bound || !spec_k || !stat ||
+      !gate || (f32 ? !qp : !qbf))
+    return hipErrorInvalidValue;
+  if (nq == 0) return hipSuccess;
+  if (f32)
+    hipLaunchKernelGGL(q8_prep_query_kernel<true>, dim3((nq + 3) / 4), dim3(256), 0, st, in, nq, dim,
+                       (int)cosine, (int)round_qp, qp, qbf, glob, q8, q8par, gate, ratio, bound,
+                       spec_k, stat, force ? 1u : 0u);
+  else
+    hipLaunchKernelGGL(q8_prep_query_kernel<false>, dim3((nq + 3) / 4), dim3(256), 0, st, in, nq,
+                       dim, (int)cosine, (int)round_qp, qp, qbf, glob, q8, q8par, gate, ratio,
+                       bound, spec_k, stat, force ? 1u : 0u);
   return hipGetLastError();
 }
 
