@@ -612,6 +612,19 @@ double q8_sample_scale() {
 
 // VS_Q8_PREP_APART=1: the int8 queries in their own launch (the r04 form
 // before the fused bound + query launch; ablation only, read once)
+// VS_Q8_SEL_VERIFY=1 (ablation): the batch's check / record by the int8
+// select's last workgroup instead of a launch of its own after the select.
+// One launch fewer, and no faster: 0.2768 / 0.2776 against 0.2763 / 0.2759 ms
+// at the N = 8 share, C3 level (profiles/r06_sel_verify_ab.json) -- the last
+// workgroup's hand-off costs what the launch did.
+bool q8_sel_verify() {
+  static const bool v = [] {
+    const char* e = std::getenv("VS_Q8_SEL_VERIFY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 bool q8_prep_apart() {
   static const bool v = [] {
     const char* e = std::getenv("VS_Q8_PREP_APART");
@@ -702,7 +715,7 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
   const size_t scbytes = (size_t)maxl * st * PS * 4;  // tile maxima, [query][wg * st]
   // counts [maxl][PS][4], then (select_qmax) the quarters' maxima, same shape
   const size_t nbytes = (size_t)maxl * PS * 4 * 4 * 2;
-  const size_t q8qb = q8 ? (size_t)PS * dim : 0, q8pb = q8 ? (size_t)PS * 16 + 64 : 0;
+  const size_t q8qb = q8 ? (size_t)PS * dim : 0, q8pb = q8 ? vsk::kQ8ParBytes : 0;
   if (eng->lists.bytes < lbytes || eng->sample_bound.bytes < sbytes || eng->cand.bytes < cbytes ||
       eng->scand.bytes < scbytes || eng->cand_cnt.bytes < nbytes || eng->q8_q.bytes < q8qb ||
       eng->q8_par.bytes < q8pb) {
@@ -714,6 +727,8 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     VS_HIP(eng->cand_cnt.ensure(nbytes), "alloc candidate counts");
     VS_HIP(eng->q8_q.ensure(q8qb), "alloc int8 queries");
     VS_HIP(eng->q8_par.ensure(q8pb), "alloc int8 query bounds");
+    // the select's verify ticket (vsk::kQ8ParBytes) starts at zero
+    if (q8pb) VS_HIP(hipMemsetAsync(eng->q8_par.p, 0, eng->q8_par.bytes, eng->stream), "zero");
   }
   const void* X = c.data;
   uint64_t* lists = eng->lists.as<uint64_t>();
@@ -739,6 +754,8 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
     int8_t* q8q = eng->q8_q.as<int8_t>();
     float* q8par = eng->q8_par.as<float>();
     uint32_t* gate = (uint32_t*)(q8par + 4 * PS);
+    float4* vq = (float4*)((char*)gate + 64);  // the select's verify hand-over
+    uint32_t* ticket = (uint32_t*)(vq + PS);
     // Speculative bound (r05): unfiltered batches whose k (or a
     // larger k') this context has seen answered in this generation of the
     // copy start from bound = ratio x |q| instead of a sample pass. The
@@ -795,15 +812,20 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                         eng->stream, allow, go),
                "int8 scan");
         VS_HIP(ev_end(eng, eng->scan_ev), "event");
+        // the check: its own launch (or the select's last workgroup: ablation)
+        const vsk::SpecVerifyArgs vchk{1u,    dim,   bound, q8par, c.q8_glob, gate,
+                                       &sk[k], sstat, c.q8_advice_dev + k, vq, ticket};
         VS_HIP(ev_begin(eng, eng->merge_ev), "event");
         VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
                                      qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
-                                     q8q, allow, n_rows, eng->stream, nullptr, nullptr, go),
+                                     q8q, allow, n_rows, eng->stream, nullptr, nullptr, go,
+                                     q8_sel_verify() ? &vchk : nullptr),
                "int8 select");
         VS_HIP(ev_end(eng, eng->merge_ev), "event");
-        VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, true, gate,
-                                            &sk[k], sstat, c.q8_advice_dev + k, eng->stream, go),
-               "speculative bound check");
+        if (!q8_sel_verify())
+          VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, true, gate,
+                                              &sk[k], sstat, c.q8_advice_dev + k, eng->stream, go),
+                 "speculative bound check");
         run_if = verdict;
       }
       // 1. sample pass(es) -> per-query lower bounds on the k-th score; the
@@ -837,13 +859,19 @@ int search_mfma(DevEngine* eng, Collection& c, float* qp, uint32_t nq, uint32_t 
                                       eng->stream, allow, run_if),
              "int8 scan");
       if (!run_if) VS_HIP(ev_end(eng, eng->scan_ev), "event");
+      // the sample path's answer is exact: with `record` it replaces the
+      // ratio (its own launch, or the select's last workgroup: ablation)
+      const vsk::SpecVerifyArgs vrec{0u,    dim,   bound, q8par, c.q8_glob, nullptr,
+                                     &sk[k], sstat, c.q8_advice_dev + k, vq, ticket};
+      const bool rec_in_sel = record && q8_sel_verify();
       if (!run_if) VS_HIP(ev_begin(eng, eng->merge_ev), "event");
       VS_HIP(vsk::launch_select_q8(slabs, slab_tile, cnt, qmax, L, cap8, nv, k, out, row_base, X,
                                    qptr(q0), f32, dim, q8par, c.q8_glob, c.q8_meta, bound, c.q8,
-                                   q8q, allow, n_rows, eng->stream, nullptr, nullptr, run_if),
+                                   q8q, allow, n_rows, eng->stream, nullptr, nullptr, run_if,
+                                   rec_in_sel ? &vrec : nullptr),
              "int8 select");
       if (!run_if) VS_HIP(ev_end(eng, eng->merge_ev), "event");
-      if (record)  // the sample path's answer is exact: it replaces the ratio
+      if (record && !rec_in_sel)
         VS_HIP(vsk::launch_q8_verify_record(out, nv, k, dim, bound, q8par, c.q8_glob, false, nullptr,
                                             &sk[k], sstat, c.q8_advice_dev + k, eng->stream,
                                             run_if),

@@ -266,6 +266,7 @@ hipError_t launch_mfma_cand_q8(const void* X8, uint32_t dim, uint32_t n_rows, ui
 // can hold a top-k row.
 // X / Q: the collection's rows and the pass's queries in its dtype (bf16, or
 // fp32 when f32: survivors rescored on the f32 pass's 16x16x4 chain).
+struct SpecVerifyArgs;  // below
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
                             const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
                             uint32_t k, uint64_t* out,
@@ -275,7 +276,10 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             const uint64_t* allow, uint32_t n_rows, hipStream_t st,
                             uint32_t* stats = nullptr,  // (tools) += slabs read, survivors, slow paths
                             uint64_t* clk = nullptr,    // (tools) [nq][16] stage wall clocks
-                            const uint32_t* run_if = nullptr);  // stand down unless *run_if
+                            const uint32_t* run_if = nullptr,   // stand down unless *run_if
+                            // (r06 ablation) the batch's check or record by the select's
+                            // last workgroup (instead of launch_q8_verify_record after it)
+                            const SpecVerifyArgs* verify = nullptr);
 // Store side (vs_q8.hip; X: bf16 rows, or fp32 rows when f32): glob[0] = max
 // |x| over n values (atomic max; zero it first); glob[3] = S = glob[0] / 127
 // (1 when 0).
@@ -329,6 +333,28 @@ inline Q8SpecK* q8_spec_k(float* glob) { return (Q8SpecK*)((char*)glob + kQ8Spec
 // verdict (the sample path runs unless 0), [1] a forced ratio (tests), [2] go
 // (the speculative launches run unless 0).
 constexpr uint32_t kGateVerdict = 0, kGateForced = 1, kGateGo = 2;
+
+// (r06) What the int8 select's last workgroup needs to check / record a batch
+// (vs_spec_dev.h). vq: one float4 per query (r, |q|, bound, ok) handed over by
+// every workgroup; ticket: one u32, zero between launches (the last workgroup
+// leaves it zero).
+struct SpecVerifyArgs {
+  uint32_t check;  // 1: check a speculative batch; 0: record a sample-path one
+  uint32_t dim;
+  const float* bound;
+  const float* q8par;
+  const float* glob;
+  uint32_t* gate;
+  Q8SpecK* sk;
+  Q8SpecStat* stat;
+  uint32_t* advice;
+  float4* vq;
+  uint32_t* ticket;
+};
+// The int8-query buffer's layout (engine scratch, kMfmaQueries slots): q8par
+// (4 floats a query), then the gate words (64 B), the verify hand-over vq (one
+// float4 a query) and its ticket.
+constexpr size_t kQ8ParBytes = (size_t)kMfmaQueries * 16 + 64 + (size_t)kMfmaQueries * 16 + 64;
 
 // Queries (bf16, or fp32 when f32; nq x dim) -> int8 rows Q8 and q8par[q] =
 // {sq * S, |sq q8|, |q - sq q8|, sigma}, norms rounded up.

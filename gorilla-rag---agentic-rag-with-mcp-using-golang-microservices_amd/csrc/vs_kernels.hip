@@ -26,6 +26,7 @@
 #include "vs_bound_dev.h"
 #include "vs_kernels.h"
 #include "vs_qprep_dev.h"
+#include "vs_spec_dev.h"
 
 namespace vsk {
 
@@ -3405,16 +3406,15 @@ __device__ __forceinline__ int q8_row_dot(const int8_t* __restrict__ xr, const i
   return d;
 }
 
-template <int D, int SV = 0, bool F32 = false>
-__global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
+template <int D, int SV, bool F32>
+__device__ __forceinline__ void select_q8_body(
     const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
     uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
     const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
     const float* __restrict__ q8glob, const float* __restrict__ meta,
     const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from, uint32_t opts,
-    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk, const uint32_t* __restrict__ run_if) {
-  if (run_if && *run_if == 0u) return;  // (r05) the fallback behind a verified speculative batch
+    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk) {
   __shared__ uint64_t buf[kMfmaSelBuf];
   __shared__ uint64_t res[kMfmaSelBuf];  // rescored keys
   __shared__ uint32_t pre[4 * kMfmaMaxLists + 1];
@@ -3879,6 +3879,54 @@ __global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
   tick(4);
 }
 
+// The select kernel: the body above, then -- with SpecVerifyArgs (r06
+// ablation, VS_Q8_SEL_VERIFY=1; measured no faster than the launch it saves)
+// -- the batch's check (a speculative batch) or record (a sample-path one) by
+// the last workgroup to finish, the work q8_verify_record_kernel does in a
+// launch of its own (vs_spec_dev.h): each workgroup hands its query's values
+// over (vq) and takes a ticket (agent-scope release / acquire, as
+// gemv_one_finish); the last runs spec_verify_core over all of them and
+// leaves the ticket zero. run_if: stand down unless *run_if.
+template <int D, int SV = 0, bool F32 = false>
+__global__ __launch_bounds__(kSelThreads) void select_q8_kernel(
+    const f32x4_t* __restrict__ slabs, const uint32_t* __restrict__ tiles,
+    const uint32_t* __restrict__ cnt, const int* __restrict__ cmax, uint32_t nwg, uint32_t cap,
+    uint32_t k, uint64_t* __restrict__ out, uint32_t row_base, const void* __restrict__ X,
+    const void* __restrict__ qb, uint32_t dim, const f32x4_t* __restrict__ q8par,
+    const float* __restrict__ q8glob, const float* __restrict__ meta,
+    const float* __restrict__ bound, const Q8Rows r8, uint32_t two_from, uint32_t opts,
+    uint32_t* __restrict__ stats, uint64_t* __restrict__ clk, const uint32_t* __restrict__ run_if,
+    const SpecVerifyArgs va) {
+  if (run_if && *run_if == 0u) return;  // (r05) the fallback behind a verified speculative batch
+  select_q8_body<D, SV, F32>(slabs, tiles, cnt, cmax, nwg, cap, k, out, row_base, X, qb, dim, q8par,
+                             q8glob, meta, bound, r8, two_from, opts, stats, clk);
+  if (!va.vq) return;
+  __shared__ float vrq[kMfmaQueries];
+  __shared__ float vpick;
+  __shared__ int vlast;
+  __syncthreads();  // every path of the body has written this query's k keys
+  const uint32_t q = blockIdx.x, nq = gridDim.x, t = threadIdx.x;
+  if (t == 0) {
+    float r, qn;
+    bool ok;
+    const float b = va.bound[q];
+    spec_query_vals(out[(size_t)q * k + k - 1], va.q8par[4 * (size_t)q + 3], b, va.glob[2], va.dim,
+                    va.check != 0u, r, qn, ok);
+    va.vq[q] = float4{r, qn, b, ok ? 1.f : 0.f};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t prev =
+        __hip_atomic_fetch_add(va.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    vlast = prev == nq - 1;
+    if (vlast) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!vlast) return;
+  float4 v{INFINITY, 0.f, -INFINITY, 1.f};
+  if (t < nq) v = va.vq[t];
+  spec_verify_core(t < nq, v.x, v.y, v.z, v.w != 0.f, va, vrq, &vpick);
+  if (t == 0) __hip_atomic_store(va.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const uint32_t* cand_cnt,
                             const uint32_t* cand_max, uint32_t nwg, uint32_t cap, uint32_t nq,
                             uint32_t k, uint64_t* out,
@@ -3886,8 +3934,12 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
                             const float* q8par, const float* q8glob, const float* meta,
                             const float* bound, const void* X8, const void* Q8,
                             const uint64_t* allow, uint32_t n_rows, hipStream_t st, uint32_t* stats,
-                            uint64_t* clk, const uint32_t* run_if) {
+                            uint64_t* clk, const uint32_t* run_if, const SpecVerifyArgs* verify) {
   if (!select_args_ok(nwg, cap, nq, k) || !cand_max || !X8 || !Q8) return hipErrorInvalidValue;
+  if (verify && (!verify->vq || !verify->ticket || !verify->sk || !verify->stat || !verify->bound ||
+                 (verify->check && !verify->gate) || nq > kMfmaQueries))
+    return hipErrorInvalidValue;
+  const SpecVerifyArgs va = verify ? *verify : SpecVerifyArgs{};
   uint32_t gwg = 0, rpw = 0;
   mfma_grid(n_rows, &gwg, &rpw);
   if (gwg != nwg) return hipErrorInvalidValue;  // the pass's static split
@@ -3920,7 +3972,7 @@ hipError_t launch_select_q8(const float* slabs, const uint32_t* slab_tile, const
   hipLaunchKernelGGL(kern, dim3(nq), dim3(kSelThreads), 0, st, (const f32x4_t*)slabs, slab_tile,
                      cand_cnt, (const int*)cand_max, nwg, cap, k, out, row_base, X, qb, dim,
                      (const f32x4_t*)q8par, q8glob, meta, bound, r8, two_from, opts, stats, clk,
-                     run_if);
+                     run_if, va);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 #include "vs_common.h"
 #include "vs_kernels.h"
 #include "vs_qprep_dev.h"
+#include "vs_spec_dev.h"
 
 namespace vsk {
 namespace {
@@ -290,69 +291,20 @@ __global__ __launch_bounds__(256) void q8_prep_query_kernel(
 // settles on the sample path instead of paying for two passes a batch.
 // run_if: stand down unless *run_if.
 __global__ __launch_bounds__(kMfmaQueries) void q8_verify_record_kernel(
-    const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, uint32_t dim,
-    const float* __restrict__ bound, const float* __restrict__ q8par,
-    const float* __restrict__ glob, uint32_t check, uint32_t* __restrict__ gate,
-    Q8SpecK* __restrict__ sk, Q8SpecStat* __restrict__ stat, uint32_t* advice,
+    const uint64_t* __restrict__ keys, uint32_t nq, uint32_t k, SpecVerifyArgs a,
     const uint32_t* __restrict__ run_if) {
   if (run_if && *run_if == 0u) return;
   __shared__ float rq[kMfmaQueries];
   __shared__ float pick;
   const uint32_t q = threadIdx.x;
+  float r = INFINITY, qn = 0.f, b = -INFINITY;
   bool ok = true;
-  float r = INFINITY;  // this query's ratio; +inf: none (no k-th, s <= 0, zero query)
-  float qn = 0.f, b = -INFINITY;
   if (q < nq) {
-    const uint64_t key = keys[(size_t)q * k + k - 1];
-    const float s = key ? vs::key_score(key) : -INFINITY;
-    const float sig = q8par[4 * (size_t)q + 3];
-    b = bound[q];
-    ok = !check || (key != 0 && s >= b - sig * glob[2]);
-    // |q| from sigma = (4 dim + 64) 2^-24 |q| (1 + 2^-20) (vs_bound_dev.h q8_sigma)
-    qn = (float)((double)sig / ((4.0 * dim + 64.0) * 0x1p-24 * (1.0 + 0x1p-20)));
-    if (key != 0 && s > 0.f && qn > 0.f) r = s / qn;
+    b = a.bound[q];
+    spec_query_vals(keys[(size_t)q * k + k - 1], a.q8par[4 * (size_t)q + 3], b, a.glob[2], a.dim,
+                    a.check != 0u, r, qn, ok);
   }
-  rq[q] = r;
-  if (q == 0) pick = INFINITY;
-  const int nbad = __syncthreads_count(!ok);
-  const int nvalid = __syncthreads_count(r < INFINITY);
-  // the m-th smallest ratio (ties by query index), m = 1 + nvalid / 64
-  if (r < INFINITY) {
-    const int m = 1 + nvalid / 64;
-    int rank = 0;
-    for (uint32_t j = 0; j < kMfmaQueries; ++j) {
-      const float o = rq[j];
-      rank += (o < r) || (o == r && j < q);
-    }
-    if (rank == m - 1) pick = r;
-  }
-  __syncthreads();
-  const float R = 0.97f * pick;  // the ratio this batch teaches (+inf: none)
-  // (sample path) queries whose sample bound the speculative bound R |q|
-  // would fall under: each would admit more rows than its sample pass does
-  const int nloose = __syncthreads_count(!check && r < INFINITY && R * qn < b);
-  if (q != 0) return;
-  if (check) {
-    if (nbad) {
-      gate[kGateVerdict] = 1u;
-      atomicAdd(&stat->fails, 1ull);
-      // the cool-down: the host runs the next `bo` batches of this k on the
-      // sample path alone, counting them off its advice word
-      const uint32_t bo = sk->backoff;
-      sk->backoff = bo ? (2 * bo < kQ8SpecMaxBackoff ? 2 * bo : kQ8SpecMaxBackoff) : 1u;
-      if (advice && bo)
-        __hip_atomic_store(advice + kQ8SpecK, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;  // the sample path's record replaces the ratio
-    }
-    sk->backoff = 0u;
-  }
-  if (pick < INFINITY) sk->ratio = R;
-  if (!check) {
-    const uint32_t loose = pick < INFINITY && 4 * nloose > nvalid ? 1u : 0u;
-    sk->loose = loose;
-    sk->since = 0u;
-    if (advice) __hip_atomic_store(advice, loose, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  spec_verify_core(q < nq, r, qn, b, ok, a, rq, &pick);  // vs_spec_dev.h
 }
 
 // Workgroups [0, nq_bound): the sample bound of query blockIdx.x; the rest:
@@ -448,8 +400,10 @@ hipError_t launch_q8_verify_record(const uint64_t* keys, uint32_t nq, uint32_t k
                                    uint32_t* advice, hipStream_t st, const uint32_t* run_if) {
   if (nq == 0 || nq > kMfmaQueries || k == 0 || !spec_k || !stat || (check && !gate))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(q8_verify_record_kernel, dim3(1), dim3(kMfmaQueries), 0, st, keys, nq, k, dim,
-                     bound, q8par, glob, check ? 1u : 0u, gate, spec_k, stat, advice, run_if);
+  const SpecVerifyArgs a{check ? 1u : 0u, dim, bound, q8par, glob, gate, spec_k, stat, advice,
+                         nullptr, nullptr};
+  hipLaunchKernelGGL(q8_verify_record_kernel, dim3(1), dim3(kMfmaQueries), 0, st, keys, nq, k, a,
+                     run_if);
   return hipGetLastError();
 }
 
