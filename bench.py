@@ -83,8 +83,11 @@ METRIC_NAME = "exact top-10 QPS on 10M×768 corpus at 1/2/4/8 GPUs; % of HBM/MFM
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults: 50 / 10 for batched configs; 400 / 50 for one-query configs,
+    # whose ~0.15 ms steps would otherwise time 7 ms, inside the clock's ramp
+    # (r06: C2 at 50 steps 6.36k QPS, at 400 7.0k on the same build)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -95,7 +98,13 @@ def parse():
                     help="time budget of each CPU baseline leg (per-query scan, batched BLAS)")
     ap.add_argument("--dump-keys", default="",
                     help="rank 0 writes the last step's merged keys here (.npy; parity tests)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    one = CONFIGS[a.config][4] == 1
+    if a.steps is None:
+        a.steps = 400 if one else 50
+    if a.warmup is None:
+        a.warmup = 50 if one else 10
+    return a
 
 
 def log(*a):

@@ -302,6 +302,7 @@ struct DevEngine {
   uint64_t scan_n = 0, merge_n = 0;
   uint64_t scan_tick = 0;   // scan launches seen (VS_FLAG_TIMING_SAMPLE)
   bool scan_skip = false;   // the current scan launch is not bracketed
+  uint32_t scan_period = 4; // VS_FLAG_TIMING_SAMPLE brackets one scan in this many
 };
 
 // ---- per-device operations (vs_engine.cpp); same contracts as the C-ABI

@@ -84,9 +84,10 @@ typedef struct vs_config {
  * few microseconds of device idle between launches, so the benchmark times
  * scans only. */
 #define VS_FLAG_TIMING_MERGE 2u
-/* With VS_FLAG_TIMING: bracket only every 16th scan launch, starting with the
- * first after a vs_timing reset (a sampled average that keeps the event gaps
- * out of 15 of 16 steps; every 4th cost a single-query step 1.5%). */
+/* With VS_FLAG_TIMING: bracket only one scan launch in 4 (batches) or in 16
+ * (one query: every 4th cost a single-query step 1.5%), the 4th / 16th after a
+ * vs_timing reset first: a sampled average that keeps the event gaps out of
+ * the other steps and the first scan after a synchronize out of the sample. */
 #define VS_FLAG_TIMING_SAMPLE 4u
 /* vs_open_multi only: place every collection WHOLE on one of the engine's
  * devices (the one with the fewest bytes reserved by capacity hints, then

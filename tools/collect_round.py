@@ -89,12 +89,14 @@ def main():
           f"{statistics.mean(dur[10:]):.4f} ms over {len(dur) - 10} ({nstand} stood down)")
     pmc_mfma(tag, bid, kname)
     fetch = []
-    for cfg in ("c3", "c3b1"):
+    for cfg in ("c3", "c3b1", "c3_s125"):
         f = os.path.join(G, f"{tag}_pmc_fetch_{cfg}", "run_counter_collection.csv")
         if os.path.exists(f):
             dst = os.path.join(P, f"{tag}_{cfg}_{bid}_pmc_fetch.csv")
             shutil.copy(f, dst)
-            if cfg == "c3":
+            if cfg == "c3_s125":  # (r05) the int8 pass at the N = 8 share
+                key = "c3_i8@1250000"
+            elif cfg == "c3":
                 key = cfg + ("_i8" if "true" in kname else "")
             else:  # (r05) B = 1 runs the int8 copy's scan when the collection keeps one
                 key = cfg + ("_i8" if "gemv_q8_scan" in open(f).read() else "")
@@ -103,9 +105,20 @@ def main():
         import subprocess
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
                         f"{tag} build {bid}", *fetch], check=True)
+    # (r06) tools/r06_close2.sh's records too, when present
     for src, dst in ((f"{tag}_c1_http.jsonl", f"{tag}_c1_http_both_backends.jsonl"),
                      (f"{tag}_rt_floor.json", f"{tag}_c1_rt_floor.json"),
-                     (f"{tag}_concurrency_overlap.json", f"{tag}_concurrency_overlap.json")):
+                     (f"{tag}_concurrency_overlap.json", f"{tag}_concurrency_overlap.json"),
+                     (f"{tag}_shares.jsonl", f"{tag}_c3_shares_{bid[:8]}.jsonl"),
+                     (f"{tag}_specab_10m_0.jsonl", f"{tag}_specab_10m_0.jsonl"),
+                     (f"{tag}_specab_10m_1.jsonl", f"{tag}_specab_10m_1.jsonl"),
+                     (f"{tag}_specab_s125_0.jsonl", f"{tag}_specab_s125_0.jsonl"),
+                     (f"{tag}_specab_s125_1.jsonl", f"{tag}_specab_s125_1.jsonl"),
+                     (f"{tag}_s125_exchange.json", f"{tag}_s125_exchange_bench.json"),
+                     (f"{tag}_c4share.json", f"{tag}_c4share_bench.json"),
+                     (f"{tag}_c5_loadgen.jsonl", f"{tag}_c5_loadgen_both.jsonl"),
+                     (f"{tag}_pipe_s125.json", f"{tag}_share_pipe_s125.json"),
+                     (f"{tag}_pipe_10m.json", f"{tag}_share_pipe_10m.json")):
         if os.path.exists(os.path.join(G, src)):
             shutil.copy(os.path.join(G, src), os.path.join(P, dst))
     for fn in sorted(os.listdir(G)):
