@@ -214,6 +214,10 @@ def scan_roofline(config, rows_local, dim, dtype, batch, k, scan_ms, int8, q8_b1
     HBM bytes of a launch over exactly that share (null when none was
     measured at that size)."""
     elem = 2 if dtype == "bf16" else 4
+    if not scan_ms > 0:  # no scan launch was bracketed (never with the sampling rule above)
+        return {"bound": "hbm" if (int8 or q8_b1 or batch == 1) else "mfma", "achieved": None,
+                "peak": None, "unit": None, "frac": None, "traffic": None, "traffic_rows": None,
+                "note": "no scan launch was timed"}
     if q8_b1:  # one query on the int8 copy
         roof = q8_gemv_roofline(rows_local, dim, k, scan_ms)
         roof["traffic"] = pmc_traffic(config + "_i8", rows_local)
@@ -461,7 +465,11 @@ def main():
     if args.rows:
         desc += " (--rows override of the config's corpus size)"
     lo, hi = shard.shard_range(n_full, world, rank)
-    eng = pkg.VectorEngine(device=local, timing=True, timing_sample=True)
+    # the scans' event pairs: one launch in 4 (batches) / 16 (one query), the
+    # 4th / 16th first (vsearch.h VS_FLAG_TIMING_SAMPLE); a run of fewer than
+    # 16 timed steps brackets every scan, so it still times some
+    sample = args.steps >= 16
+    eng = pkg.VectorEngine(device=local, timing=True, timing_sample=sample)
     coll = "bench"
     eng.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else pkg.METRIC_COSINE,
                           pkg.DTYPE_BF16 if dtype == "bf16" else pkg.DTYPE_F32, hi - lo, lo)
@@ -586,7 +594,7 @@ def main():
     # second engine without the int8 copy over the same generated rows
     if int8 and world == 1 and not dist_on and not args.no_secondary:
         eng.drop_collection(coll)  # room for the second corpus
-        e2 = pkg.VectorEngine(device=local, timing=True, timing_sample=True, prefilter=False)
+        e2 = pkg.VectorEngine(device=local, timing=True, timing_sample=sample, prefilter=False)
         try:
             e2.create_collection(coll, dim, pkg.METRIC_DOT if metric == "dot" else
                                  pkg.METRIC_COSINE,
