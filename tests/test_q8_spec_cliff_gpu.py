@@ -187,8 +187,13 @@ def test_outlier_queries_do_not_poison_later_batches(kind):
     b = r["batches"]
     # the engines' relative speed on identical (sample-path) work: every ratio
     # below is taken relative to it
+    # (the low end, not the median: the first run of each k on each engine
+    # grows its scratch -- a synchronize and an allocation -- which both
+    # speculating engines' only run pays and the stateless engine's second run
+    # does not, so that term only ever inflates a calibration ratio; r06h:
+    # 3 of 9 read 1.07-1.34 beside 1.004-1.039)
     cal = sorted(x["on_ms"] / x["off_ms"] for x in b if x["phase"] == "calib")
-    r0 = cal[len(cal) // 2]
+    r0 = cal[1]
     assert 0.9 <= r0 <= 1.1, cal
     after = [x for x in b if x["phase"] == "after"]
     # single-batch times jitter by ~1-2% on the same work, so each ratio is
